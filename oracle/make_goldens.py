@@ -1,0 +1,285 @@
+"""Generate tests/golden/*.npz by running the READ-ONLY reference on CPU in float64.
+
+TEST INFRASTRUCTURE. Run in the build container only:
+    PYTHONDONTWRITEBYTECODE=1 python oracle/make_goldens.py
+It imports /root/reference through oracle/ref_shims (mmcv/mmengine restatements),
+loads deterministic weights from oracle/gen.py, and stores forward outputs and
+upstream-grad-seeded backward results. Nothing from the reference is copied: the
+.npz files hold only arrays (inputs are regenerated from the seeds in gen.py).
+
+Routing around HEAD's crashes: the backbone's `(outs, None)` tuple is
+indexed with [0] before the decode head, and the loss of builder.py:230 is applied
+by hand.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import gen  # noqa: E402
+import ref_import  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+torch.set_default_dtype(torch.float64)
+dformer, ham, mlpdec, builder, droppath = ref_import.import_ref()
+
+BN = dict(type="BN", requires_grad=True)
+MODELS = {  # DFormer.py:460-497
+    "tiny": dict(dims=[32, 64, 128, 256], heads=[1, 2, 4, 8], ratios=[8, 8, 4, 4], depths=[3, 3, 5, 2]),
+    "base": dict(dims=[64, 128, 256, 512], heads=[1, 2, 4, 8], ratios=[8, 8, 4, 4], depths=[3, 3, 12, 2]),
+    "large": dict(dims=[96, 192, 288, 576], heads=[1, 2, 4, 8], ratios=[8, 8, 4, 4], depths=[3, 3, 12, 2]),
+}
+
+
+def load_weights(mod, seed=1234):
+    sd = mod.state_dict()
+    vals = gen.state_dict_values([(k, v.shape) for k, v in sd.items()], seed)
+    mod.load_state_dict({k: torch.from_numpy(np.asarray(v)).to(sd[k].dtype) for k, v in vals.items()})
+
+
+def t(a, grad=True):
+    x = torch.from_numpy(np.asarray(a, dtype=np.float64)).clone()
+    return x.requires_grad_(grad)
+
+
+def param_grads(mod, prefix="grad/", big=65536):
+    """Full grads for small tensors; 256-sample fingerprints ("gradfp/") for large ones."""
+    out = {}
+    for n, p in mod.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().numpy()
+        if g.size > big:
+            out["gradfp/" + n] = gen.fingerprint(g, 256)
+        else:
+            out[prefix + n] = g.astype(np.float32)
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + ".npz")
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"  wrote {name}.npz ({os.path.getsize(path) / 1e6:.2f} MB)")
+
+
+def make_block(model, stage, last=False, drop_prob=0.0):
+    m = MODELS[model]
+    C = m["dims"][stage]
+    depth = m["depths"][stage]
+    j = depth - 1 if last else 0
+    return dformer.Block(index=0, dim=C, num_head=m["heads"][stage], norm_cfg=BN,
+                         mlp_ratio=m["ratios"][stage], block_index=depth - j, last_block_index=50,
+                         window=0 if stage == 0 else 7,
+                         dropout_layer=dict(type="DropPath", drop_prob=drop_prob),
+                         drop_depth=(stage == 3 and last))
+
+
+def golden_block(name, model, stage, B, H, W, last=False, drop_prob=0.0, masks=None):
+    C = MODELS[model]["dims"][stage]
+    blk = make_block(model, stage, last, drop_prob)
+    load_weights(blk)
+    blk.train()
+    x = t(gen.normal(name + "/x", (B, H, W, C)))
+    xe = t(gen.normal(name + "/xe", (B, H, W, C // 2)))
+    if masks is not None:
+        droppath.INJECTED_MASKS = [torch.tensor(mk, dtype=torch.float64) for mk in masks]
+    y, ye = blk(x, xe)
+    droppath.INJECTED_MASKS = None
+    gy = gen.normal(name + "/gy", y.shape)
+    loss = (y * t(gy, False)).sum()
+    extra = {}
+    if not last:
+        gye = gen.normal(name + "/gye", ye.shape)
+        loss = loss + (ye * t(gye, False)).sum()
+        extra["y_e"] = ye.detach().numpy().astype(np.float32)
+    loss.backward()
+    save(name, y=y.detach().numpy().astype(np.float32), gx=x.grad.numpy().astype(np.float32),
+         gxe=x.grad.new_zeros(0).numpy() if xe.grad is None else xe.grad.numpy().astype(np.float32),
+         meta=np.array([B, H, W, C, stage, int(last), drop_prob * 1e6]), **extra, **param_grads(blk))
+
+
+def golden_nmf(name, B, C, H, W, train=True):
+    nmf = ham.NMF2D(dict(device="cpu"))
+    nmf.train(train)
+    bases = gen.nmf_bases(B, C, 64, name=name + "/bases")
+    nmf._build_bases = lambda B_, S, D, R, cuda=False: torch.from_numpy(bases.copy())
+    x = t(gen.uniform(name + "/x", (B, C, H, W)))
+    y = nmf(x)
+    gy = gen.normal(name + "/gy", y.shape)
+    (y * t(gy, False)).sum().backward()
+    save(name, y=y.detach().numpy().astype(np.float32), gx=x.grad.numpy().astype(np.float32),
+         meta=np.array([B, C, H, W, int(train)]))
+
+
+def golden_ham(name, in_ch, B, H, W, ncls=40, train=True):
+    head = ham.LightHamHead(in_channels=in_ch, num_classes=ncls, in_index=[1, 2, 3], norm_cfg=BN,
+                            channels=512, device="cpu")
+    for mdl in head.modules():  # init_func.py:11-15 applies bn_eps / momentum to the decoder
+        if isinstance(mdl, nn.BatchNorm2d):
+            mdl.eps, mdl.momentum = 1e-3, 0.1
+    head.dropout = None  # value golden: Dropout2d removed (p=0)
+    load_weights(head)
+    head.train(train)
+    bases = gen.nmf_bases(B, 512, 64, name=name + "/bases")
+    head.hamburger.ham._build_bases = lambda B_, S, D, R, cuda=False: torch.from_numpy(bases.copy())
+    feats = [t(gen.normal(name + f"/f{i}", (B, c, H >> i, W >> i))) for i, c in enumerate(in_ch)]
+    inputs = [None] + feats
+    y = head(inputs)
+    gy = gen.normal(name + "/gy", y.shape)
+    (y * t(gy, False)).sum().backward()
+    extra = {}
+    for n, b in head.named_buffers():
+        if "running" in n:
+            extra["buf/" + n] = b.numpy().astype(np.float32)
+    save(name, y=y.detach().numpy().astype(np.float32),
+         **{f"gf{i + 1}": f.grad.numpy().astype(np.float32) for i, f in enumerate(feats)},
+         meta=np.array([B, H, W, ncls, int(train)] + list(in_ch)), **param_grads(head), **extra)
+
+
+def golden_mlpdec(name, in_ch, B, H, W, embed, ncls=40):
+    head = mlpdec.DecoderHead(in_channels=in_ch, num_classes=ncls, norm_layer=nn.BatchNorm2d,
+                              embed_dim=embed)
+    for mdl in head.modules():
+        if isinstance(mdl, nn.BatchNorm2d):
+            mdl.eps, mdl.momentum = 1e-3, 0.1
+    head.dropout = nn.Identity()
+    load_weights(head)
+    head.train()
+    sizes = [(H, W)]
+    for _ in range(3):
+        h, w = sizes[-1]
+        sizes.append(((h - 1) // 2 + 1, (w - 1) // 2 + 1))
+    feats = [t(gen.normal(name + f"/f{i}", (B, c, *sizes[i]))) for i, c in enumerate(in_ch)]
+    y = head(feats)
+    gy = gen.normal(name + "/gy", y.shape)
+    (y * t(gy, False)).sum().backward()
+    save(name, y=y.detach().numpy().astype(np.float32),
+         **{f"gf{i}": f.grad.numpy().astype(np.float32) for i, f in enumerate(feats)},
+         meta=np.array([B, H, W, ncls, embed] + list(in_ch)), **param_grads(head))
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def build_segmentor(backbone, decoder="ham", ncls=40, embed=512):
+    cfg = Cfg(backbone=backbone, decoder=decoder, decoder_embed_dim=embed, num_classes=ncls,
+              drop_path_rate=0.0, aux_rate=0, device="cpu", pretrained_model=None, bn_eps=1e-3,
+              bn_momentum=0.1, background=255)
+    crit = nn.CrossEntropyLoss(reduction="none", ignore_index=255)
+    model = builder.EncoderDecoder(cfg=cfg, criterion=crit, norm_layer=nn.BatchNorm2d, syncbn=False)
+    if decoder == "ham":
+        model.decode_head.dropout = None
+    else:
+        model.decode_head.dropout = nn.Identity()
+    load_weights(model)
+    return model, cfg
+
+
+def e2e_forward(model, rgb, dep, bases=None):
+    """encode_decode of builder.py:193-208 with the HEAD tuple bug routed around."""
+    if bases is not None:
+        model.decode_head.hamburger.ham._build_bases = \
+            lambda B_, S, D, R, cuda=False: torch.from_numpy(bases.copy())
+    feats = model.encoder_backbone(rgb, dep)[0]
+    low = model.decode_head.forward(feats)
+    out = F.interpolate(low, size=rgb.shape[-2:], mode="bilinear", align_corners=False)
+    return feats, low, out
+
+
+def golden_e2e(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, backward=True):
+    t0 = time.time()
+    model, cfg = build_segmentor(backbone, decoder, ncls, embed)
+    model.train()
+    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb, dep = t(rgb_np, backward), t(dep_np, backward)
+    lab = torch.from_numpy(gen.labels(B, H, W, ncls))
+    bases = gen.nmf_bases(B, 512, 64, name=name + "/bases") if decoder == "ham" else None
+    if not backward:
+        with torch.no_grad():
+            feats, low, out = e2e_forward(model, rgb, dep, bases)
+        save(name, low_fp=gen.fingerprint(low.numpy()), out_fp=gen.fingerprint(out.numpy()),
+             **{f"feat{i}_fp": gen.fingerprint(f.numpy()) for i, f in enumerate(feats)},
+             meta=np.array([B, H, W, ncls]))
+        print(f"  {name}: {time.time() - t0:.1f}s")
+        return
+    feats, low, out = e2e_forward(model, rgb, dep, bases)
+    loss = model.criterion(out, lab.long())[lab.long() != cfg.background].mean()  # builder.py:230
+    loss.backward()
+    gfp = {"gfp/" + n: gen.fingerprint(p.grad.numpy(), 16) for n, p in model.named_parameters()
+           if p.grad is not None}
+    save(name, low=low.detach().numpy().astype(np.float32), loss=np.array(loss.item()),
+         grgb_fp=gen.fingerprint(rgb.grad.numpy()), gdep_fp=gen.fingerprint(dep.grad.numpy()),
+         **{f"feat{i}": f.detach().numpy().astype(np.float32) for i, f in enumerate(feats)},
+         meta=np.array([B, H, W, ncls]), **gfp)
+    print(f"  {name}: {time.time() - t0:.1f}s")
+
+
+def golden_groups():
+    """Optimizer-group membership of group_weight (init_func.py:26-70) for Base + ham."""
+    from utils.init_func import group_weight
+    model, _ = build_segmentor("DFormer-Base")
+    groups = group_weight([], model, nn.BatchNorm2d, 6e-5)
+    ids = {id(p): n for n, p in model.named_parameters()}
+    decay = sorted(ids[id(p)] for p in groups[0]["params"])
+    nodecay = sorted(ids[id(p)] for p in groups[1]["params"])
+    excluded = sorted(set(ids.values()) - set(decay) - set(nodecay))
+    save("groups_base", decay=np.array(decay), nodecay=np.array(nodecay), excluded=np.array(excluded),
+         counts=np.array([sum(p.numel() for n, p in model.named_parameters() if n in excluded),
+                          sum(p.numel() for p in model.parameters())]))
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:]
+
+    def want(n):
+        return not which or any(n.startswith(w) for w in which)
+
+    torch.manual_seed(0)
+    blocks = [
+        ("block_tiny_s0", "tiny", 0, 2, 12, 16, False),
+        ("block_tiny_s1", "tiny", 1, 2, 11, 13, False),
+        ("block_tiny_s3_last", "tiny", 3, 2, 5, 7, True),
+        ("block_base_s0", "base", 0, 1, 16, 20, False),
+        ("block_base_s1", "base", 1, 2, 15, 20, False),
+        ("block_base_s2", "base", 2, 2, 9, 10, False),
+        ("block_base_s3", "base", 3, 2, 8, 10, False),
+        ("block_base_s3_last", "base", 3, 2, 8, 10, True),
+        ("block_large_s1", "large", 1, 1, 9, 11, False),
+        ("block_large_s2", "large", 2, 1, 8, 9, False),
+    ]
+    for n, mdl, st, B, H, W, last in blocks:
+        if want(n):
+            golden_block(n, mdl, st, B, H, W, last)
+    if want("block_droppath"):
+        # DropPath with injected keep masks: 6 DropPath calls per block (x/xe × attn/mlp … order of Block.forward)
+        masks = [np.array([1.0, 0.0]), np.array([0.0, 1.0]), np.array([1.0, 1.0]), np.array([0.0, 1.0])]
+        golden_block("block_droppath_base_s1", "base", 1, 2, 9, 11, False, drop_prob=0.25, masks=masks)
+    if want("nmf"):
+        golden_nmf("nmf_train", 2, 64, 8, 10, True)
+        golden_nmf("nmf_eval", 1, 64, 7, 9, False)
+    if want("ham"):
+        golden_ham("ham_tiny", [64, 128, 256], 2, 12, 16)
+    if want("mlpdec"):
+        golden_mlpdec("mlpdec_small", [32, 64, 128, 256], 2, 16, 20, embed=64)
+    if want("e2e_tiny_small"):
+        golden_e2e("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
+    if want("e2e_base_small"):
+        golden_e2e("e2e_base_small", "DFormer-Base", 2, 64, 80)
+    if want("e2e_large_mlp"):
+        golden_e2e("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37)
+    if want("e2e_tiny_full"):
+        golden_e2e("e2e_tiny_full_fwd", "DFormer-Tiny", 2, 480, 640, backward=False)
+    if want("groups"):
+        golden_groups()
+
+
+if __name__ == "__main__":
+    main()
