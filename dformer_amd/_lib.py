@@ -1,0 +1,119 @@
+"""ctypes binding of libdformer_hip.so (the C ABI declared in include/dformer_hip.h).
+
+This is the only place Python touches the native library. Every wrapper takes torch tensors
+that already live on the GPU, passes raw pointers + sizes + the current HIP stream, and
+raises RuntimeError with the library's message on a non-zero status. There is no CPU
+fallback: if the library is missing the import fails loudly.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdformer_hip.so")
+
+F32, BF16 = 0, 1
+
+c_int, c_long, c_float, c_double, c_void_p, c_size_t = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
+                                                         ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t)
+P = c_void_p
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [("M", c_int), ("N", c_int), ("K", c_int), ("batch", c_int),
+                ("a_kcontig", c_int), ("b_kcontig", c_int),
+                ("lda", c_long), ("ldb", c_long), ("ldc", c_long),
+                ("stride_a", c_long), ("stride_b", c_long), ("stride_c", c_long),
+                ("alpha", c_float), ("beta", c_float), ("c_f32", c_int),
+                ("bias", P), ("act", c_int), ("preact", P), ("ldpre", c_long),
+                ("mul", P), ("ldmul", c_long), ("res", P), ("ldres", c_long),
+                ("colscale", P), ("rowscale", P), ("rows_per_scale", c_long), ("split_k", c_int),
+                ("act_col0", c_int)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "dfm_last_error": (ctypes.c_char_p, []),
+    "dfm_abi_version": (c_int, []),
+    "dfm_gemm_workspace_size": (c_size_t, [ctypes.POINTER(GemmDesc)]),
+    "dfm_gemm": (c_int, [c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
+    "dfm_layernorm_fwd": (c_int, [c_int, c_long, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P]),
+    "dfm_layernorm_bwd_workspace": (c_size_t, [c_long, c_int]),
+    "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, c_int, P, P, P,
+                                  P]),
+    "dfm_dwconv_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, c_int, P, c_long, P, c_long,
+                               P]),
+    "dfm_dwconv_bwd_data": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_int, P, c_long,
+                                    c_int, P]),
+    "dfm_dwconv_bwd_weight_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "dfm_dwconv_bwd_weight": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P]),
+    "dfm_colsum_workspace": (c_size_t, [c_long, c_int]),
+    "dfm_colsum": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_int, P, P]),
+    "dfm_cast": (c_int, [c_int, c_int, c_long, P, P, P]),
+    "dfm_gelu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, c_int, P]),
+    "dfm_scale_mul": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, c_float, P, c_long, c_int,
+                              P]),
+    "dfm_adaptive_pool7_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P]),
+    "dfm_adaptive_pool7_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_int, P]),
+    "dfm_bilinear_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_int, P]),
+    "dfm_bilinear_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_int, P]),
+    "dfm_pooled_attn_workspace": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "dfm_pooled_attn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, c_long, c_float, P, c_long,
+                                    P, P, P]),
+    "dfm_pooled_attn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, c_long, c_float, P, c_long,
+                                    P, c_long, P, P, P, P, c_long, P, P]),
+    "dfm_bn_workspace": (c_size_t, [c_long, c_int]),
+    "dfm_bn_stats": (c_int, [c_int, c_long, c_int, P, c_long, P, P, P]),
+    "dfm_bn_finalize": (c_int, [c_int, P, c_double, c_float, c_float, P, P, P, P, P]),
+    "dfm_bn_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, P, P, P, P, c_long, c_int, P, c_long, P]),
+    "dfm_bn_bwd_stats": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, P]),
+    "dfm_bn_bwd_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_double, P, c_long, c_int,
+                                 P]),
+    "dfm_relu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P]),
+    "dfm_nmf_update": (c_int, [c_long, P, P, P, c_float, P, P]),
+    "dfm_nmf_update_bwd": (c_int, [c_long, P, P, P, P, P, c_float, P, c_int, P, P, P]),
+    "dfm_softmax_rows": (c_int, [c_long, c_int, P, P, P]),
+    "dfm_softmax_rows_bwd": (c_int, [c_long, c_int, P, P, P, c_int, P]),
+    "dfm_seg_loss_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "dfm_seg_loss_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P]),
+    "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P]),
+    "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, P]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"dformer_amd: native library missing at {LIB_PATH}; run "
+                          f"`python -c 'import __graft_entry__ as g; g.build()'` (make -C dformer_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+SYMBOLS = tuple(_SIGS)
+
+
+def check(status, what):
+    if status != 0:
+        raise RuntimeError(f"{what} failed ({status}): {lib.dfm_last_error().decode()}")
+
+
+def dtype_code(t):
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"dformer_amd: unsupported dtype {t.dtype}")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,396 @@
+// Bandwidth-bound helpers: column reductions (bias / layer-scale grads, BatchNorm statistics),
+// activation backward, residual chain rule, dtype casts, NMF multiplicative updates and AdamW.
+// All reductions are two-stage with fixed order (deterministic, no float atomics).
+#include "common.h"
+
+namespace {
+constexpr int COLS = 64;       // columns per block in column reductions
+constexpr int RED_BLOCKS = 512;
+
+// part[blk][k][c] for k < NOUT: sum over this block's rows of f_k(row, c)
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void colred_kernel(long rows, int C, const T* __restrict__ x, long ldx,
+                                                     const T* __restrict__ y, long ldy, const float* __restrict__ p0,
+                                                     const float* __restrict__ p1, long rps, float* __restrict__ part,
+                                                     int nblk) {
+  // MODE 0: sum x * (y?) * rowscale(p1?)           -> 1 output
+  // MODE 1: BN stats: sum x, sum x^2               -> 2 outputs
+  // MODE 2: BN bwd:  sum y, sum y * (x - p0[c]) * p1[c]   -> 2 outputs (y = dy, p0 mean, p1 rstd)
+  constexpr int NOUT = MODE == 0 ? 1 : 2;
+  const int cl = threadIdx.x % COLS, rl = threadIdx.x / COLS;  // 4 row lanes
+  const int c = blockIdx.y * COLS + cl;
+  const long per = (rows + nblk - 1) / nblk;
+  const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    for (long r = r0 + rl; r < r1; r += 4) {
+      const float xv = ldf(x + r * ldx + c);
+      if (MODE == 0) {
+        float v = xv;
+        if (y) v *= ldf(y + r * ldy + c);
+        if (p1) v *= p1[r / rps];
+        s0 += v;
+      } else if (MODE == 1) {
+        s0 += xv;
+        s1 += xv * xv;
+      } else {
+        const float g = ldf(y + r * ldy + c);
+        s0 += g;
+        s1 += g * (xv - p0[c]) * p1[c];
+      }
+    }
+  }
+  __shared__ float red[NOUT][4][COLS];
+  red[0][rl][cl] = s0;
+  if (NOUT == 2) red[NOUT - 1][rl][cl] = s1;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    part[((long)blockIdx.x * NOUT + 0) * C + c] = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+    if (NOUT == 2)
+      part[((long)blockIdx.x * NOUT + 1) * C + c] =
+          red[NOUT - 1][0][cl] + red[NOUT - 1][1][cl] + red[NOUT - 1][2][cl] + red[NOUT - 1][3][cl];
+  }
+}
+
+__global__ void colred_sum_kernel(int nblk, int n, const float* __restrict__ part, float* __restrict__ out,
+                                  int accumulate) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * n + e];
+  out[e] = accumulate ? out[e] + s : s;
+}
+
+int red_blocks(long rows) { return (int)min((long)RED_BLOCKS, max(1L, (rows + 255) / 256)); }
+
+template <typename T, int MODE>
+int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, const float* p0, const float* p1,
+           long rps, float* out, int accumulate, void* ws, hipStream_t s) {
+  constexpr int NOUT = MODE == 0 ? 1 : 2;
+  const int nblk = red_blocks(rows);
+  hipLaunchKernelGGL((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x, ldx,
+                     (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
+  DFM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colred_sum_kernel, dim3(cdiv(NOUT * C, 256)), dim3(256), 0, s, nblk, NOUT * C, (const float*)ws,
+                     out, accumulate);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+// ---- elementwise over [rows, C] with strides
+template <typename T, int OP>
+__global__ void ew2d_kernel(long rows, int C, const T* __restrict__ a, long lda, const T* __restrict__ b, long ldb,
+                            const float* __restrict__ colscale, const float* __restrict__ rowscale, long rps,
+                            float alpha, T* __restrict__ d, long ldd, int accumulate) {
+  const long n = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = i % C;
+    const float av = ldf(a + r * lda + c);
+    float v;
+    if (OP == 0) {  // scale_mul
+      v = alpha * av;
+      if (b) v *= ldf(b + r * ldb + c);
+      if (colscale) v *= colscale[c];
+      if (rowscale) v *= rowscale[r / rps];
+    } else if (OP == 1) {  // gelu bwd: a = dy, b = pre
+      v = av * gelu_grad_f(ldf(b + r * ldb + c));
+    } else {  // relu bwd: a = dy, b = relu output
+      v = ldf(b + r * ldb + c) > 0.f ? av : 0.f;
+    }
+    T* dp = d + r * ldd + c;
+    if (accumulate) v += ldf(dp);
+    stf(dp, v);
+  }
+}
+
+unsigned ew_grid(long n) { return (unsigned)min((long)8192, max(1L, (n + 255) / 256)); }
+
+template <int OP>
+int ew2d(int dtype, long rows, int C, const void* a, long lda, const void* b, long ldb, const float* cs,
+         const float* rs, long rps, float alpha, void* d, long ldd, int acc, hipStream_t s) {
+  if (rows * C == 0) return DFM_OK;
+  const unsigned g = ew_grid(rows * C);
+  if (dtype == DFM_BF16)
+    hipLaunchKernelGGL((ew2d_kernel<bf16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
+                       (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
+  else if (dtype == DFM_F32)
+    hipLaunchKernelGGL((ew2d_kernel<float, OP>), dim3(g), dim3(256), 0, s, rows, C, (const float*)a, lda,
+                       (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
+  else {
+    dfm_set_error("elementwise: bad dtype");
+    return DFM_ERR_DTYPE;
+  }
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(long n, const TI* __restrict__ x, TO* __restrict__ y) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    stf(y + i, ldf(x + i));
+}
+
+// ---- BatchNorm
+__global__ void bn_finalize_kernel(int C, const float* __restrict__ st, double count, float eps, float mom,
+                                   float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rm,
+                                   float* __restrict__ rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mu = st[c] / count;
+  double var = st[C + c] / count - mu * mu;
+  if (var < 0) var = 0;
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + eps));
+  if (rm) rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
+  if (rv) rv[c] = (1.f - mom) * rv[c] + mom * (float)(var * count / max(count - 1.0, 1.0));
+}
+
+template <typename T>
+__global__ void bn_apply_kernel(long rows, int C, const T* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, const T* __restrict__ res, long ldres, int act,
+                                T* __restrict__ y, long ldy) {
+  const long n = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = i % C;
+    float v = (ldf(x + r * ldx + c) - mean[c]) * rstd[c] * gamma[c] + beta[c];
+    if (res) v += ldf(res + r * ldres + c);
+    if (act == 2) v = fmaxf(v, 0.f);
+    stf(y + r * ldy + c, v);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(long rows, int C, const T* __restrict__ x, long ldx, const T* __restrict__ dy,
+                                    long lddy, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ gamma, const float* __restrict__ st, float inv_n,
+                                    T* __restrict__ dx, long lddx, int accumulate) {
+  const long n = rows * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / C;
+    const int c = i % C;
+    const float xh = (ldf(x + r * ldx + c) - mean[c]) * rstd[c];
+    float v = gamma[c] * rstd[c] * (ldf(dy + r * lddy + c) - st[c] * inv_n - xh * st[C + c] * inv_n);
+    T* dp = dx + r * lddx + c;
+    if (accumulate) v += ldf(dp);
+    stf(dp, v);
+  }
+}
+
+// ---- NMF multiplicative update
+__global__ void nmf_update_kernel(long n, const float* __restrict__ a, const float* __restrict__ num,
+                                  const float* __restrict__ den, float eps, float* __restrict__ out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = a[i] * num[i] / (den[i] + eps);
+}
+__global__ void nmf_update_bwd_kernel(long n, const float* __restrict__ g, const float* __restrict__ a,
+                                      const float* __restrict__ num, const float* __restrict__ den,
+                                      const float* __restrict__ out, float eps, float* __restrict__ ga, int acc,
+                                      float* __restrict__ gnum, float* __restrict__ gden) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float r = 1.f / (den[i] + eps);
+    const float gi = g[i];
+    const float v = gi * num[i] * r;
+    ga[i] = acc ? ga[i] + v : v;
+    gnum[i] = gi * a[i] * r;
+    gden[i] = -gi * out[i] * r;
+  }
+}
+
+// ---- row softmax (one wave per row)
+__global__ void softmax_rows_kernel(long rows, int R, const float* __restrict__ x, float* __restrict__ y) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* xr = x + row * R;
+  float m = -INFINITY;
+  for (int c = lane; c < R; c += 64) m = fmaxf(m, xr[c]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < R; c += 64) s += __expf(xr[c] - m);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int c = lane; c < R; c += 64) y[row * R + c] = __expf(xr[c] - m) * inv;
+}
+__global__ void softmax_rows_bwd_kernel(long rows, int R, const float* __restrict__ y, const float* __restrict__ dy,
+                                        float* __restrict__ dx, int acc) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float d = 0.f;
+  for (int c = lane; c < R; c += 64) d += y[row * R + c] * dy[row * R + c];
+  d = wave_sum(d);
+  for (int c = lane; c < R; c += 64) {
+    const float v = y[row * R + c] * (dy[row * R + c] - d);
+    dx[row * R + c] = acc ? dx[row * R + c] + v : v;
+  }
+}
+
+// ---- AdamW (torch.optim.AdamW semantics, decoupled weight decay)
+__global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, float lr, float b1, float b2, float eps, float wd, float bc1,
+                             float bc2_sqrt, float gscale, bf16_t* __restrict__ copy) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+    if (copy) copy[i] = f2bf(pi);
+  }
+}
+}  // namespace
+
+// ================================================================ C ABI
+extern "C" size_t dfm_colsum_workspace(long rows, int C) { return (size_t)red_blocks(rows) * 2 * C * sizeof(float); }
+extern "C" size_t dfm_bn_workspace(long rows, int C) { return dfm_colsum_workspace(rows, C); }
+
+extern "C" int dfm_colsum(int dtype, long rows, int C, const void* x, long ldx, const void* mul, long ldmul,
+                          const float* rowscale, long rps, float* out, int accumulate, void* ws, dfm_stream_t stream) {
+  DFM_CHECK_ARG(x && out && ws && C > 0, "dfm_colsum: bad argument");
+  if (rows == 0) return DFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFM_BF16) return colred<bf16_t, 0>(rows, C, x, ldx, mul, ldmul, nullptr, rowscale, rps, out, accumulate, ws, s);
+  if (dtype == DFM_F32) return colred<float, 0>(rows, C, x, ldx, mul, ldmul, nullptr, rowscale, rps, out, accumulate, ws, s);
+  dfm_set_error("dfm_colsum: bad dtype");
+  return DFM_ERR_DTYPE;
+}
+
+extern "C" int dfm_cast(int din, int dout, long n, const void* x, void* y, dfm_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return DFM_OK;
+  const unsigned g = ew_grid(n);
+  if (din == DFM_F32 && dout == DFM_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(g), dim3(256), 0, s, n, (const float*)x, (bf16_t*)y);
+  else if (din == DFM_BF16 && dout == DFM_F32) hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (float*)y);
+  else if (din == DFM_F32 && dout == DFM_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, n, (const float*)x, (float*)y);
+  else if (din == DFM_BF16 && dout == DFM_BF16) hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (bf16_t*)y);
+  else {
+    dfm_set_error("dfm_cast: bad dtype");
+    return DFM_ERR_DTYPE;
+  }
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_gelu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* pre, long ldpre,
+                            void* dx, long lddx, int accumulate, dfm_stream_t stream) {
+  DFM_CHECK_ARG(dy && pre && dx, "dfm_gelu_bwd: null argument");
+  return ew2d<1>(dtype, rows, C, dy, lddy, pre, ldpre, nullptr, nullptr, 1, 1.f, dx, lddx, accumulate, (hipStream_t)stream);
+}
+
+extern "C" int dfm_relu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* y, long ldy, void* dx,
+                            long lddx, dfm_stream_t stream) {
+  DFM_CHECK_ARG(dy && y && dx, "dfm_relu_bwd: null argument");
+  return ew2d<2>(dtype, rows, C, dy, lddy, y, ldy, nullptr, nullptr, 1, 1.f, dx, lddx, 0, (hipStream_t)stream);
+}
+
+extern "C" int dfm_scale_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* mul, long ldmul,
+                             const float* colscale, const float* rowscale, long rps, float alpha, void* dst,
+                             long lddst, int accumulate, dfm_stream_t stream) {
+  DFM_CHECK_ARG(src && dst, "dfm_scale_mul: null argument");
+  return ew2d<0>(dtype, rows, C, src, ldsrc, mul, ldmul, colscale, rowscale, rps, alpha, dst, lddst, accumulate,
+                 (hipStream_t)stream);
+}
+
+extern "C" int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx, float* stats, void* ws,
+                            dfm_stream_t stream) {
+  DFM_CHECK_ARG(x && stats && ws, "dfm_bn_stats: null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFM_BF16) return colred<bf16_t, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s);
+  if (dtype == DFM_F32) return colred<float, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s);
+  dfm_set_error("dfm_bn_stats: bad dtype");
+  return DFM_ERR_DTYPE;
+}
+
+extern "C" int dfm_bn_finalize(int C, const float* stats, double count, float eps, float momentum, float* mean,
+                               float* rstd, float* rm, float* rv, dfm_stream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, stats, count, eps,
+                     momentum, mean, rstd, rm, rv);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx, const float* mean, const float* rstd,
+                            const float* gamma, const float* beta, const void* res, long ldres, int act, void* y,
+                            long ldy, dfm_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = ew_grid(rows * C);
+  if (dtype == DFM_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean, rstd,
+                       gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean, rstd,
+                       gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_bn_bwd_stats(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
+                                const float* mean, const float* rstd, float* stats2, void* ws, dfm_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFM_BF16) return colred<bf16_t, 2>(rows, C, x, ldx, dy, lddy, mean, rstd, 1, stats2, 0, ws, s);
+  return colred<float, 2>(rows, C, x, ldx, dy, lddy, mean, rstd, 1, stats2, 0, ws, s);
+}
+
+extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
+                                const float* mean, const float* rstd, const float* gamma, const float* stats2,
+                                double count, void* dx, long lddx, int accumulate, dfm_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = ew_grid(rows * C);
+  const float inv_n = (float)(1.0 / count);
+  if (dtype == DFM_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
+                       (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx,
+                       (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
+                              dfm_stream_t stream) {
+  hipLaunchKernelGGL(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
+                                  const float* out, float eps, float* ga, int acc, float* gnum, float* gden,
+                                  dfm_stream_t stream) {
+  hipLaunchKernelGGL(nmf_update_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den, out,
+                     eps, ga, acc, gnum, gden);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream) {
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, x, y);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int acc,
+                                    dfm_stream_t stream) {
+  hipLaunchKernelGGL(softmax_rows_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, y, dy, dx,
+                     acc);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_adamw(long n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
+                         float eps, float wd, int step, float gscale, void* bf16_copy, dfm_stream_t stream) {
+  DFM_CHECK_ARG(p && g && m && v && step >= 1, "dfm_adamw: bad argument");
+  if (n == 0) return DFM_OK;
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2 = 1.f - powf(beta2, (float)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1, beta2,
+                     eps, wd, bc1, sqrtf(bc2), gscale, (bf16_t*)bf16_copy);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}

@@ -1,0 +1,254 @@
+"""DFormer RGB-D encoder with the reference's module tree, constructor arguments and state_dict
+keys (Originofamonia/DFormer models/encoders/DFormer.py), computed by HIP kernels.
+
+Layout: inside a stage the activations are NHWC rows in the compute dtype; the reference's
+Block.forward(x [B,H,W,C], x_e [B,H,W,C/2]) -> (x, x_e) surface is kept. nn.Linear / nn.Conv2d
+children are parameter containers only (their forward is never called on the hot path).
+The stems / stage downsampling (BN + conv3x3 s2, DFormer.py:194-228) run as channels-last
+PyTorch convolutions in round 1 (SURVEY.md §8f item 2 lists them as the next native target).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, invalidate_weights
+
+_EMPTY = {}
+
+
+def _empty(dev):
+    t = _EMPTY.get(dev)
+    if t is None:
+        t = _EMPTY[dev] = torch.empty(0, device=dev)
+    return t
+
+
+class LayerNorm(nn.Module):
+    """channels_last LayerNorm parameters (DFormer.py:21-45); compute happens inside the fused ops."""
+
+    def __init__(self, normalized_shape, eps=1e-6, data_format="channels_last"):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(normalized_shape))
+        self.bias = nn.Parameter(torch.zeros(normalized_shape))
+        self.eps = eps
+        self.data_format = data_format
+        self.normalized_shape = (normalized_shape,)
+
+    def forward(self, x):  # standalone use (not on the fused path)
+        return F.layer_norm(x, self.normalized_shape, self.weight, self.bias, self.eps)
+
+
+class MLP(nn.Module):
+    """ConvFFN: LN -> fc1 -> DW3x3 + identity -> GELU -> fc2 (DFormer.py:48-67)."""
+
+    def __init__(self, dim, mlp_ratio=4, norm_cfg=None):
+        super().__init__()
+        self.norm = LayerNorm(dim, eps=1e-6)
+        self.fc1 = nn.Linear(dim, dim * mlp_ratio)
+        self.pos = nn.Conv2d(dim * mlp_ratio, dim * mlp_ratio, 3, padding=1, groups=dim * mlp_ratio)
+        self.fc2 = nn.Linear(dim * mlp_ratio, dim)
+        self.act = nn.GELU()
+
+    def fused(self, x2d, shape, rowscale, layer_scale):
+        return ConvFFNFn.apply(x2d, shape, rowscale, self.norm.weight, self.norm.bias, self.fc1.weight,
+                               self.fc1.bias, self.pos.weight, self.pos.bias, self.fc2.weight, self.fc2.bias,
+                               layer_scale)
+
+
+class Attention(nn.Module):
+    """RGB-D attention (DFormer.py:70-145): conv modulation, pooled-query attention, depth branch."""
+
+    def __init__(self, dim, num_head=8, window=7, norm_cfg=None, drop_depth=False):
+        super().__init__()
+        self.num_head = num_head
+        self.window = window
+        self.q = nn.Linear(dim, dim)
+        self.q_cut = nn.Linear(dim, dim // 2)
+        self.a = nn.Linear(dim, dim)
+        self.l = nn.Linear(dim, dim)
+        self.conv = nn.Conv2d(dim, dim, 7, padding=3, groups=dim)
+        self.e_conv = nn.Conv2d(dim // 2, dim // 2, 7, padding=3, groups=dim // 2)
+        self.e_fore = nn.Linear(dim // 2, dim // 2)
+        self.e_back = nn.Linear(dim // 2, dim // 2)
+        kin = dim * 2 if window != 0 else dim // 2 * 3
+        self.proj = nn.Linear(kin, dim)
+        if not drop_depth:
+            self.proj_e = nn.Linear(kin, dim // 2)
+        if window != 0:
+            self.short_cut_linear = nn.Linear(dim // 2 * 3, dim // 2)
+            self.kv = nn.Linear(dim, dim)
+            self.pool = nn.AdaptiveAvgPool2d(output_size=(7, 7))
+        self.act = nn.GELU()
+        self.norm = LayerNorm(dim, eps=1e-6)
+        self.norm_e = LayerNorm(dim // 2, eps=1e-6)
+        self.drop_depth = drop_depth
+
+    def fused_params(self, ls1, ls1e):
+        e = _empty(self.q.weight.device)
+        w = self.window != 0
+        d = not self.drop_depth
+        vals = dict(n_w=self.norm.weight, n_b=self.norm.bias, ne_w=self.norm_e.weight, ne_b=self.norm_e.bias,
+                    wq=self.q.weight, bq=self.q.bias, wqc=self.q_cut.weight, bqc=self.q_cut.bias, wl=self.l.weight,
+                    bl=self.l.bias, wconv=self.conv.weight, bconv=self.conv.bias, wa=self.a.weight, ba=self.a.bias,
+                    wef=self.e_fore.weight, bef=self.e_fore.bias, wec=self.e_conv.weight, bec=self.e_conv.bias,
+                    web=self.e_back.weight, beb=self.e_back.bias,
+                    wkv=self.kv.weight if w else e, bkv=self.kv.bias if w else e,
+                    wsc=self.short_cut_linear.weight if w else e, bsc=self.short_cut_linear.bias if w else e,
+                    wp=self.proj.weight, bp=self.proj.bias,
+                    wpe=self.proj_e.weight if d else e, bpe=self.proj_e.bias if d else e,
+                    ls1=ls1, ls1e=ls1e if ls1e is not None else e)
+        return [vals[n] for n in ATTN_PARAM_NAMES]
+
+
+def _drop_path_scale(B, drop_prob, training, dev):
+    """mmcv DropPath as a per-sample row scale: floor(keep + U[0,1)) / keep, or None."""
+    if drop_prob == 0.0 or not training:
+        return None
+    keep = 1.0 - drop_prob
+    return (keep + torch.rand(B, device=dev)).floor_().div_(keep)
+
+
+class Block(nn.Module):
+    """DFormer Block (DFormer.py:147-181): x + DropPath(ls1 * attn), + DropPath(ls2 * MLP), both branches."""
+
+    def __init__(self, index, dim, num_head, norm_cfg=None, mlp_ratio=4.0, block_index=0, last_block_index=50,
+                 window=7, dropout_layer=None, drop_depth=False):
+        super().__init__()
+        self.index = index
+        layer_scale_init_value = 1e-6
+        if block_index > last_block_index:
+            window = 0
+        self.attn = Attention(dim, num_head, window=window, norm_cfg=norm_cfg, drop_depth=drop_depth)
+        self.mlp = MLP(dim, int(mlp_ratio), norm_cfg=norm_cfg)
+        self.drop_prob = float(dropout_layer.get("drop_prob", 0.0)) if dropout_layer else 0.0
+        self.layer_scale_1 = nn.Parameter(layer_scale_init_value * torch.ones(dim))
+        self.layer_scale_2 = nn.Parameter(layer_scale_init_value * torch.ones(dim))
+        if not drop_depth:
+            self.layer_scale_1_e = nn.Parameter(layer_scale_init_value * torch.ones(dim // 2))
+            self.layer_scale_2_e = nn.Parameter(layer_scale_init_value * torch.ones(dim // 2))
+            self.mlp_e2 = MLP(dim // 2, int(mlp_ratio))
+        self.drop_depth = drop_depth
+        self.drop_path_masks = None  # tests may inject the 4 per-sample keep masks (mmcv call order)
+
+    def forward(self, x, x_e):
+        B, H, W, C = x.shape
+        shape = (B, H, W)
+        xr = x.reshape(B * H * W, C)
+        xer = x_e.reshape(B * H * W, C // 2)
+        if self.drop_path_masks is not None and self.training and self.drop_prob > 0:
+            keep = 1.0 - self.drop_prob
+            rs = [m.to(device=x.device, dtype=torch.float32) / keep for m in self.drop_path_masks]
+        else:
+            rs = [_drop_path_scale(B, self.drop_prob, self.training, x.device) for _ in range(4)]
+        ls1e = self.layer_scale_1_e if not self.drop_depth else None
+        x1, xe1 = AttentionFn.apply(xr, xer, shape, self.attn.num_head, self.attn.window, self.drop_depth, rs[0],
+                                    rs[2], *self.attn.fused_params(self.layer_scale_1, ls1e))
+        x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
+        if self.drop_depth:
+            return x2.view(B, H, W, C), x_e
+        xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
+        return x2.view(B, H, W, C), xe2.view(B, H, W, C // 2)
+
+
+def _bn(c, syncbn):
+    return nn.SyncBatchNorm(c) if syncbn else nn.BatchNorm2d(c)
+
+
+class DFormer(nn.Module):
+    """DFormer backbone (DFormer.py:184-305). forward(x, x_e) -> (outs[4] NCHW views, None) like the
+    reference; outs are channels-last buffers in the compute dtype."""
+
+    def __init__(self, in_channels=4, depths=(2, 2, 8, 2), dims=(32, 64, 128, 256), out_indices=(0, 1, 2, 3),
+                 windows=(7, 7, 7, 7), norm_cfg=None, mlp_ratios=(8, 8, 4, 4), num_heads=(2, 4, 10, 16),
+                 last_block=(50, 50, 50, 50), drop_path_rate=0.1, init_cfg=None):
+        super().__init__()
+        syncbn = bool(norm_cfg) and norm_cfg.get("type") == "SyncBN" and torch.distributed.is_initialized() \
+            and torch.distributed.get_world_size() > 1
+        self.depths = depths
+        self.dims = dims
+        self.out_indices = out_indices
+        self.compute_dtype = torch.float32
+        self.downsample_layers = nn.ModuleList()
+        self.downsample_layers.append(nn.Sequential(
+            nn.Conv2d(3, dims[0] // 2, 3, 2, 1), nn.BatchNorm2d(dims[0] // 2), nn.GELU(),
+            nn.Conv2d(dims[0] // 2, dims[0], 3, 2, 1), nn.BatchNorm2d(dims[0])))
+        # unused by the reference forward (DFormer.py:202-203, 287-291); kept for state_dict parity
+        self.stem_e_fc1 = nn.Linear(360, 640)
+        self.stem_e_fc2 = nn.Linear(1, 480)
+        self.downsample_layers_e = nn.ModuleList()
+        self.downsample_layers_e.append(nn.Sequential(
+            nn.Conv2d(1, dims[0] // 4, 3, 2, 1), nn.BatchNorm2d(dims[0] // 4), nn.GELU(),
+            nn.Conv2d(dims[0] // 4, dims[0] // 2, 3, 2, 1), nn.BatchNorm2d(dims[0] // 2)))
+        for i in range(len(dims) - 1):
+            self.downsample_layers.append(nn.Sequential(_bn(dims[i], syncbn),
+                                                        nn.Conv2d(dims[i], dims[i + 1], 3, 2, 1)))
+            self.downsample_layers_e.append(nn.Sequential(_bn(dims[i] // 2, syncbn),
+                                                          nn.Conv2d(dims[i] // 2, dims[i + 1] // 2, 3, 2, 1)))
+        self.stages = nn.ModuleList()
+        dp_rates = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        cur = 0
+        for i in range(len(dims)):
+            self.stages.append(nn.Sequential(*[
+                Block(index=cur + j, dim=dims[i], window=windows[i],
+                      dropout_layer=dict(type="DropPath", drop_prob=dp_rates[cur + j]), num_head=num_heads[i],
+                      norm_cfg=norm_cfg, block_index=depths[i] - j, last_block_index=last_block[i],
+                      mlp_ratio=mlp_ratios[i], drop_depth=((i == 3) & (j == depths[i] - 1)))
+                for j in range(depths[i])]))
+            cur += depths[i]
+        for p in (self.stem_e_fc1.weight, self.stem_e_fc1.bias, self.stem_e_fc2.weight, self.stem_e_fc2.bias):
+            p.requires_grad_(False)  # never used: excluded from gradients (and DDP buckets)
+
+    def load_state_dict(self, *a, **k):
+        r = super().load_state_dict(*a, **k)
+        invalidate_weights()
+        return r
+
+    def _downsample(self, i, x, e):
+        dt = self.compute_dtype
+        with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
+            x = self.downsample_layers[i](x)
+            e = self.downsample_layers_e[i](e)
+        return x, e
+
+    def forward(self, x, x_e):
+        if x_e is None:
+            x_e = x
+        if x.dim() == 3:
+            x = x.unsqueeze(0)
+        if x_e.dim() == 3:
+            x_e = x_e.unsqueeze(2)
+        x_e = x_e[:, 0:1]
+        dt = self.compute_dtype
+        x = x.to(dt).contiguous(memory_format=torch.channels_last)
+        x_e = x_e.to(dt).contiguous(memory_format=torch.channels_last)
+        outs = []
+        for i in range(4):
+            x, x_e = self._downsample(i, x, x_e)
+            xh = x.permute(0, 2, 3, 1).to(dt).contiguous()
+            eh = x_e.permute(0, 2, 3, 1).to(dt).contiguous()
+            for blk in self.stages[i]:
+                xh, eh = blk(xh, eh)
+            x = xh.permute(0, 3, 1, 2)  # NCHW view of the channels-last buffer
+            x_e = eh.permute(0, 3, 1, 2)
+            outs.append(x)
+        return outs, None
+
+
+def DFormer_Tiny(pretrained=False, **kwargs):
+    return DFormer(dims=[32, 64, 128, 256], mlp_ratios=[8, 8, 4, 4], depths=[3, 3, 5, 2], num_heads=[1, 2, 4, 8],
+                   windows=[0, 7, 7, 7], **kwargs)
+
+
+def DFormer_Small(pretrained=False, **kwargs):
+    return DFormer(dims=[64, 128, 256, 512], mlp_ratios=[8, 8, 4, 4], depths=[2, 2, 4, 2], num_heads=[1, 2, 4, 8],
+                   windows=[0, 7, 7, 7], **kwargs)
+
+
+def DFormer_Base(pretrained=False, drop_path_rate=0.1, **kwargs):
+    return DFormer(dims=[64, 128, 256, 512], mlp_ratios=[8, 8, 4, 4], depths=[3, 3, 12, 2], num_heads=[1, 2, 4, 8],
+                   windows=[0, 7, 7, 7], drop_path_rate=drop_path_rate, **kwargs)
+
+
+def DFormer_Large(pretrained=False, drop_path_rate=0.1, **kwargs):
+    return DFormer(dims=[96, 192, 288, 576], mlp_ratios=[8, 8, 4, 4], depths=[3, 3, 12, 2], num_heads=[1, 2, 4, 8],
+                   windows=[0, 7, 7, 7], drop_path_rate=drop_path_rate, **kwargs)

@@ -1,0 +1,276 @@
+"""autograd.Functions of DFormer's encoder Block with hand-written backward passes.
+
+Every tensor op inside these Functions is a libdformer_hip.so kernel (dformer_amd.kernels);
+torch provides allocation, views and the autograd tape only. Activations are NHWC rows [P, C]
+in the compute dtype (float32 for parity runs, bfloat16 for training); parameters and their
+gradients are float32 (GEMM operands use cached compute-dtype copies of the weights).
+
+Reference semantics (file:line in Originofamonia/DFormer):
+  ConvFFNFn     MLP.forward + Block residual/layer-scale/DropPath   DFormer.py:48-67, 173-179
+  AttentionFn   Attention.forward + Block residuals                 DFormer.py:70-145, 168-179
+"""
+import torch
+
+from . import kernels as K
+
+# ---------------------------------------------------------------- compute-dtype weight cache
+_EPOCH = [0]
+_WCACHE = {}
+
+
+def invalidate_weights():
+    """Call after parameters change outside dformer_amd's optimizer (load_state_dict, manual edits)."""
+    _EPOCH[0] += 1
+    _WCACHE.clear()
+
+
+def register_shadow(p, shadow):
+    """The fused optimizer keeps `shadow` (bf16 copy of p) up to date itself."""
+    _WCACHE[(id(p), shadow.dtype)] = (_EPOCH[0], shadow, (p.data_ptr(),))
+
+
+def wcast(dtype, *params):
+    """Compute-dtype 2-D copy of one parameter (or the row-concatenation of several), cached per epoch."""
+    if dtype == torch.float32 and len(params) == 1:
+        p = params[0].detach()
+        return p if p.dim() == 2 else p.reshape(p.shape[0], -1)
+    key = tuple(id(p) for p in params) + (dtype,)
+    ptrs = tuple(p.data_ptr() for p in params)
+    hit = _WCACHE.get(key)
+    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
+        return hit[1]
+    src = params[0].detach().reshape(params[0].shape[0], -1) if len(params) == 1 else \
+        torch.cat([p.detach().reshape(p.shape[0], -1) for p in params], 0)
+    src = src.contiguous()
+    w = src if dtype == torch.float32 else K.cast(src, dtype)
+    _WCACHE[key] = (_EPOCH[0], w, ptrs)
+    return w
+
+
+def _cat1(*vs):
+    """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
+    key = tuple(id(v) for v in vs) + ("bias",)
+    ptrs = tuple(v.data_ptr() for v in vs)
+    hit = _WCACHE.get(key)
+    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
+        return hit[1]
+    out = torch.cat([v.detach() for v in vs])
+    _WCACHE[key] = (_EPOCH[0], out, ptrs)
+    return out
+
+
+# ====================================================================== ConvFFN (+ residual)
+class ConvFFNFn(torch.autograd.Function):
+    """out = x + rowscale * ls * fc2(GELU(DW3x3(h) + h)),  h = fc1(LN(x))   on [P, C] rows.
+
+    forward kernels: LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
+                     GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue)."""
+
+    @staticmethod
+    def forward(ctx, x, shape, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls):
+        B, H, W = shape
+        P, C = x.shape
+        dt = x.dtype
+        W1, W2 = wcast(dt, w1), wcast(dt, w2)
+        xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
+        h = K.linear(xn, W1, b1)
+        g = torch.empty_like(h)
+        hpre = K.dwconv(h, shape, wpos, bpos, 3, add_identity=True, gelu_out=g)
+        f = torch.empty(P, C, device=x.device, dtype=dt)
+        out = K.linear(g, W2, b2, preact=f, res=x, colscale=ls, rowscale=rowscale, rows_per_scale=H * W)
+        ctx.save_for_backward(x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, wpos, w2, ls)
+        ctx.shape = shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, wpos, w2, ls = ctx.saved_tensors
+        B, H, W = ctx.shape
+        dt = x.dtype
+        dout = dout.contiguous()
+        W1, W2 = wcast(dt, w1), wcast(dt, w2)
+        rps = H * W
+        dls = K.colsum(dout, mul=f, rowscale=rowscale, rows_per_scale=rps)
+        df = K.scale_mul(dout, colscale=ls, rowscale=rowscale, rows_per_scale=rps)
+        db2 = K.colsum(df)
+        dW2 = K.linear_wgrad(df, g)
+        dg = K.linear_dgrad(df, W2)
+        dhpre = K.gelu_bwd(dg, hpre)
+        dwpos, dbpos = K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3)
+        dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
+        db1 = K.colsum(dh)
+        dW1 = K.linear_wgrad(dh, xn)
+        dxn = K.linear_dgrad(dh, W1)
+        dx = dout.clone()
+        _, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dx=dx, accumulate=True)
+        return dx, None, None, dlnw, dlnb, dW1, db1, dwpos.view_as(wpos), dbpos, dW2, db2, dls
+
+
+# ====================================================================== Attention (+ residuals)
+class AttentionFn(torch.autograd.Function):
+    """(x1, xe1) = (x + rs*ls1*proj(f), xe + rs*ls1e*proj_e(f)),  f = cat(q*a, attn, cx*xe')
+
+    Parameter order (`params`): see ATTN_PARAM_NAMES. Window 0 (stage 0) has no kv / pooled
+    attention (f = cat(q*a, cx*xe')); drop_depth (last block) has no proj_e, xe passes through.
+    """
+
+    @staticmethod
+    def forward(ctx, x, xe, shape, heads, window, drop_depth, rowscale, rowscale_e, *params):
+        (n_w, n_b, ne_w, ne_b, wq, bq, wqc, bqc, wl, bl, wconv, bconv, wa, ba, wef, bef, wec, bec, web, beb,
+         wkv, bkv, wsc, bsc, wp, bp, wpe, bpe, ls1, ls1e) = params
+        B, H, W = shape
+        P, C = x.shape
+        Ch = C // 2
+        dt = x.dtype
+        dev = x.device
+        rps = H * W
+        xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
+        xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
+        # q | q_cut | l in one GEMM; GELU (and its pre-activation store) only on the l columns
+        Wqcl = wcast(dt, wq, wqc, wl)
+        bqcl = _cat1(bq, bqc, bl)
+        qcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
+        lpre = torch.empty(P, C, device=dev, dtype=dt)
+        K.linear(xn, Wqcl, bqcl, act=1, preact=lpre, act_col0=C + Ch, out=qcl)
+        q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
+        fw = 2 * C if window else C + Ch
+        f = torch.empty(P, fw, device=dev, dtype=dt)
+        # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward)
+        apre = K.dwconv(g, shape, wconv, bconv, 7)
+        a = torch.empty(P, C, device=dev, dtype=dt)
+        K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C])
+        saved_attn = ()
+        if window:
+            dh = C // heads // 2
+            kv = K.linear(g, wcast(dt, wkv), bkv)
+            pooled = torch.empty(B * 49, C + Ch, device=dev, dtype=dt)
+            K.pool7(xn, shape, out=pooled[:, :C])
+            K.pool7(xen, shape, out=pooled[:, C:])
+            m = K.linear(pooled, wcast(dt, wsc), bsc)
+            o, lse = K.pooled_attn(m, kv[:, :Ch], kv[:, Ch:], B, heads, P // B, dh, dh ** -0.5)
+            K.bilinear(o, (7, 7), (H, W), B, out=f[:, C:C + Ch])
+            saved_attn = (kv, pooled, m, o, lse)
+        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
+        e1 = K.linear(xen, wcast(dt, wef), bef)
+        e2 = K.dwconv(e1, shape, wec, bec, 7)
+        xep = torch.empty(P, Ch, device=dev, dtype=dt)
+        K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
+        # projections with the Block's residual / layer-scale / DropPath epilogue
+        p1 = torch.empty(P, C, device=dev, dtype=dt)
+        x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
+        if drop_depth:
+            xe1, p1e = xe, None
+        else:
+            p1e = torch.empty(P, Ch, device=dev, dtype=dt)
+            xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
+                           rows_per_scale=rps)
+        ctx.shape, ctx.heads, ctx.window, ctx.drop_depth = shape, heads, window, drop_depth
+        ctx.n_attn = len(saved_attn)
+        ctx.save_for_backward(x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1,
+                              p1e if p1e is not None else x.new_empty(0), rowscale, rowscale_e, *params,
+                              *saved_attn)
+        return x1, xe1
+
+    @staticmethod
+    def backward(ctx, dx1, dxe1):
+        sv = ctx.saved_tensors
+        (x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1, p1e, rowscale,
+         rowscale_e) = sv[:20]
+        params = sv[20:20 + 30]
+        (n_w, n_b, ne_w, ne_b, wq, bq, wqc, bqc, wl, bl, wconv, bconv, wa, ba, wef, bef, wec, bec, web, beb,
+         wkv, bkv, wsc, bsc, wp, bp, wpe, bpe, ls1, ls1e) = params
+        saved_attn = sv[50:]
+        shape, heads, window, drop_depth = ctx.shape, ctx.heads, ctx.window, ctx.drop_depth
+        B, H, W = shape
+        P, C = x.shape
+        Ch = C // 2
+        dt = x.dtype
+        dev = x.device
+        rps = H * W
+        fw = f.shape[1]
+        grads = {}
+        dx1 = dx1.contiguous()
+        # projections
+        grads["ls1"] = K.colsum(dx1, mul=p1, rowscale=rowscale, rows_per_scale=rps)
+        dp1 = K.scale_mul(dx1, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
+        grads["bp"] = K.colsum(dp1)
+        grads["wp"] = K.linear_wgrad(dp1, f)
+        df = K.linear_dgrad(dp1, wcast(dt, wp))
+        if drop_depth:
+            dxe = dxe1.contiguous().clone() if dxe1 is not None else torch.zeros_like(xe)
+        else:
+            dxe1 = dxe1.contiguous()
+            grads["ls1e"] = K.colsum(dxe1, mul=p1e, rowscale=rowscale_e, rows_per_scale=rps)
+            dp1e = K.scale_mul(dxe1, colscale=ls1e, rowscale=rowscale_e, rows_per_scale=rps)
+            grads["bpe"] = K.colsum(dp1e)
+            grads["wpe"] = K.linear_wgrad(dp1e, f)
+            K.linear_dgrad(dp1e, wcast(dt, wpe), out=df, accumulate=True)
+            dxe = dxe1.clone()
+        q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
+        dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
+        dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
+        # depth branch: cxe = cx * xe'
+        dcxe = df[:, fw - Ch:]
+        K.scale_mul(dcxe, mul=xep, out=dcx)
+        dxep = K.scale_mul(dcxe, mul=cx)
+        grads["beb"] = K.colsum(dxep)
+        grads["web"] = K.linear_wgrad(dxep, e2)
+        de2 = K.linear_dgrad(dxep, wcast(dt, web))
+        grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7)
+        de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
+        grads["bef"] = K.colsum(de1)
+        grads["wef"] = K.linear_wgrad(de1, xen)
+        dxen = K.linear_dgrad(de1, wcast(dt, wef))
+        dg = torch.empty(P, C, device=dev, dtype=dt)
+        dxn = None
+        if window:
+            kv, pooled, m, o, lse = saved_attn
+            dh = C // heads // 2
+            do = K.bilinear_bwd(df[:, C:C + Ch], (7, 7), (H, W), B)
+            dm = torch.empty_like(m)
+            dkv = torch.empty(P, C, device=dev, dtype=dt)
+            K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
+                              dkv[:, :Ch], dkv[:, Ch:])
+            grads["bsc"] = K.colsum(dm)
+            grads["wsc"] = K.linear_wgrad(dm, pooled)
+            dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
+            dxn = K.pool7_bwd(dpooled[:, :C], shape)
+            K.pool7_bwd(dpooled[:, C:], shape, dx=dxen, accumulate=True)
+            grads["bkv"] = K.colsum(dkv)
+            grads["wkv"] = K.linear_wgrad(dkv, g)
+            K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
+        # q * a
+        dqa = df[:, :C]
+        K.scale_mul(dqa, mul=a, out=dq)
+        da = K.scale_mul(dqa, mul=q)
+        grads["ba"] = K.colsum(da)
+        grads["wa"] = K.linear_wgrad(da, apre)
+        dapre = K.linear_dgrad(da, wcast(dt, wa))
+        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7)
+        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
+        K.gelu_bwd(dg, lpre, out=dl)
+        # q | q_cut | l
+        dbqcl = K.colsum(dqcl)
+        dWqcl = K.linear_wgrad(dqcl, xn)
+        grads["bq"], grads["bqc"], grads["bl"] = dbqcl[:C], dbqcl[C:C + Ch], dbqcl[C + Ch:]
+        grads["wq"], grads["wqc"], grads["wl"] = dWqcl[:C], dWqcl[C:C + Ch], dWqcl[C + Ch:]
+        Wqcl = wcast(dt, wq, wqc, wl)
+        if dxn is None:
+            dxn = K.linear_dgrad(dqcl, Wqcl)
+        else:
+            K.linear_dgrad(dqcl, Wqcl, out=dxn, accumulate=True)
+        dx = dx1.clone()
+        _, grads["n_w"], grads["n_b"] = K.layernorm_bwd(x, dxn, n_w, mu1, rs1, dx=dx, accumulate=True)
+        _, grads["ne_w"], grads["ne_b"] = K.layernorm_bwd(xe, dxen, ne_w, mu2, rs2, dx=dxe, accumulate=True)
+        out = []
+        for name, p in zip(ATTN_PARAM_NAMES, params):
+            gr = grads.get(name)
+            if gr is not None and p.numel() > 0:
+                gr = gr.reshape(p.shape)
+            out.append(gr if p.numel() > 0 else None)
+        return (dx, dxe, None, None, None, None, None, None, *out)
+
+
+ATTN_PARAM_NAMES = ("n_w", "n_b", "ne_w", "ne_b", "wq", "bq", "wqc", "bqc", "wl", "bl", "wconv", "bconv", "wa", "ba",
+                    "wef", "bef", "wec", "bec", "web", "beb", "wkv", "bkv", "wsc", "bsc", "wp", "bp", "wpe", "bpe",
+                    "ls1", "ls1e")

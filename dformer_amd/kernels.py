@@ -1,0 +1,380 @@
+"""Thin tensor-level wrappers over the C ABI (allocation of outputs / workspaces + launch).
+
+All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose last stride is 1
+(the row stride is passed through as `ld`, so column slices of wider buffers work in place).
+Activations are float32 or bfloat16; statistics / params / param-grads are float32.
+"""
+import torch
+
+from . import _lib
+from ._lib import check, dtype_code, lib, ptr, stream
+
+_ws_cache = {}
+
+
+def _ws(nbytes, dev):
+    """Per-device scratch buffer that only grows (the library never allocates)."""
+    if nbytes == 0:
+        return None
+    buf = _ws_cache.get(dev)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+        _ws_cache[dev] = buf
+    return buf
+
+
+def ld(t):
+    assert t.dim() >= 2 and t.stride(-1) == 1, "inner dimension must be contiguous"
+    return t.stride(-2)
+
+
+def rows_of(t):
+    return t.numel() // t.shape[-1] if t.is_contiguous() else t.shape[0]
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
+         stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
+         ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0):
+    dt = dtype_code(a)
+    assert b.dtype == a.dtype, (a.dtype, b.dtype)
+    c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
+    if out.dtype != torch.float32:
+        assert out.dtype == a.dtype
+    d = _lib.GemmDesc(M, N, K, batch, int(a_kcontig), int(b_kcontig), lda, ldb, ldc, stride_a, stride_b, stride_c,
+                      alpha, beta, c_f32, ptr(bias), act, ptr(preact), ldpre, ptr(mul), ldmul, ptr(res), ldres,
+                      ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0)
+    nbytes = lib.dfm_gemm_workspace_size(d)
+    ws = _ws(nbytes, a.device)
+    check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
+    return out
+
+
+def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=None, rowscale=None,
+           rows_per_scale=1, out=None, beta=0.0, act_col0=0):
+    """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=x.dtype)
+    return gemm(x, w, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=ld(x), ldb=ld(w), out=out, ldc=ld(out),
+                beta=beta, bias=bias, act=act, preact=preact, ldpre=ld(preact) if preact is not None else 0,
+                mul=mul, ldmul=ld(mul) if mul is not None else 0, res=res, ldres=ld(res) if res is not None else 0,
+                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0)
+
+
+def linear_dgrad(dy, w, out=None, accumulate=False, mul=None):
+    """dx[M,K] (+)= dy[M,N] @ w[N,K]   (optionally times `mul` elementwise)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
+    return gemm(dy, w, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=ld(dy), ldb=ld(w), out=out, ldc=ld(out),
+                beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0)
+
+
+def linear_wgrad(dy, x, out=None, accumulate=False):
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]  (float32 output, split-K over M)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    if out is None:
+        out = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+    return gemm(dy, x, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=ld(dy), ldb=ld(x), out=out,
+                ldc=ld(out), beta=1.0 if accumulate else 0.0)
+
+
+def bmm(a, b, *, a_t=False, b_t=False, out=None, alpha=1.0):
+    """Batched out[b] = op(a[b]) @ op(b[b]) for contiguous 3-D tensors (op = transpose if *_t)."""
+    B = a.shape[0]
+    M = a.shape[2] if a_t else a.shape[1]
+    K = a.shape[1] if a_t else a.shape[2]
+    N = b.shape[1] if b_t else b.shape[2]
+    assert (b.shape[2] if b_t else b.shape[1]) == K
+    if out is None:
+        out = torch.empty(B, M, N, device=a.device, dtype=a.dtype)
+    # A(m,k): a[m][k] (k-contig, lda=K) or a[k][m] (a_t: row-contig, lda=M)
+    # B(k,n): b[k][n] (row-contig, ldb=N) or b[n][k] (b_t: k-contig, ldb=K)
+    return gemm(a, b, M=M, N=N, K=K, a_kcontig=not a_t, b_kcontig=b_t, lda=a.shape[2], ldb=b.shape[2], out=out,
+                ldc=N, batch=B, stride_a=a.shape[1] * a.shape[2], stride_b=b.shape[1] * b.shape[2],
+                stride_c=M * N, alpha=alpha)
+
+
+# ------------------------------------------------------------------------------------ LayerNorm
+def layernorm(x, gamma, beta, eps=1e-6, out=None):
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty(rows, C, device=x.device, dtype=x.dtype)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    check(lib.dfm_layernorm_fwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(gamma), ptr(beta), eps, ptr(out),
+                                ld(out), ptr(mean), ptr(rstd), stream()), "dfm_layernorm_fwd")
+    return out, mean, rstd
+
+
+def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False):
+    rows, C = x.shape
+    if dx is None:
+        dx = torch.empty(rows, C, device=x.device, dtype=x.dtype)
+        accumulate = False
+    dg = torch.empty(C, device=x.device, dtype=torch.float32)
+    db = torch.empty(C, device=x.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_layernorm_bwd_workspace(rows, C), x.device)
+    check(lib.dfm_layernorm_bwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(gamma), ptr(mean),
+                                ptr(rstd), ptr(dx), ld(dx), int(accumulate), ptr(dg), ptr(db), ptr(ws), stream()),
+          "dfm_layernorm_bwd")
+    return dx, dg, db
+
+
+# ---------------------------------------------------------------------------- depthwise conv
+def dwconv(x, shape, w, bias, k, add_identity=False, out=None, gelu_out=None):
+    """x: [B*H*W, C] view (NHWC rows); w float32 [C,1,k,k] or [C,k,k]. gelu_out: also GELU(y)."""
+    B, H, W = shape
+    C = x.shape[1]
+    if out is None:
+        out = torch.empty(x.shape[0], C, device=x.device, dtype=x.dtype)
+    check(lib.dfm_dwconv_fwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(w), ptr(bias), int(add_identity),
+                             ptr(out), ld(out), ptr(gelu_out), ld(gelu_out) if gelu_out is not None else 0,
+                             stream()), "dfm_dwconv_fwd")
+    return out
+
+
+def dwconv_bwd_data(dy, shape, w, k, add_identity=False, dx=None, accumulate=False):
+    B, H, W = shape
+    C = dy.shape[1]
+    if dx is None:
+        dx = torch.empty(dy.shape[0], C, device=dy.device, dtype=dy.dtype)
+        accumulate = False
+    check(lib.dfm_dwconv_bwd_data(dtype_code(dy), B, H, W, C, k, ptr(dy), ld(dy), ptr(w), int(add_identity),
+                                  ptr(dx), ld(dx), int(accumulate), stream()), "dfm_dwconv_bwd_data")
+    return dx
+
+
+def dwconv_bwd_weight(x, dy, shape, k):
+    B, H, W = shape
+    C = x.shape[1]
+    dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
+    db = torch.empty(C, device=x.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
+    check(lib.dfm_dwconv_bwd_weight(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(dw), ptr(db),
+                                    ptr(ws), stream()), "dfm_dwconv_bwd_weight")
+    return dw, db
+
+
+# -------------------------------------------------------------------------- reductions / misc
+def colsum(x, mul=None, rowscale=None, rows_per_scale=1, out=None, accumulate=False):
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty(C, device=x.device, dtype=torch.float32)
+        accumulate = False
+    ws = _ws(lib.dfm_colsum_workspace(rows, C), x.device)
+    check(lib.dfm_colsum(dtype_code(x), rows, C, ptr(x), ld(x), ptr(mul), ld(mul) if mul is not None else 0,
+                         ptr(rowscale), rows_per_scale, ptr(out), int(accumulate), ptr(ws), stream()), "dfm_colsum")
+    return out
+
+
+def cast(x, dtype, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    assert x.is_contiguous() and out.is_contiguous()
+    check(lib.dfm_cast(dtype_code(x), dtype_code(out), x.numel(), ptr(x), ptr(out), stream()), "dfm_cast")
+    return out
+
+
+def gelu_bwd(dy, pre, out=None, accumulate=False):
+    rows, C = dy.shape
+    if out is None:
+        out = torch.empty(rows, C, device=dy.device, dtype=dy.dtype)
+        accumulate = False
+    check(lib.dfm_gelu_bwd(dtype_code(dy), rows, C, ptr(dy), ld(dy), ptr(pre), ld(pre), ptr(out), ld(out),
+                           int(accumulate), stream()), "dfm_gelu_bwd")
+    return out
+
+
+def relu_bwd(dy, y, out=None):
+    rows, C = dy.shape
+    if out is None:
+        out = torch.empty(rows, C, device=dy.device, dtype=dy.dtype)
+    check(lib.dfm_relu_bwd(dtype_code(dy), rows, C, ptr(dy), ld(dy), ptr(y), ld(y), ptr(out), ld(out), stream()),
+          "dfm_relu_bwd")
+    return out
+
+
+def scale_mul(src, mul=None, colscale=None, rowscale=None, rows_per_scale=1, alpha=1.0, out=None, accumulate=False):
+    rows, C = src.shape
+    if out is None:
+        out = torch.empty(rows, C, device=src.device, dtype=src.dtype)
+        accumulate = False
+    check(lib.dfm_scale_mul(dtype_code(src), rows, C, ptr(src), ld(src), ptr(mul), ld(mul) if mul is not None else 0,
+                            ptr(colscale), ptr(rowscale), rows_per_scale, alpha, ptr(out), ld(out), int(accumulate),
+                            stream()), "dfm_scale_mul")
+    return out
+
+
+# ---------------------------------------------------------------------- pool / bilinear / attn
+def pool7(x, shape, out=None):
+    B, H, W = shape
+    C = x.shape[1]
+    if out is None:
+        out = torch.empty(B * 49, C, device=x.device, dtype=x.dtype)
+    check(lib.dfm_adaptive_pool7_fwd(dtype_code(x), B, H, W, C, ptr(x), ld(x), ptr(out), ld(out), stream()),
+          "dfm_adaptive_pool7_fwd")
+    return out
+
+
+def pool7_bwd(dy, shape, dx=None, accumulate=False):
+    B, H, W = shape
+    C = dy.shape[1]
+    if dx is None:
+        dx = torch.empty(B * H * W, C, device=dy.device, dtype=dy.dtype)
+        accumulate = False
+    check(lib.dfm_adaptive_pool7_bwd(dtype_code(dy), B, H, W, C, ptr(dy), ld(dy), ptr(dx), ld(dx), int(accumulate),
+                                     stream()), "dfm_adaptive_pool7_bwd")
+    return dx
+
+
+def bilinear(x, in_hw, out_hw, B, out=None, accumulate=False):
+    (Hi, Wi), (Ho, Wo) = in_hw, out_hw
+    C = x.shape[1]
+    if out is None:
+        out = torch.empty(B * Ho * Wo, C, device=x.device, dtype=x.dtype)
+        accumulate = False
+    check(lib.dfm_bilinear_fwd(dtype_code(x), B, Hi, Wi, Ho, Wo, C, ptr(x), ld(x), ptr(out), ld(out),
+                               int(accumulate), stream()), "dfm_bilinear_fwd")
+    return out
+
+
+def bilinear_bwd(dy, in_hw, out_hw, B, dx=None, accumulate=False):
+    (Hi, Wi), (Ho, Wo) = in_hw, out_hw
+    C = dy.shape[1]
+    if dx is None:
+        dx = torch.empty(B * Hi * Wi, C, device=dy.device, dtype=dy.dtype)
+        accumulate = False
+    check(lib.dfm_bilinear_bwd(dtype_code(dy), B, Hi, Wi, Ho, Wo, C, ptr(dy), ld(dy), ptr(dx), ld(dx),
+                               int(accumulate), stream()), "dfm_bilinear_bwd")
+    return dx
+
+
+def pooled_attn(q, k, v, B, heads, N, dh, scale, out=None):
+    """q: [B*49, >=heads*dh] view, k/v: [B*N, ...] views (head h at cols h*dh)."""
+    if out is None:
+        out = torch.empty(B * 49, heads * dh, device=q.device, dtype=q.dtype)
+    lse = torch.empty(B * heads * 49, device=q.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_pooled_attn_workspace(B, heads, N, dh), q.device)
+    assert ld(k) == ld(v)
+    check(lib.dfm_pooled_attn_fwd(dtype_code(q), B, heads, N, dh, ptr(q), ld(q), ptr(k), ptr(v), ld(k), scale,
+                                  ptr(out), ld(out), ptr(lse), ptr(ws), stream()), "dfm_pooled_attn_fwd")
+    return out, lse
+
+
+def pooled_attn_bwd(q, k, v, o, dout, lse, B, heads, N, dh, scale, dq, dk, dv):
+    ws = _ws(lib.dfm_pooled_attn_workspace(B, heads, N, dh), q.device)
+    assert ld(dk) == ld(dv) and ld(dq) == ld(q)
+    check(lib.dfm_pooled_attn_bwd(dtype_code(q), B, heads, N, dh, ptr(q), ld(q), ptr(k), ptr(v), ld(k), scale,
+                                  ptr(o), ld(o), ptr(dout), ld(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv), ld(dk),
+                                  ptr(ws), stream()), "dfm_pooled_attn_bwd")
+
+
+# ---------------------------------------------------------------------------------- BatchNorm
+def bn_stats(x):
+    rows, C = x.shape
+    st = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_bn_workspace(rows, C), x.device)
+    check(lib.dfm_bn_stats(dtype_code(x), rows, C, ptr(x), ld(x), ptr(st), ptr(ws), stream()), "dfm_bn_stats")
+    return st
+
+
+def bn_finalize(stats, count, eps, momentum, running_mean=None, running_var=None):
+    C = stats.shape[1]
+    mean = torch.empty(C, device=stats.device, dtype=torch.float32)
+    rstd = torch.empty(C, device=stats.device, dtype=torch.float32)
+    check(lib.dfm_bn_finalize(C, ptr(stats), float(count), eps, momentum, ptr(mean), ptr(rstd), ptr(running_mean),
+                              ptr(running_var), stream()), "dfm_bn_finalize")
+    return mean, rstd
+
+
+def bn_apply(x, mean, rstd, gamma, beta, res=None, act=0, out=None):
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty(rows, C, device=x.device, dtype=x.dtype)
+    check(lib.dfm_bn_apply(dtype_code(x), rows, C, ptr(x), ld(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
+                           ptr(res), ld(res) if res is not None else 0, act, ptr(out), ld(out), stream()),
+          "dfm_bn_apply")
+    return out
+
+
+def bn_bwd_stats(x, dy, mean, rstd):
+    rows, C = x.shape
+    st = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_bn_workspace(rows, C), x.device)
+    check(lib.dfm_bn_bwd_stats(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(mean), ptr(rstd),
+                               ptr(st), ptr(ws), stream()), "dfm_bn_bwd_stats")
+    return st
+
+
+def bn_bwd_apply(x, dy, mean, rstd, gamma, stats2, count, dx=None, accumulate=False):
+    rows, C = x.shape
+    if dx is None:
+        dx = torch.empty(rows, C, device=x.device, dtype=x.dtype)
+        accumulate = False
+    check(lib.dfm_bn_bwd_apply(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(mean), ptr(rstd),
+                               ptr(gamma), ptr(stats2), float(count), ptr(dx), ld(dx), int(accumulate), stream()),
+          "dfm_bn_bwd_apply")
+    return dx
+
+
+# ---------------------------------------------------------------------------------------- NMF
+def nmf_update(a, num, den, eps=1e-6, out=None):
+    if out is None:
+        out = torch.empty_like(a)
+    check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), stream()), "dfm_nmf_update")
+    return out
+
+
+def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6):
+    if ga is None:
+        ga = torch.empty_like(a)
+        accumulate = False
+    gnum = torch.empty_like(a)
+    gden = torch.empty_like(a)
+    check(lib.dfm_nmf_update_bwd(a.numel(), ptr(g), ptr(a), ptr(num), ptr(den), ptr(out), eps, ptr(ga),
+                                 int(accumulate), ptr(gnum), ptr(gden), stream()), "dfm_nmf_update_bwd")
+    return ga, gnum, gden
+
+
+def softmax_rows(x):
+    y = torch.empty_like(x)
+    check(lib.dfm_softmax_rows(x.numel() // x.shape[-1], x.shape[-1], ptr(x), ptr(y), stream()), "dfm_softmax_rows")
+    return y
+
+
+def softmax_rows_bwd(y, dy, dx=None, accumulate=False):
+    if dx is None:
+        dx = torch.empty_like(y)
+        accumulate = False
+    check(lib.dfm_softmax_rows_bwd(y.numel() // y.shape[-1], y.shape[-1], ptr(y), ptr(dy), ptr(dx), int(accumulate),
+                                   stream()), "dfm_softmax_rows_bwd")
+    return dx
+
+
+# --------------------------------------------------------------------------------------- loss
+def seg_loss_fwd(logits, B, h, w, ncls, label, ignore=255):
+    H, W = label.shape[-2:]
+    out = torch.empty(2, device=logits.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_seg_loss_workspace(B, H, W), logits.device)
+    check(lib.dfm_seg_loss_fwd(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore, None,
+                               ptr(out), ptr(ws), stream()), "dfm_seg_loss_fwd")
+    return out
+
+
+def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255):
+    H, W = label.shape[-2:]
+    dl = torch.empty(B * h * w, ncls, device=logits.device, dtype=torch.float32)
+    check(lib.dfm_seg_loss_bwd(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore, None,
+                               ptr(loss_out), ptr(gscale), ptr(dl), stream()), "dfm_seg_loss_bwd")
+    return dl
+
+
+# -------------------------------------------------------------------------------------- AdamW
+def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None):
+    check(lib.dfm_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), lr, beta1, beta2, eps, weight_decay, step,
+                        grad_scale, ptr(bf16_copy), stream()), "dfm_adamw")

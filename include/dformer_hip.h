@@ -1,0 +1,216 @@
+/* dformer_hip.h — C ABI of libdformer_hip.so, the MI355X (gfx950) kernels behind DFormer's
+ * encoder Block and segmentation decoders.
+ *
+ * Contract:
+ *   - plain pointers (device memory) + sizes/strides in ELEMENTS; no torch types;
+ *   - the caller owns every buffer, including workspaces (query the *_workspace functions);
+ *     the library never allocates, never synchronises the host, and only enqueues on `stream`
+ *     (a hipStream_t passed as void*; NULL = default stream);
+ *   - return 0 on success, negative on bad arguments / unsupported dtype / launch failure;
+ *     dfm_last_error() returns a thread-local message for the last failure;
+ *   - dtype selects the storage type of activations: DFM_F32 or DFM_BF16. Statistics,
+ *     accumulators, LayerNorm / BatchNorm affine params, biases, depthwise weights and
+ *     gradients of parameters are always float32.
+ *   - layouts are NHWC ("channels-last"): pixel p of image b at row (b*H + h)*W + w,
+ *     channel c at column c; `ld*` is the row (pixel) stride so column slices of a wider
+ *     buffer can be read and written in place.
+ *
+ * Each entry point names the reference operation it replaces (file:line in
+ * Originofamonia/DFormer).
+ */
+#ifndef DFORMER_HIP_H
+#define DFORMER_HIP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFM_OK 0
+#define DFM_ERR_ARG (-1)
+#define DFM_ERR_DTYPE (-2)
+#define DFM_ERR_LAUNCH (-3)
+
+#define DFM_F32 0
+#define DFM_BF16 1
+
+typedef void* dfm_stream_t;
+
+const char* dfm_last_error(void);
+int dfm_abi_version(void);
+
+/* ---------------------------------------------------------------- GEMM (MFMA)
+ * C[b][m][n] = epilogue( alpha * sum_k A(b,m,k) * B(b,k,n) )
+ *   A(m,k) = A[m*lda + k] if a_kcontig else A[k*lda + m]
+ *   B(k,n) = B[n*ldb + k] if b_kcontig else B[k*ldb + n]
+ * Replaces every nn.Linear / 1x1 conv / torch.bmm on the hot path:
+ *   DFormer.py:76-95 (q, q_cut, a, l, kv, e_fore, e_back, proj, proj_e, short_cut_linear),
+ *   DFormer.py:53-55 (fc1, fc2), ham_head.py:46-145 (NMF bmm), ham_head.py:156-220 (1x1
+ *   ConvModules), decode_head.py:104 (conv_seg), MLPDecoder.py:14-57 (linear_c*, fuse, pred),
+ *   and their backward (dX = dY W: a_kcontig=1,b_kcontig=0; dW = dY^T X: both 0, split_k).
+ * Epilogue, in order (each optional):
+ *   v += beta * C_old ; v += bias[n] ; [n >= act_col0: preact[m,n-act_col0] = v ; v = act(v)
+ *   (1 gelu, 2 relu)] ;
+ *   v *= mul[m,n] ; v = res[m,n] + colscale[n] * rowscale[m / rows_per_scale] * v ;
+ *   C[m,n] = v (stored as dtype, or float32 when c_f32).
+ * Operands A, B, mul, res, preact are `dtype`; C is dtype or float32 (c_f32).
+ */
+typedef struct DfmGemmDesc {
+  int M, N, K;
+  int batch;
+  int a_kcontig, b_kcontig;
+  long lda, ldb, ldc;
+  long stride_a, stride_b, stride_c; /* batch strides, elements */
+  float alpha, beta;
+  int c_f32;
+  const float* bias;
+  int act;
+  void* preact;
+  long ldpre;
+  const void* mul;
+  long ldmul;
+  const void* res;
+  long ldres;
+  const float* colscale;
+  const float* rowscale;
+  long rows_per_scale;
+  int split_k;  /* 0 = auto, 1 = off, >1 = forced */
+  int act_col0; /* act / preact apply to columns n >= act_col0; preact[m, n - act_col0] */
+} DfmGemmDesc;
+
+size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);
+int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const void* B, void* C, void* workspace,
+             dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- LayerNorm, channels_last
+ * DFormer.py:21-45 (F.layer_norm over the last dim, eps 1e-6). mean/rstd: float32 [rows].
+ * bwd: dx (+= when accumulate), dgamma/dbeta float32 [C] (overwritten); workspace from
+ * dfm_layernorm_bwd_workspace. */
+int dfm_layernorm_fwd(int dtype, long rows, int C, const void* x, long ldx, const float* gamma,
+                      const float* beta, float eps, void* y, long ldy, float* mean, float* rstd,
+                      dfm_stream_t stream);
+size_t dfm_layernorm_bwd_workspace(long rows, int C);
+int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
+                      const float* gamma, const float* mean, const float* rstd, void* dx, long lddx,
+                      int accumulate, float* dgamma, float* dbeta, void* workspace, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- depthwise conv k x k, NHWC
+ * DFormer.py:80-81 (7x7 conv/e_conv, pad 3) and DFormer.py:54,62 (3x3 pos + identity).
+ * w: float32 [C][k][k], bias float32 [C] or NULL. add_identity: y += x. gelu_out (optional):
+ * GELU(y) as well (the ConvFFN activation, DFormer.py:64).
+ * bwd_data: dx (+= when accumulate) = conv(dy, flipped w) (+ dy when add_identity).
+ * bwd_weight: dw [C][k][k], db [C] (overwritten), workspace from dfm_dwconv_bwd_weight_workspace. */
+int dfm_dwconv_fwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const float* w,
+                   const float* bias, int add_identity, void* y, long ldy, void* gelu_out, long ldg,
+                   dfm_stream_t stream);
+int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k, const void* dy, long lddy,
+                        const float* w, int add_identity, void* dx, long lddx, int accumulate,
+                        dfm_stream_t stream);
+size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k);
+int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
+                          const void* dy, long lddy, float* dw, float* db, void* workspace,
+                          dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- reductions / elementwise */
+/* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)
+ * (bias grads: nn.Linear backward; layer_scale grads: DFormer.py:173-179). */
+size_t dfm_colsum_workspace(long rows, int C);
+int dfm_colsum(int dtype, long rows, int C, const void* x, long ldx, const void* mul, long ldmul,
+               const float* rowscale, long rows_per_scale, float* out, int accumulate, void* workspace,
+               dfm_stream_t stream);
+/* y = op(x): 0 copy/cast, used for float32 <-> bf16 conversion (dtype_in, dtype_out). */
+int dfm_cast(int dtype_in, int dtype_out, long n, const void* x, void* y, dfm_stream_t stream);
+/* dx (+= when accumulate) = dy * gelu'(pre)   (nn.GELU backward, DFormer.py:56,97,113) */
+int dfm_gelu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* pre, long ldpre,
+                 void* dx, long lddx, int accumulate, dfm_stream_t stream);
+/* dst (+= when accumulate) = alpha * src * (mul ? mul : 1) * (colscale ? colscale[c] : 1)
+ *   * (rowscale ? rowscale[r/rps] : 1)   — the residual / layer-scale / DropPath chain rule
+ *   (DFormer.py:173-179) and q*a, cx*xe products (DFormer.py:134-135). */
+int dfm_scale_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* mul, long ldmul,
+                  const float* colscale, const float* rowscale, long rows_per_scale, float alpha,
+                  void* dst, long lddst, int accumulate, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- pooled-query attention
+ * AdaptiveAvgPool2d(7) over NHWC (DFormer.py:92,124): y[b][i*7+j][c] = bin mean. */
+int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, const void* x, long ldx, void* y,
+                           long ldy, dfm_stream_t stream);
+int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, const void* dy, long lddy, void* dx,
+                           long lddx, int accumulate, dfm_stream_t stream);
+/* F.interpolate(bilinear, align_corners=False) NHWC [B,Hi,Wi,C] -> [B,Ho,Wo,C]
+ * (DFormer.py:131, ham_head.py:226-231, MLPDecoder.py:67-73, builder.py:203). */
+int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* x, long ldx,
+                     void* y, long ldy, int accumulate, dfm_stream_t stream);
+int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* dy, long lddy,
+                     void* dx, long lddx, int accumulate, dfm_stream_t stream);
+/* softmax(q*scale k^T) v for 49 pooled queries over N keys, per (b, head) (DFormer.py:119-130).
+ * q: [B][49][ldq] head h at cols h*dh; k, v: [B][N][ldkv] head h at cols h*dh; o like q.
+ * lse: float32 [B][heads][49] saved for backward. */
+size_t dfm_pooled_attn_workspace(int B, int heads, int N, int dh);
+int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, const void* q, long ldq, const void* k,
+                        const void* v, long ldkv, float scale, void* o, long ldo, float* lse,
+                        void* workspace, dfm_stream_t stream);
+int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, const void* q, long ldq, const void* k,
+                        const void* v, long ldkv, float scale, const void* o, long ldo, const void* dout,
+                        long lddo, const float* lse, void* dq, void* dk, void* dv, long lddkv,
+                        void* workspace, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- BatchNorm (+ SyncBN stats)
+ * mmcv ConvModule norm / nn.BatchNorm2d / SyncBatchNorm over NHWC rows (ham_head.py:204-220,
+ * MLPDecoder.py:53). stats: float32 [2][C] = (sum, sumsq) to be all-reduced by the caller for
+ * SyncBN. apply: y = act((x - mean) * rstd * gamma + beta) [+ res] ; mean/rstd float32 [C]. */
+size_t dfm_bn_workspace(long rows, int C);
+int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx, float* stats, void* workspace,
+                 dfm_stream_t stream);
+int dfm_bn_finalize(int C, const float* stats, double count, float eps, float momentum, float* mean,
+                    float* rstd, float* running_mean, float* running_var, dfm_stream_t stream);
+int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx, const float* mean, const float* rstd,
+                 const float* gamma, const float* beta, const void* res, long ldres, int act, void* y,
+                 long ldy, dfm_stream_t stream);
+/* bwd: given dy (already multiplied by the activation mask by the caller) compute
+ * stats2 float32 [2][C] = (sum dy, sum dy*xhat) ; then dx = gamma*rstd*(dy - s0/n - xhat*s1/n). */
+int dfm_bn_bwd_stats(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
+                     const float* mean, const float* rstd, float* stats2, void* workspace, dfm_stream_t stream);
+int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
+                     const float* mean, const float* rstd, const float* gamma, const float* stats2,
+                     double count, void* dx, long lddx, int accumulate, dfm_stream_t stream);
+/* act backward helper: dst = dy * (y > 0) (ReLU backward given the ReLU output) */
+int dfm_relu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* y, long ldy, void* dx,
+                 long lddx, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- NMF2D multiplicative update
+ * ham_head.py:120-145:  out = a * num / (den + eps)  (float32), and its backward:
+ *   ga (+= when accumulate_ga) = g * num / (den+eps);  gnum = g * a / (den+eps);
+ *   gden = -g * out / (den+eps). */
+int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
+                   dfm_stream_t stream);
+int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
+                       const float* out, float eps, float* ga, int accumulate_ga, float* gnum, float* gden,
+                       dfm_stream_t stream);
+/* row softmax over R (NMF coef init, ham_head.py:48-49) and its backward */
+int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream);
+int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int accumulate,
+                         dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- segmentation loss
+ * builder.py:203,230: logits [B,h,w,ncls] (NHWC, low res) bilinearly upsampled to [B,H,W]
+ * + cross-entropy(ignore_index) + mean over valid pixels. Fused: the full-resolution logits are
+ * never materialised. loss_out: float32 [2] = (sum of CE, valid count). dlogits float32 low-res; gscale: device float32 scalar (upstream grad) or NULL = 1. */
+size_t dfm_seg_loss_workspace(int B, int H, int W);
+int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
+                     const long* label, int ignore, float* lse, float* loss_out, void* workspace,
+                     dfm_stream_t stream);
+int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
+                     const long* label, int ignore, const float* lse, const float* loss_out,
+                     const float* gscale, float* dlogits, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- optimizer
+ * torch.optim.AdamW step (train.py:210-216) over a flat float32 parameter buffer; optional
+ * bf16 shadow copy for the next step's GEMM operands. grad_scale multiplies g (1/world). */
+int dfm_adamw(long n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
+              float eps, float weight_decay, int step, float grad_scale, void* bf16_copy,
+              dfm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFORMER_HIP_H */

@@ -1,0 +1,303 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from dformer_amd import kernels  # noqa: F401
+    torch.manual_seed(0)
+
+
+def K():
+    from dformer_amd import kernels
+    return kernels
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2}
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,Kd", [(300, 64, 64), (1000, 160, 96), (77, 33, 40), (4096, 512, 128), (5, 7, 16),
+                                    (640, 1024, 256)])
+def test_gemm_layouts(dt, M, N, Kd):
+    k = K()
+    x = torch.randn(M, Kd, device=DEV).to(dt)
+    w = torch.randn(N, Kd, device=DEV).to(dt)
+    b = torch.randn(N, device=DEV)
+    y = k.linear(x, w, b)
+    ref = x.float() @ w.float().t() + b
+    assert rel(y.float(), ref) < TOL[dt]
+    dy = torch.randn(M, N, device=DEV).to(dt)
+    dx = k.linear_dgrad(dy, w)
+    assert rel(dx.float(), dy.float() @ w.float()) < TOL[dt]
+    dw = k.linear_wgrad(dy, x)
+    assert dw.dtype == torch.float32
+    assert rel(dw, dy.float().t() @ x.float()) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_splitk_and_strided(dt):
+    k = K()
+    big = torch.randn(20000, 96, device=DEV).to(dt)
+    x = big[:, 16:80]  # strided view, ld=96
+    dy = torch.randn(20000, 48, device=DEV).to(dt)
+    dw = k.linear_wgrad(dy, x)
+    assert rel(dw, dy.float().t() @ x.float()) < TOL[dt]
+    acc = torch.randn(48, 64, device=DEV)
+    ref = acc + dy.float().t() @ x.float()
+    k.linear_wgrad(dy, x, out=acc, accumulate=True)
+    assert rel(acc, ref) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_epilogues(dt):
+    k = K()
+    M, N, Kd = 513, 96, 64
+    x = torch.randn(M, Kd, device=DEV).to(dt)
+    w = torch.randn(N, Kd, device=DEV).to(dt)
+    b = torch.randn(N, device=DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=dt)
+    y = k.linear(x, w, b, act=1, preact=pre)
+    lin = x.float() @ w.float().t() + b
+    assert rel(pre.float(), lin) < TOL[dt]
+    assert rel(y.float(), F.gelu(lin)) < TOL[dt]
+    mul = torch.randn(M, N, device=DEV).to(dt)
+    res = torch.randn(M, N, device=DEV).to(dt)
+    cs = torch.rand(N, device=DEV)
+    rs = torch.rand(3, device=DEV)
+    y = k.linear(x, w, b, mul=mul, res=res, colscale=cs, rowscale=rs, rows_per_scale=171)
+    rsx = rs.repeat_interleave(171)[:M, None]
+    assert rel(y.float(), res.float() + cs * rsx * (lin * mul.float())) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", [torch.float32])
+def test_bmm_layouts(dt):
+    k = K()
+    a = torch.randn(3, 70, 40, device=DEV, dtype=dt)
+    b = torch.randn(3, 40, 24, device=DEV, dtype=dt)
+    assert rel(k.bmm(a, b), a @ b) < TOL[dt]
+    at = a.transpose(1, 2).contiguous()
+    assert rel(k.bmm(at, b, a_t=True), a @ b) < TOL[dt]
+    bt = b.transpose(1, 2).contiguous()
+    assert rel(k.bmm(a, bt, b_t=True), a @ b) < TOL[dt]
+    assert rel(k.bmm(at, bt, a_t=True, b_t=True), a @ b) < TOL[dt]
+    # odd N (not a multiple of the vector width): NMF at 530x730 (N = 67*92)
+    x = torch.rand(2, 64, 6164, device=DEV)
+    c = torch.rand(2, 6164, 32, device=DEV)
+    assert rel(k.bmm(x, c), x @ c) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("C", [16, 32, 64, 96, 288, 576])
+def test_layernorm(dt, C):
+    k = K()
+    x = (torch.randn(1037, C, device=DEV) * 2 + 0.5).to(dt)
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    y, mean, rstd = k.layernorm(x, g, b, 1e-6)
+    xr = x.float().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = F.layer_norm(xr, (C,), gr, br, 1e-6)
+    assert rel(y.float(), ref) < TOL[dt]
+    dy = torch.randn(1037, C, device=DEV).to(dt)
+    ref.backward(dy.float())
+    dx, dg, db = k.layernorm_bwd(x, dy, g, mean, rstd)
+    assert rel(dx.float(), xr.grad) < TOL[dt] * 2
+    assert rel(dg, gr.grad) < TOL[dt] * 2
+    assert rel(db, br.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("ks,ident", [(7, False), (3, True)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16)])
+def test_dwconv(dt, ks, ident, B, H, W, C):
+    k = K()
+    x = torch.randn(B, H, W, C, device=DEV).to(dt)
+    w = torch.randn(C, 1, ks, ks, device=DEV) / ks
+    bias = torch.randn(C, device=DEV)
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    wr, br = w.clone().requires_grad_(), bias.clone().requires_grad_()
+    ref = F.conv2d(xr, wr, br, padding=ks // 2, groups=C)
+    if ident:
+        ref = ref + xr
+    y = k.dwconv(x.view(-1, C), (B, H, W), w, bias, ks, ident)
+    assert rel(y.float().view(B, H, W, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    dy = torch.randn(B, H, W, C, device=DEV).to(dt)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = k.dwconv_bwd_data(dy.view(-1, C), (B, H, W), w, ks, ident)
+    assert rel(dx.float().view(B, H, W, C).permute(0, 3, 1, 2), xr.grad) < TOL[dt]
+    dw, db = k.dwconv_bwd_weight(x.view(-1, C), dy.view(-1, C), (B, H, W), ks)
+    assert rel(dw, wr.grad) < TOL[dt] * 2
+    assert rel(db, br.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("H,W", [(15, 20), (8, 10), (5, 7), (60, 80), (17, 23)])
+def test_pool7(dt, H, W):
+    k = K()
+    B, C = 2, 40
+    x = torch.randn(B, H, W, C, device=DEV).to(dt)
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    ref = F.adaptive_avg_pool2d(xr, 7)
+    y = k.pool7(x.view(-1, C), (B, H, W))
+    assert rel(y.float().view(B, 7, 7, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    dy = torch.randn(B, 7, 7, C, device=DEV).to(dt)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = k.pool7_bwd(dy.view(-1, C), (B, H, W))
+    assert rel(dx.float().view(B, H, W, C).permute(0, 3, 1, 2), xr.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("hi,ho", [((7, 7), (15, 20)), ((7, 7), (5, 7)), ((30, 40), (60, 80)), ((15, 20), (60, 80)),
+                                   ((60, 80), (480, 640)), ((34, 46), (133, 183))])
+def test_bilinear(dt, hi, ho):
+    k = K()
+    B, C = 2, 24
+    x = torch.randn(B, *hi, C, device=DEV).to(dt)
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    ref = F.interpolate(xr, ho, mode="bilinear", align_corners=False)
+    y = k.bilinear(x.view(-1, C), hi, ho, B)
+    assert rel(y.float().view(B, *ho, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    dy = torch.randn(B, *ho, C, device=DEV).to(dt)
+    ref.backward(dy.float().permute(0, 3, 1, 2))
+    dx = k.bilinear_bwd(dy.view(-1, C), hi, ho, B)
+    assert rel(dx.float().view(B, *hi, C).permute(0, 3, 1, 2), xr.grad) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,heads,N,dh", [(2, 2, 300, 32), (1, 4, 1200, 32), (2, 1, 37, 16), (1, 2, 150, 48),
+                                         (2, 4, 99, 36)])
+def test_pooled_attention(dt, B, heads, N, dh):
+    k = K()
+    C2 = heads * dh
+    q = torch.randn(B * 49, C2, device=DEV).to(dt)
+    kv = torch.randn(B * N, 2 * C2, device=DEV).to(dt)
+    scale = dh ** -0.5
+    o, lse = k.pooled_attn(q, kv[:, :C2], kv[:, C2:], B, heads, N, dh, scale)
+    qr = q.float().view(B, 49, heads, dh).permute(0, 2, 1, 3).requires_grad_()
+    kr = kv.float()[:, :C2].reshape(B, N, heads, dh).permute(0, 2, 1, 3).contiguous().requires_grad_()
+    vr = kv.float()[:, C2:].reshape(B, N, heads, dh).permute(0, 2, 1, 3).contiguous().requires_grad_()
+    ref = ((qr * scale) @ kr.transpose(-2, -1)).softmax(-1) @ vr
+    assert rel(o.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), ref) < TOL[dt]
+    do = torch.randn(B * 49, C2, device=DEV).to(dt)
+    ref.backward(do.float().view(B, 49, heads, dh).permute(0, 2, 1, 3))
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    k.pooled_attn_bwd(q, kv[:, :C2], kv[:, C2:], o, do, lse, B, heads, N, dh, scale, dq, dkv[:, :C2], dkv[:, C2:])
+    assert rel(dq.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), qr.grad) < TOL[dt] * 2
+    assert rel(dkv[:, :C2].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), kr.grad) < TOL[dt] * 2
+    assert rel(dkv[:, C2:].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), vr.grad) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_colsum_and_elementwise(dt):
+    k = K()
+    x = torch.randn(5000, 72, device=DEV).to(dt)
+    m = torch.randn(5000, 72, device=DEV).to(dt)
+    rs = torch.rand(4, device=DEV)
+    s = k.colsum(x, mul=m, rowscale=rs, rows_per_scale=1250)
+    ref = (x.float() * m.float() * rs.repeat_interleave(1250)[:, None]).sum(0)
+    assert rel(s, ref) < TOL[dt]
+    pre = torch.randn(5000, 72, device=DEV).to(dt)
+    g = k.gelu_bwd(x, pre)
+    pr = pre.float().requires_grad_()
+    F.gelu(pr).backward(x.float())
+    assert rel(g.float(), pr.grad) < TOL[dt]
+    y = k.scale_mul(x, mul=m, colscale=torch.rand(72, device=DEV))
+    assert y.shape == x.shape
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_batchnorm(dt):
+    k = K()
+    x = (torch.randn(3000, 64, device=DEV) * 3 + 1).to(dt)
+    g = torch.rand(64, device=DEV) + 0.5
+    b = torch.randn(64, device=DEV)
+    rm, rv = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    st = k.bn_stats(x)
+    mean, rstd = k.bn_finalize(st, 3000, 1e-3, 0.1, rm, rv)
+    y = k.bn_apply(x, mean, rstd, g, b, act=2)
+    xr = x.float().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    rm2, rv2 = torch.zeros(64, device=DEV), torch.ones(64, device=DEV)
+    ref = F.relu(F.batch_norm(xr, rm2, rv2, gr, br, True, 0.1, 1e-3))
+    assert rel(y.float(), ref) < TOL[dt]
+    assert rel(rm, rm2) < 1e-4 and rel(rv, rv2) < 1e-4
+    dy = torch.randn(3000, 64, device=DEV).to(dt)
+    ref.backward(dy.float())
+    dyr = k.relu_bwd(dy, y)
+    st2 = k.bn_bwd_stats(x, dyr, mean, rstd)
+    dx = k.bn_bwd_apply(x, dyr, mean, rstd, g, st2, 3000)
+    assert rel(dx.float(), xr.grad) < TOL[dt] * 2
+    assert rel(st2[1] , gr.grad) < TOL[dt] * 2
+    assert rel(st2[0], br.grad) < TOL[dt] * 2
+
+
+def test_nmf_update_softmax():
+    k = K()
+    a, num, den = (torch.rand(4, 100, 64, device=DEV) for _ in range(3))
+    out = k.nmf_update(a, num, den)
+    assert rel(out, a * num / (den + 1e-6)) < 1e-6
+    ar, nr, dr = (t.clone().requires_grad_() for t in (a, num, den))
+    o2 = ar * nr / (dr + 1e-6)
+    g = torch.randn_like(o2)
+    o2.backward(g)
+    ga, gn, gd = k.nmf_update_bwd(g, a, num, den, out)
+    assert rel(ga, ar.grad) < 1e-5 and rel(gn, nr.grad) < 1e-5 and rel(gd, dr.grad) < 1e-5
+    x = torch.randn(500, 64, device=DEV)
+    y = k.softmax_rows(x)
+    assert rel(y, x.softmax(-1)) < 1e-5
+    xr = x.clone().requires_grad_()
+    gy = torch.randn(500, 64, device=DEV)
+    xr.softmax(-1).backward(gy)
+    assert rel(k.softmax_rows_bwd(y, gy), xr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (1, 17, 23, 67, 92, 37), (2, 8, 12, 64, 96, 40)])
+def test_seg_loss(dt, B, h, w, H, W, ncls):
+    k = K()
+    lg = torch.randn(B, h, w, ncls, device=DEV).to(dt)
+    lab = torch.randint(0, ncls, (B, H, W), device=DEV)
+    lab[torch.rand(B, H, W, device=DEV) < 0.1] = 255
+    out = k.seg_loss_fwd(lg.view(-1, ncls), B, h, w, ncls, lab)
+    lr = lg.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    up = F.interpolate(lr, (H, W), mode="bilinear", align_corners=False)
+    ce = F.cross_entropy(up, lab, reduction="none", ignore_index=255)
+    loss = ce[lab != 255].mean()
+    assert abs((out[0] / out[1]).item() - loss.item()) < 1e-4 * abs(loss.item())
+    loss.backward()
+    dl = k.seg_loss_bwd(lg.view(-1, ncls), B, h, w, ncls, lab, out)
+    assert rel(dl.view(B, h, w, ncls).permute(0, 3, 1, 2), lr.grad) < 1e-3
+
+
+def test_adamw_matches_torch():
+    k = K()
+    p = torch.randn(10000, device=DEV)
+    g = torch.randn(10000, device=DEV)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    pr = p.clone().requires_grad_()
+    opt = torch.optim.AdamW([pr], lr=6e-5, betas=(0.9, 0.999), weight_decay=0.01)
+    copy = torch.empty(10000, device=DEV, dtype=torch.bfloat16)
+    for step in range(1, 4):
+        pr.grad = g * step
+        opt.step()
+        k.adamw(p, g * step, m, v, 6e-5, 0.9, 0.999, 1e-8, 0.01, step, 1.0, copy)
+    assert rel(p, pr.detach()) < 1e-6
+    assert rel(copy.float(), p) < 1e-2
