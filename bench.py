@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""DFormer-Base + ham decoder, 480x640, bs=16 per GPU, bf16 training-step throughput (images/s).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL over xGMI)
+
+One step = forward + fused CE loss + backward (bucketed RCCL all-reduce overlapped) + fused AdamW,
+on synthetic inputs resident in HBM (BASELINE.json config 3 / 4). Rank 0 prints one JSON line with
+the whole-job images/s, the roofline of the dominant kernel and the CPU-oracle baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "images/s training-step, DFormer-B 480×640 bs=16/GPU, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def make_cfg(arch="DFormer-Base", decoder="ham", ncls=40):
+    # local_configs/NYUDepthv2/DFormer_Base.py + _base_/datasets/NYUDepthv2.py
+    return Cfg(backbone=arch, decoder=decoder, decoder_embed_dim=512, num_classes=ncls, drop_path_rate=0.1,
+               bn_eps=1e-3, bn_momentum=0.1, background=255, lr=6e-5, weight_decay=0.01)
+
+
+def synthetic_batch(B, H, W, ncls, device, seed):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1)
+    rgb = (torch.randint(0, 256, (B, 3, H, W), device=device, generator=g).float() / 255 - mean) / std
+    dep = (torch.randint(0, 256, (B, 1, H, W), device=device, generator=g).float() / 255 - 0.48) / 0.28
+    lab = torch.randint(0, ncls, (B, H, W), device=device, generator=g)
+    lab[torch.rand(B, H, W, device=device, generator=g) < 0.1] = 255
+    return rgb, dep, lab
+
+
+def measure_dominant_kernel(device, iters=50):
+    """Roofline of the dominant kernel family (MFMA GEMM): the ConvFFN fc2 GEMM of stage 0
+    (M = 16*120*160 pixels, K = 512 hidden, N = 64) as launched in the step, bf16, timed with HIP
+    events on the launching stream. Algorithmic bytes = read A (M*K) + B (N*K) + residual (M*N)
+    + write C and preact (2*M*N), 2 B each."""
+    from dformer_amd import kernels as K
+    M, Kd, N = 16 * 120 * 160, 512, 64
+    a = torch.randn(M, Kd, device=device).to(torch.bfloat16)
+    w = torch.randn(N, Kd, device=device).to(torch.bfloat16)
+    b = torch.randn(N, device=device)
+    res = torch.randn(M, N, device=device).to(torch.bfloat16)
+    pre = torch.empty(M, N, device=device, dtype=torch.bfloat16)
+    ls = torch.rand(N, device=device)
+    out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
+    for _ in range(5):
+        K.linear(a, w, b, preact=pre, res=res, colscale=ls, out=out)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        K.linear(a, w, b, preact=pre, res=res, colscale=ls, out=out)
+    e1.record(s)
+    e1.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / iters
+    nbytes = 2 * (M * Kd + N * Kd + 3 * M * N)
+    flops = 2 * M * N * Kd
+    ach = nbytes / sec / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "gemm_kernel<bf16,128x64> ConvFFN fc2 stage0 (M=307200,K=512,N=64)",
+            "avg_us": round(sec * 1e6, 2), "bytes_per_launch": nbytes, "tflops": round(flops / sec / 1e12, 1)}
+
+
+def cpu_baseline(model_sd, seconds=20.0):
+    """The CPU oracle (oracle/dformer_ref.py, parity-pinned to the reference goldens) timed on
+    this host: DFormer-B + ham fwd+bwd, fp32, bs=2 at 480x640 (SURVEY §8d CPU baseline)."""
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import dformer_ref as R
+    ncores = len(os.sched_getaffinity(0))
+    threads = max(1, min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores))))
+    torch.set_num_threads(threads)
+    p = {k: v.detach().float().cpu().clone().requires_grad_(v.is_floating_point() and "running" not in k)
+         for k, v in model_sd.items() if not k.endswith("num_batches_tracked")}
+    B, H, W = 2, 480, 640
+    rgb, dep, lab = synthetic_batch(B, H, W, 40, "cpu", 0)
+    g = torch.Generator().manual_seed(1)
+    bases = torch.rand(B, 512, 64, generator=g)
+    bases = bases / bases.norm(dim=1, keepdim=True)
+    n, t_total = 0, 0.0
+    while t_total < seconds and n < 20:
+        t0 = time.perf_counter()
+        _, _, loss = R.segmentor_forward(p, "DFormer-Base", "ham", rgb, dep, bases, True, lab)
+        loss.backward()
+        dt = time.perf_counter() - t0
+        if n > 0 or seconds < 1:  # first iteration is warm-up
+            t_total += dt
+        n += 1
+    timed = max(1, n - 1)
+    return {"value": round(B * timed / max(t_total, 1e-9), 3), "unit": "images/s", "cores": threads,
+            "kind": "port", "sample": f"oracle DFormer-B+ham fwd+bwd fp32 bs=2 480x640, {timed} timed iters"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--arch", default="DFormer-Base")
+    ap.add_argument("--decoder", default="ham")
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dformer_amd.segmentor import EncoderDecoder
+    from dformer_amd.train import FusedAdamW, train_step
+
+    torch.manual_seed(8964 + rank)
+    cfg = make_cfg(args.arch, args.decoder)
+    model = EncoderDecoder(cfg=cfg, syncbn=world > 1)
+    for m in model.decode_head.modules():  # init_func.init_weight: kaiming on decoder convs
+        if isinstance(m, torch.nn.Conv2d):
+            torch.nn.init.kaiming_normal_(m.weight, mode="fan_in", nonlinearity="relu")
+    sd_cpu = {k: v.clone() for k, v in model.state_dict().items()} if rank == 0 else None
+    model = model.to(dev).set_compute_dtype(torch.bfloat16)
+    if world > 1:
+        for t in model.state_dict().values():
+            dist.broadcast(t, 0)
+    model.return_logits = False
+    model.train()
+    opt = FusedAdamW(model, lr=cfg.lr, weight_decay=cfg.weight_decay, world=world, compute_dtype=torch.bfloat16)
+    rgb, dep, lab = synthetic_batch(args.batch, args.height, args.width, cfg.num_classes, dev, 8964 + rank)
+
+    for _ in range(args.warmup):
+        train_step(model, opt, rgb, dep, lab)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = train_step(model, opt, rgb, dep, lab)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = elapsed.item()
+    images = world * args.batch * args.steps
+    value = images / elapsed
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights)",
+        "config": {"workload": f"{args.arch}+{args.decoder} train step fwd+bwd+AdamW",
+                   "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                   "image": [args.height, args.width], "parallelism": f"dp{world}"},
+        "loss": round(float(loss.item()), 4) if loss is not None else None,
+    }
+    if rank == 0:
+        result["roofline"] = measure_dominant_kernel(dev)
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(sd_cpu, args.cpu_seconds)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -29,7 +29,7 @@ class GemmDesc(ctypes.Structure):
                 ("bias", P), ("act", c_int), ("preact", P), ("ldpre", c_long),
                 ("mul", P), ("ldmul", c_long), ("res", P), ("ldres", c_long),
                 ("colscale", P), ("rowscale", P), ("rows_per_scale", c_long), ("split_k", c_int),
-                ("act_col0", c_int)]
+                ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int)]
 
 
 # name -> (restype, argtypes)

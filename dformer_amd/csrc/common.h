@@ -57,6 +57,40 @@ template <int G> DFM_INLINE float group_sum(float v) {
   return v;
 }
 
+// ---- second stage of the deterministic two-stage column reductions:
+// out[e] (+)= sum_{b < nblk} part[b * n + e], fixed summation order; 64 columns x 16 row-lanes
+// per 1024-thread block so the nblk partials of a column are read by 16 lanes in parallel.
+//   MODE 0: out0[e]                      MODE 1: e < n0 ? out0[e] : out1[e - n0]
+//   MODE 2: depthwise layout, n0 = k*k+1: i = e % n0, c = e / n0 -> i < n0-1 ? out0[c*(n0-1)+i] : out1[c]
+template <int MODE>
+__global__ __launch_bounds__(1024) void partial_sum_kernel(int nblk, long n, const float* __restrict__ part,
+                                                           float* __restrict__ out0, float* __restrict__ out1, long n0,
+                                                           int accumulate) {
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const long e = blockIdx.x * 64L + cl;
+  float s = 0.f;
+  if (e < n) {
+#pragma unroll 4
+    for (int b = rl; b < nblk; b += 16) s += part[(long)b * n + e];
+  }
+  __shared__ float red[16][64];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && e < n) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += red[r][cl];
+    float* dst;
+    if (MODE == 0) dst = out0 + e;
+    else if (MODE == 1) dst = e < n0 ? out0 + e : out1 + (e - n0);
+    else {
+      const long c = e / n0, i = e % n0;
+      dst = i < n0 - 1 ? out0 + c * (n0 - 1) + i : (out1 ? out1 + c : nullptr);
+    }
+    if (dst) *dst = accumulate ? *dst + v : v;
+  }
+}
+
 // ---- host-side error plumbing (thread-local last error string)
 void dfm_set_error(const char* fmt, ...);
 #define DFM_CHECK_ARG(cond, ...)          \

@@ -238,8 +238,8 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   }
 #undef GO
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dw_wgrad_sum_kernel, dim3(cdiv(C * (k * k + 1), 256)), dim3(256), 0, s, nb, C, k * k + 1, part,
-                     dw, db);
+  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, nb,
+                     (long)C * (k * k + 1), (const float*)part, dw, db, (long)(k * k + 1), 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -71,8 +71,8 @@ int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, c
   hipLaunchKernelGGL((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x, ldx,
                      (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colred_sum_kernel, dim3(cdiv(NOUT * C, 256)), dim3(256), 0, s, nblk, NOUT * C, (const float*)ws,
-                     out, accumulate);
+  hipLaunchKernelGGL(partial_sum_kernel<0>, dim3(cdiv((long)NOUT * C, 64)), dim3(1024), 0, s, nblk, (long)NOUT * C,
+                     (const float*)ws, out, (float*)nullptr, 0L, accumulate);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -3,11 +3,15 @@
 // One templated kernel covers the three layouts of a linear layer's forward and backward:
 //   forward  Y  = X W^T   : A k-contiguous, B k-contiguous
 //   dgrad    dX = dY W    : A k-contiguous, B row-contiguous   (ds_read_b64_tr_b16 for B)
-//   wgrad    dW = dY^T X  : A row-contiguous, B row-contiguous (split-K over pixels)
+//   wgrad    dW = dY^T X  : A row-contiguous, B row-contiguous (split-K over pixels); the bias
+//                           gradient sum_p dY[p, :] rides along as a virtual all-ones column of X
 // bf16 operands use v_mfma_f32_16x16x32_bf16 (fp32 accumulate); float32 operands use the
 // exact-f32 v_mfma_f32_16x16x4_f32. Both operands are staged through a double-buffered LDS
 // tile filled by 16-byte register-staged loads; row-contiguous bf16 tiles are consumed with
 // the hardware transposing LDS read so no operand is ever transposed in memory.
+// The epilogue stages the fp32 accumulator tile through LDS (two row halves) and applies bias /
+// activation / multiplier / residual on 8-column vectors, so every global read and write of the
+// output side is a coalesced 16-byte access (these GEMMs are mostly HBM-bound: K <= 2048).
 #include "common.h"
 
 namespace {
@@ -17,7 +21,7 @@ struct GemmArgs {
   const void* B;
   void* C;
   float* ws;
-  int M, N, K, batch, splits;
+  int M, N, K, batch, splits, Nw;
   long lda, ldb, ldc, sa, sb, sc;
   float alpha, beta;
   int c_f32;
@@ -33,34 +37,43 @@ struct GemmArgs {
   const float* rowscale;
   long rps;
   int act_col0;
+  float* colsum;   // optional: colsum[m] (+)= alpha * sum_k A(m,k)  (virtual ones column of B)
+  int colsum_acc;
+  int ala, alb;    // operand rows 16-byte aligned (vector loads)
+  int vec_ok;      // output-side rows 16-byte aligned (vector epilogue)
 };
 
 template <typename T> struct Mf;
 template <> struct Mf<bf16_t> {
   static constexpr int VEC = 8;    // elements per 16-byte vector
   static constexpr int KSTEP = 32; // k per MFMA
-  static constexpr int BK = 64;
   static constexpr int PADK = 8;   // k-contiguous row pad (elements)
   static constexpr int PADR = 8;   // row-contiguous row pad (elements)
 };
 template <> struct Mf<float> {
   static constexpr int VEC = 4;
   static constexpr int KSTEP = 4;
-  static constexpr int BK = 32;
   static constexpr int PADK = 1;
   static constexpr int PADR = 16;
 };
 
 // Load one 16-byte vector (VEC elements) of operand tile element (r, k..k+VEC) or (k, r..r+VEC)
 // with zero fill outside [0, rows) x [0, K).
-template <typename T, bool KC, bool ALIGNED>
-DFM_INLINE uint4 load_vec(const T* __restrict__ p, long ld, int r, int k, int rows, int K) {
+template <typename T, bool KC>
+DFM_INLINE uint4 load_vec(const T* __restrict__ p, long ld, int r, int k, int rows, int K, bool aligned,
+                          int ones_r) {
   constexpr int VEC = Mf<T>::VEC;
   uint4 out = make_uint4(0, 0, 0, 0);
   if (KC) {
+    if (r == ones_r) {  // virtual all-ones row (bias-gradient column of a wgrad GEMM)
+      T tmp[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) tmp[e] = Num<T>::from_f(k + e < K ? 1.0f : 0.0f);
+      return *reinterpret_cast<uint4*>(tmp);
+    }
     if (r >= rows) return out;
     const T* src = p + (long)r * ld + k;
-    if (ALIGNED && k + VEC <= K) return *reinterpret_cast<const uint4*>(src);
+    if (aligned && k + VEC <= K) return *reinterpret_cast<const uint4*>(src);
     T tmp[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) tmp[e] = (k + e < K) ? src[e] : T(0);
@@ -68,50 +81,51 @@ DFM_INLINE uint4 load_vec(const T* __restrict__ p, long ld, int r, int k, int ro
   } else {
     if (k >= K) return out;
     const T* src = p + (long)k * ld + r;
-    if (ALIGNED && r + VEC <= rows) return *reinterpret_cast<const uint4*>(src);
+    if (aligned && r + VEC <= rows) return *reinterpret_cast<const uint4*>(src);
     T tmp[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) tmp[e] = (r + e < rows) ? src[e] : T(0);
+    for (int e = 0; e < VEC; ++e) tmp[e] = (r + e < rows) ? src[e] : Num<T>::from_f(r + e == ones_r ? 1.0f : 0.0f);
     return *reinterpret_cast<uint4*>(tmp);
   }
 }
 
-template <typename T, int R, bool KC>
+template <typename T, int R, int BK, bool KC>
 struct TileGeom {
-  static constexpr int BK = Mf<T>::BK;
   static constexpr int VEC = Mf<T>::VEC;
   // k-contiguous: [R][BK+PADK]; row-contiguous: [BK][R+PADR]
   static constexpr int LD = KC ? (BK + Mf<T>::PADK) : (R + Mf<T>::PADR);
   static constexpr int ELEMS = KC ? R * LD : BK * LD;
-  static constexpr int NVEC = R * BK / VEC / 256;  // vectors per thread
-  static_assert(NVEC >= 1, "tile too small");
+  static constexpr int TOTAL = R * BK / VEC;        // 16-byte vectors per tile
+  static constexpr int NVEC = (TOTAL + 255) / 256;  // vectors per thread (last one partial)
 };
 
-template <typename T, int R, bool KC, bool ALIGNED>
-DFM_INLINE void stage_load(uint4* regs, const T* __restrict__ base, long ld,
-                           int r0, int k0, int rows, int K) {
-  using G = TileGeom<T, R, KC>;
-  constexpr int VEC = G::VEC, BK = G::BK;
+template <typename T, int R, int BK, bool KC>
+DFM_INLINE void stage_load(uint4* regs, const T* __restrict__ base, long ld, int r0, int k0, int rows, int K,
+                           bool aligned, int ones_r = -1) {
+  using G = TileGeom<T, R, BK, KC>;
+  constexpr int VEC = G::VEC;
 #pragma unroll
   for (int i = 0; i < G::NVEC; ++i) {
     const int v = threadIdx.x + i * 256;
+    if (G::TOTAL % 256 != 0 && v >= G::TOTAL) break;
     if (KC) {
       const int r = v / (BK / VEC), kc = (v % (BK / VEC)) * VEC;
-      regs[i] = load_vec<T, true, ALIGNED>(base, ld, r0 + r, k0 + kc, rows, K);
+      regs[i] = load_vec<T, true>(base, ld, r0 + r, k0 + kc, rows, K, aligned, ones_r);
     } else {
       const int k = v / (R / VEC), rc = (v % (R / VEC)) * VEC;
-      regs[i] = load_vec<T, false, ALIGNED>(base, ld, r0 + rc, k0 + k, rows, K);
+      regs[i] = load_vec<T, false>(base, ld, r0 + rc, k0 + k, rows, K, aligned, ones_r);
     }
   }
 }
 
-template <typename T, int R, bool KC>
+template <typename T, int R, int BK, bool KC>
 DFM_INLINE void stage_store(const uint4* regs, T* lds) {
-  using G = TileGeom<T, R, KC>;
-  constexpr int VEC = G::VEC, BK = G::BK;
+  using G = TileGeom<T, R, BK, KC>;
+  constexpr int VEC = G::VEC;
 #pragma unroll
   for (int i = 0; i < G::NVEC; ++i) {
     const int v = threadIdx.x + i * 256;
+    if (G::TOTAL % 256 != 0 && v >= G::TOTAL) break;
     if (KC) {
       const int r = v / (BK / VEC), kc = (v % (BK / VEC)) * VEC;
       *reinterpret_cast<uint4*>(lds + r * G::LD + kc) = regs[i];
@@ -146,12 +160,15 @@ DFM_INLINE float frag_f32(const float* lds, int r0, int k0, int lane) {
   return lds[(k0 + (lane >> 4)) * LD + r0 + (lane & 15)];
 }
 
+// ---- epilogue (scalar element)
 template <typename TO>
 DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) {
-  if (a.beta != 0.0f) {
-    if (a.c_f32) v += a.beta * ((const float*)a.C)[b * a.sc + (long)m * a.ldc + n];
-    else v += a.beta * ldf((const TO*)a.C + b * a.sc + (long)m * a.ldc + n);
+  if (n == a.N) {  // virtual ones column -> row sums (bias gradient)
+    a.colsum[m] = a.colsum_acc ? a.colsum[m] + v : v;
+    return;
   }
+  const long ci = b * a.sc + (long)m * a.ldc + n;
+  if (a.beta != 0.0f) v += a.beta * (a.c_f32 ? ((const float*)a.C)[ci] : ldf((const TO*)a.C + ci));
   if (a.bias) v += a.bias[n];
   if (n >= a.act_col0) {
     if (a.preact) stf((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), v);
@@ -164,18 +181,84 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
     if (a.rowscale) s *= a.rowscale[m / a.rps];
     v = ldf((const TO*)a.res + (long)m * a.ldres + n) + s * v;
   }
-  if (a.c_f32) ((float*)a.C)[b * a.sc + (long)m * a.ldc + n] = v;
-  else stf((TO*)a.C + b * a.sc + (long)m * a.ldc + n, v);
+  if (a.c_f32) ((float*)a.C)[ci] = v;
+  else stf((TO*)a.C + ci, v);
 }
 
-template <typename T, int BM, int BN, int WAVES_M, bool AK, bool BKC, bool ALA, bool ALB>
+// 8 consecutive T elements <-> floats
+template <typename T> DFM_INLINE void ld8(const T* p, float* v);
+template <> DFM_INLINE void ld8<bf16_t>(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+template <> DFM_INLINE void ld8<float>(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <typename T> DFM_INLINE void st8(T* p, const float* v);
+template <> DFM_INLINE void st8<bf16_t>(bf16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <> DFM_INLINE void st8<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+template <typename TO>
+DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
+  const long ci = b * a.sc + (long)m * a.ldc + n;
+  float t[8];
+  if (a.beta != 0.0f) {
+    if (a.c_f32) ld8<float>((const float*)a.C + ci, t);
+    else ld8<TO>((const TO*)a.C + ci, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += a.beta * t[e];
+  }
+  if (a.bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
+  }
+  if (n >= a.act_col0) {  // act_col0 is a multiple of 8 whenever the vector path is taken
+    if (a.preact) st8<TO>((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), v);
+    if (a.act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
+    } else if (a.act == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
+    }
+  }
+  if (a.mul) {
+    ld8<TO>((const TO*)a.mul + (long)m * a.ldmul + n, t);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= t[e];
+  }
+  if (a.res) {
+    ld8<TO>((const TO*)a.res + (long)m * a.ldres + n, t);
+    const float rs = a.rowscale ? a.rowscale[m / a.rps] : 1.0f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = t[e] + (a.colscale ? a.colscale[n + e] : 1.0f) * rs * v[e];
+  }
+  if (a.c_f32) st8<float>((float*)a.C + ci, v);
+  else st8<TO>((TO*)a.C + ci, v);
+}
+
+template <typename T, int BM, int BN, int WAVES_M, int BK, bool AK, bool BKC>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   constexpr int WAVES_N = 4 / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int BK = Mf<T>::BK, KSTEP = Mf<T>::KSTEP;
-  using GA = TileGeom<T, BM, AK>;
-  using GB = TileGeom<T, BN, BKC>;
+  constexpr int KSTEP = Mf<T>::KSTEP;
+  using GA = TileGeom<T, BM, BK, AK>;
+  using GB = TileGeom<T, BN, BK, BKC>;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* const lds_base = reinterpret_cast<T*>(smem);
@@ -190,6 +273,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   const int kper = ((a.K + a.splits - 1) / a.splits + BK - 1) / BK * BK;
   const int kbeg = split * kper;
   const int kend = min(a.K, kbeg + kper);
+  const int ones_r = a.colsum != nullptr ? a.N : -1;
 
   const T* A = (const T*)a.A + (long)b * a.sa;
   const T* Bp = (const T*)a.B + (long)b * a.sb;
@@ -203,18 +287,18 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   uint4 ra[GA::NVEC], rb[GB::NVEC];
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    stage_load<T, BM, AK, ALA>(ra, A, a.lda, bm, kbeg, a.M, kend);
-    stage_load<T, BN, BKC, ALB>(rb, Bp, a.ldb, bn, kbeg, a.N, kend);
-    stage_store<T, BM, AK>(ra, LDS_A(0));
-    stage_store<T, BN, BKC>(rb, LDS_B(0));
+    stage_load<T, BM, BK, AK>(ra, A, a.lda, bm, kbeg, a.M, kend, a.ala);
+    stage_load<T, BN, BK, BKC>(rb, Bp, a.ldb, bn, kbeg, a.N, kend, a.alb, ones_r);
+    stage_store<T, BM, BK, AK>(ra, LDS_A(0));
+    stage_store<T, BN, BK, BKC>(rb, LDS_B(0));
   }
   __syncthreads();
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
-      stage_load<T, BM, AK, ALA>(ra, A, a.lda, bm, kbeg + (kt + 1) * BK, a.M, kend);
-      stage_load<T, BN, BKC, ALB>(rb, Bp, a.ldb, bn, kbeg + (kt + 1) * BK, a.N, kend);
+      stage_load<T, BM, BK, AK>(ra, A, a.lda, bm, kbeg + (kt + 1) * BK, a.M, kend, a.ala);
+      stage_load<T, BN, BK, BKC>(rb, Bp, a.ldb, bn, kbeg + (kt + 1) * BK, a.N, kend, a.alb, ones_r);
     }
     const T* la = LDS_A(cur);
     const T* lb = LDS_B(cur);
@@ -245,87 +329,117 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
       }
     }
     if (more) {
-      stage_store<T, BM, AK>(ra, LDS_A(cur ^ 1));
-      stage_store<T, BN, BKC>(rb, LDS_B(cur ^ 1));
+      stage_store<T, BM, BK, AK>(ra, LDS_A(cur ^ 1));
+      stage_store<T, BN, BK, BKC>(rb, LDS_B(cur ^ 1));
     }
     __syncthreads();
     cur ^= 1;
   }
-
 #undef LDS_A
 #undef LDS_B
-  // C/D layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r
+
+  // ---- epilogue: accumulator tile -> LDS (fp32, one row half at a time) -> 8-column vectors
+  constexpr int HALF = BM / 2;
+  constexpr int CLD = BN + 4;
+  float* cs = reinterpret_cast<float*>(smem);
+  constexpr int TPR = BN / 8;  // threads per row
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int half = 0; half < 2; ++half) {
+    if ((wm * WM) / HALF == half) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = bn + wn * WN + j * 16 + (lane & 15);
-      if (n >= a.N) continue;
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m >= a.M) continue;
-        const float v = acc[i][j][r] * a.alpha;
-        if (a.splits > 1) a.ws[(((long)split * a.batch + b) * a.M + m) * a.N + n] = v;
-        else epilogue_store<T>(a, b, m, n, v);
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r - half * HALF;
+            cs[row * CLD + col] = acc[i][j][r] * a.alpha;
+          }
+        }
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < HALF * TPR; idx += 256) {
+      const int row = idx / TPR, c8 = (idx % TPR) * 8;
+      const int m = bm + half * HALF + row, n = bn + c8;
+      if (m >= a.M || n >= a.Nw) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = cs[row * CLD + c8 + e];
+      if (a.splits > 1) {
+        float* wp = a.ws + (((long)split * a.batch + b) * a.M + m) * a.Nw + n;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < a.Nw) wp[e] = v[e];
+      } else if (a.vec_ok && n + 8 <= a.N && (a.act_col0 <= n || a.act_col0 >= n + 8)) {
+        epilogue8<T>(a, b, m, n, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n + e < a.Nw) epilogue_store<T>(a, b, m, n + e, v[e]);
       }
     }
+    __syncthreads();
+  }
 }
 
 template <typename T>
 __global__ void splitk_reduce_kernel(GemmArgs a) {
-  const long total = (long)a.batch * a.M * a.N;
+  const long total = (long)a.batch * a.M * a.Nw;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     float v = 0.f;
     for (int s = 0; s < a.splits; ++s) v += a.ws[s * total + idx];
-    const int n = idx % a.N;
-    const long bm = idx / a.N;
+    const int n = idx % a.Nw;
+    const long bm = idx / a.Nw;
     const int m = bm % a.M, b = bm / a.M;
     epilogue_store<T>(a, b, m, n, v);
   }
 }
 
-template <typename T, int BM, int BN, int WM_, bool AK, bool BKC>
-int launch_cfg(GemmArgs& a, bool ala, bool alb, hipStream_t s) {
-  using GA = TileGeom<T, BM, AK>;
-  using GB = TileGeom<T, BN, BKC>;
-  const size_t lds = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
-  dim3 grid(cdiv(a.M, BM), cdiv(a.N, BN), a.batch * a.splits);
-#define DFM_GEMM_GO(X, Y)                                                                         \
-  do {                                                                                            \
-    static bool attr_set = false;                                                                 \
-    if (!attr_set) {                                                                              \
-      (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, WM_, AK, BKC, X, Y>,                \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);                \
-      attr_set = true;                                                                            \
-    }                                                                                             \
-    hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM_, AK, BKC, X, Y>), grid, dim3(256), lds, s, a); \
-  } while (0)
-  if (ala && alb) DFM_GEMM_GO(true, true);
-  else if (ala) DFM_GEMM_GO(true, false);
-  else if (alb) DFM_GEMM_GO(false, true);
-  else DFM_GEMM_GO(false, false);
-#undef DFM_GEMM_GO
+template <typename T, int BM, int BN, int WM_, int BK, bool AK, bool BKC>
+int launch_cfg(GemmArgs& a, hipStream_t s) {
+  using GA = TileGeom<T, BM, BK, AK>;
+  using GB = TileGeom<T, BN, BK, BKC>;
+  const size_t lds_op = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
+  const size_t lds_c = (size_t)(BM / 2) * (BN + 4) * sizeof(float);
+  const size_t lds = lds_op > lds_c ? lds_op : lds_c;
+  dim3 grid(cdiv(a.M, BM), cdiv(a.Nw, BN), a.batch * a.splits);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, WM_, BK, AK, BKC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM_, BK, AK, BKC>), grid, dim3(256), lds, s, a);
   DFM_LAUNCH_CHECK();
   if (a.splits > 1) {
-    const long total = (long)a.batch * a.M * a.N;
+    const long total = (long)a.batch * a.M * a.Nw;
     hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(min(cdiv(total, 256), 4096u)), dim3(256), 0, s, a);
     DFM_LAUNCH_CHECK();
   }
   return DFM_OK;
 }
 
-template <typename T, int BM, int BN, int WM_>
-int launch_layout(GemmArgs& a, bool ak, bool bk, bool ala, bool alb, hipStream_t s) {
-  if (ak && bk) return launch_cfg<T, BM, BN, WM_, true, true>(a, ala, alb, s);
-  if (ak && !bk) return launch_cfg<T, BM, BN, WM_, true, false>(a, ala, alb, s);
-  if (!ak && bk) return launch_cfg<T, BM, BN, WM_, false, true>(a, ala, alb, s);
-  return launch_cfg<T, BM, BN, WM_, false, false>(a, ala, alb, s);
+template <typename T, int BM, int BN, int WM_, int BK>
+int launch_layout(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
+  if (ak && bk) return launch_cfg<T, BM, BN, WM_, BK, true, true>(a, s);
+  if (ak && !bk) return launch_cfg<T, BM, BN, WM_, BK, true, false>(a, s);
+  if (!ak && bk) return launch_cfg<T, BM, BN, WM_, BK, false, true>(a, s);
+  return launch_cfg<T, BM, BN, WM_, BK, false, false>(a, s);
 }
 
-int choose_splits(const DfmGemmDesc* d, int BM, int BN) {
+void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
+  const int Nw = d->N + (d->colsum ? 1 : 0);
+  BM = 128;
+  BN = Nw <= 32 ? 32 : (Nw <= 64 ? 64 : 128);
+}
+
+int choose_splits(const DfmGemmDesc* d) {
   if (d->split_k >= 1) return d->split_k;
-  const long tiles = (long)cdiv(d->M, BM) * cdiv(d->N, BN) * d->batch;
+  int BM, BN;
+  pick_tile(d, BM, BN);
+  const int Nw = d->N + (d->colsum ? 1 : 0);
+  const long tiles = (long)cdiv(d->M, BM) * cdiv(Nw, BN) * (d->batch > 0 ? d->batch : 1);
   if (tiles >= 256 || d->K < 2048) return 1;
   int s = (int)((512 + tiles - 1) / tiles);
   s = min(s, d->K / 1024);
@@ -333,10 +447,8 @@ int choose_splits(const DfmGemmDesc* d, int BM, int BN) {
 }
 
 template <typename T>
-void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
-  if (d->N <= 32) { BM = 128; BN = 32; }
-  else if (d->N <= 64) { BM = 128; BN = 64; }
-  else { BM = 128; BN = 128; }
+bool al16(const void* p, long ld) {
+  return p == nullptr || (((uintptr_t)p % 16 == 0) && (ld % 8 == 0));
 }
 
 template <typename T>
@@ -345,31 +457,43 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   GemmArgs a;
   a.A = A; a.B = B; a.C = C; a.ws = (float*)ws;
   a.M = d->M; a.N = d->N; a.K = d->K; a.batch = d->batch > 0 ? d->batch : 1;
+  a.Nw = d->N + (d->colsum ? 1 : 0);
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
   a.sa = d->stride_a; a.sb = d->stride_b; a.sc = d->stride_c;
   a.alpha = d->alpha; a.beta = d->beta; a.c_f32 = d->c_f32;
   a.bias = d->bias; a.act = d->act; a.preact = d->preact; a.ldpre = d->ldpre;
   a.mul = d->mul; a.ldmul = d->ldmul; a.res = d->res; a.ldres = d->ldres;
-  a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0; a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
+  a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
+  a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
+  a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
   int BM, BN;
-  pick_tile<T>(d, BM, BN);
-  a.splits = choose_splits(d, BM, BN);
+  pick_tile(d, BM, BN);
+  a.splits = choose_splits(d);
   if (a.splits > 1) DFM_CHECK_ARG(ws != nullptr, "dfm_gemm: split-K needs a workspace");
-  const bool ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0);
-  const bool alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0);
+  a.ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0);
+  a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0);
+  a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
+             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
   const bool ak = d->a_kcontig, bk = d->b_kcontig;
-  if (BN == 32) return launch_layout<T, 128, 32, 4>(a, ak, bk, ala, alb, s);
-  if (BN == 64) return launch_layout<T, 128, 64, 2>(a, ak, bk, ala, alb, s);
-  return launch_layout<T, 128, 128, 2>(a, ak, bk, ala, alb, s);
+  const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
+  if (small_k) {
+    constexpr int BKs = sizeof(T) == 2 ? 32 : 16;
+    if (BN == 32) return launch_layout<T, 128, 32, 4, BKs>(a, ak, bk, s);
+    if (BN == 64) return launch_layout<T, 128, 64, 2, BKs>(a, ak, bk, s);
+    return launch_layout<T, 128, 128, 2, BKs>(a, ak, bk, s);
+  }
+  constexpr int BKl = sizeof(T) == 2 ? 64 : 32;
+  if (BN == 32) return launch_layout<T, 128, 32, 4, BKl>(a, ak, bk, s);
+  if (BN == 64) return launch_layout<T, 128, 64, 2, BKl>(a, ak, bk, s);
+  return launch_layout<T, 128, 128, 2, BKl>(a, ak, bk, s);
 }
 
 }  // namespace
 
 extern "C" size_t dfm_gemm_workspace_size(const DfmGemmDesc* d) {
-  int BM = 128, BN = d->N <= 32 ? 32 : (d->N <= 64 ? 64 : 128);
-  const int s = choose_splits(d, BM, BN);
+  const int s = choose_splits(d);
   if (s <= 1) return 0;
-  return (size_t)s * (d->batch > 0 ? d->batch : 1) * d->M * d->N * sizeof(float);
+  return (size_t)s * (d->batch > 0 ? d->batch : 1) * d->M * (d->N + (d->colsum ? 1 : 0)) * sizeof(float);
 }
 
 extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const void* B, void* C, void* ws,
@@ -380,6 +504,7 @@ extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const vo
   DFM_CHECK_ARG(d->a_kcontig ? d->lda >= d->K : d->lda >= d->M, "dfm_gemm: lda too small");
   DFM_CHECK_ARG(d->b_kcontig ? d->ldb >= d->K : d->ldb >= d->N, "dfm_gemm: ldb too small");
   DFM_CHECK_ARG(d->ldc >= d->N, "dfm_gemm: ldc too small");
+  DFM_CHECK_ARG(d->colsum == nullptr || d->batch <= 1, "dfm_gemm: colsum needs batch 1");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) return gemm_typed<bf16_t>(d, A, B, C, ws, s);
   if (dtype == DFM_F32) return gemm_typed<float>(d, A, B, C, ws, s);

@@ -94,26 +94,27 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, int C, const T* 
       }
     }
   }
-  // block reduce of the column partials: groups -> LDS
-  __shared__ float red[2][1024];
-  for (int c = threadIdx.x; c < 2 * 1024; c += 256) (&red[0][0])[c] = 0.f;
-  __syncthreads();
-  for (int gi = 0; gi < RPB; ++gi) {
-    if (grp == gi) {
+  // block reduce of the column partials: groups of a wave by shuffles, then the 4 waves via LDS
+  __shared__ float red[4][2][1024];
+  const int wave = threadIdx.x >> 6;
 #pragma unroll
-      for (int j = 0; j < MAXE; ++j) {
-        const int c = j * G + lg;
-        if (c < C) {
-          red[0][c] += pg[j];
-          red[1][c] += pb[j];
-        }
-      }
+  for (int j = 0; j < MAXE; ++j) {
+    float a = pg[j], bsum = pb[j];
+#pragma unroll
+    for (int o = G; o < 64; o <<= 1) {
+      a += __shfl_xor(a, o, 64);
+      bsum += __shfl_xor(bsum, o, 64);
     }
-    __syncthreads();
+    const int c = j * G + lg;
+    if ((threadIdx.x & 63) < G && c < C) {
+      red[wave][0][c] = a;
+      red[wave][1][c] = bsum;
+    }
   }
+  __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
-    part[(long)blockIdx.x * 2 * C + c] = red[0][c];
-    part[(long)blockIdx.x * 2 * C + C + c] = red[1][c];
+    part[(long)blockIdx.x * 2 * C + c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    part[(long)blockIdx.x * 2 * C + C + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
   }
 }
 
@@ -173,7 +174,8 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
   }
 #undef GO
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ln_partial_sum_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, s, (int)grid, C, part, dg, db);
+  hipLaunchKernelGGL(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)grid, 2L * C,
+                     (const float*)part, dg, db, (long)C, 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -1,17 +1,18 @@
 // Segmentation loss of EncoderDecoder.forward (builder.py:203,230): bilinear upsampling of the
 // low-resolution logits to the label size + cross-entropy(ignore_index) + mean over valid pixels.
 // Fused: the full-resolution logits (786 MB fp32 for DFormer-B bs16) are never materialised.
-// Forward: one thread per label pixel interpolates its ncls logits from the 4 taps, computes the
-// log-sum-exp and the CE term; block partials are summed in a fixed order.
-// Backward: each block owns a 4 x 64 tile of label pixels, accumulates
-// (softmax - onehot) * tap weight into an LDS copy of the low-res patch the tile touches, then
-// flushes the patch with global float atomics (<= 4 blocks add into any low-res cell).
+// Forward: one thread per label pixel interpolates its ncls logits from the 4 taps (registers,
+//   compile-time unrolled over MAXC classes), computes log-sum-exp and the CE term; block partials
+//   are summed in a fixed order.
+// Backward: a block owns a TY x TX tile of label pixels. Phase 1: every thread writes its pixel's
+//   (softmax - onehot) / count row into LDS. Phase 2: threads own (low-res cell, class) pairs of the
+//   patch the tile touches and gather the bilinear-weighted sum from LDS (separable tap weights).
+//   Phase 3: one global float atomic per (cell, class) per block (a cell is shared by <= ~10 blocks).
 #include "common.h"
 
 namespace {
 constexpr int TY = 4, TX = 64;
 constexpr int MAXC = 64;
-constexpr int PATCH = 8192;
 
 DFM_INLINE void src_idx(int dst, int in, int out, int& i0, int& i1, float& l1) {
   const float scale = (float)in / (float)out;
@@ -23,17 +24,21 @@ DFM_INLINE void src_idx(int dst, int in, int out, int& i0, int& i1, float& l1) {
   l1 = src - (float)i0;
 }
 
+// z[c] for c < ncls (others -inf); returns the logit of class `lab` through a predicated select
 template <typename T>
-DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float* z, int& h0,
-                       int& h1, int& w0, int& w1, float& lh, float& lw) {
+DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float (&z)[MAXC]) {
+  int h0, h1, w0, w1;
+  float lh, lw;
   src_idx(y, h, H, h0, h1, lh);
   src_idx(x, w, W, w0, w1, lw);
   const T* p00 = lg + (((long)b * h + h0) * w + w0) * ncls;
   const T* p01 = lg + (((long)b * h + h0) * w + w1) * ncls;
   const T* p10 = lg + (((long)b * h + h1) * w + w0) * ncls;
   const T* p11 = lg + (((long)b * h + h1) * w + w1) * ncls;
-  for (int c = 0; c < ncls; ++c)
-    z[c] = (1.f - lh) * ((1.f - lw) * ldf(p00 + c) + lw * ldf(p01 + c)) + lh * ((1.f - lw) * ldf(p10 + c) + lw * ldf(p11 + c));
+  const float a00 = (1.f - lh) * (1.f - lw), a01 = (1.f - lh) * lw, a10 = lh * (1.f - lw), a11 = lh * lw;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    z[c] = c < ncls ? a00 * ldf(p00 + c) + a01 * ldf(p01 + c) + a10 * ldf(p10 + c) + a11 * ldf(p11 + c) : -INFINITY;
 }
 
 template <typename T>
@@ -46,17 +51,20 @@ __global__ __launch_bounds__(256) void seg_loss_fwd_kernel(int B, int h, int w, 
     const int x = p % W, y = (p / W) % H, b = p / ((long)W * H);
     const long lab = label[p];
     float z[MAXC];
-    int h0, h1, w0, w1;
-    float lh, lw;
-    interp(lg, b, h, w, ncls, y, x, H, W, z, h0, h1, w0, w1, lh, lw);
-    float m = -INFINITY;
-    for (int c = 0; c < ncls; ++c) m = fmaxf(m, z[c]);
+    interp(lg, b, h, w, ncls, y, x, H, W, z);
+    float m = -INFINITY, zl = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      m = fmaxf(m, z[c]);
+      zl = (c == lab) ? z[c] : zl;
+    }
     float se = 0.f;
-    for (int c = 0; c < ncls; ++c) se += __expf(z[c] - m);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) se += c < ncls ? __expf(z[c] - m) : 0.f;
     const float lse = m + __logf(se);
     if (lse_out) lse_out[p] = lse;
     if (lab != ignore && lab >= 0 && lab < ncls) {
-      s += lse - z[lab];
+      s += lse - zl;
       cnt += 1.f;
     }
   }
@@ -86,72 +94,83 @@ __global__ void zero_kernel(long n, float* __restrict__ p) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = 0.f;
 }
 
+DFM_INLINE float tap_w(int dst, int src_i, int in, int out) {
+  int i0, i1;
+  float l1;
+  src_idx(dst, in, out, i0, i1, l1);
+  return (i0 == src_i ? 1.f - l1 : 0.f) + (i1 == src_i ? l1 : 0.f);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, int ncls, const T* __restrict__ lg,
                                                            int H, int W, const long* __restrict__ label, int ignore,
-                                                           const float* __restrict__ loss_out, const float* __restrict__ gscale,
-                                                           float* __restrict__ dlg) {
-  __shared__ float patch[PATCH];
+                                                           const float* __restrict__ loss_out,
+                                                           const float* __restrict__ gscale, float* __restrict__ dlg) {
+  extern __shared__ __attribute__((aligned(16))) float gt[];  // [TY*TX][ncls+1]
+  const int GLD = ncls + 1;
   const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY;
   int bid = blockIdx.x;
   const int tx = bid % tiles_x; bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int b = bid / tiles_y;
   const int y0 = ty * TY, x0 = tx * TX;
-  const int y1 = min(H, y0 + TY) - 1, x1 = min(W, x0 + TX) - 1;
-  int a0, a1, c0, c1;
-  float t;
-  src_idx(y0, h, H, a0, c0, t);
-  src_idx(y1, h, H, c0, a1, t);
-  int b0, b1, d0, d1;
-  src_idx(x0, w, W, b0, d0, t);
-  src_idx(x1, w, W, d0, b1, t);
-  const int pr = a1 - a0 + 1, pc = b1 - b0 + 1;
-  const bool use_lds = pr * pc * ncls <= PATCH;
-  if (use_lds) {
-    for (int e = threadIdx.x; e < pr * pc * ncls; e += 256) patch[e] = 0.f;
-    __syncthreads();
-  }
+  const int ny = min(TY, H - y0), nx = min(TX, W - x0);
   const float inv = (gscale ? gscale[0] : 1.f) / fmaxf(loss_out[1], 1.f);
-  const int y = y0 + threadIdx.x / TX, x = x0 + threadIdx.x % TX;
-  if (y < H && x < W) {
-    const long p = ((long)b * H + y) * W + x;
-    const long lab = label[p];
-    if (lab != ignore && lab >= 0 && lab < ncls) {
+  // phase 1: per-pixel d loss / d upsampled logits
+  {
+    const int py = threadIdx.x / TX, px = threadIdx.x % TX;
+    float* row = gt + threadIdx.x * GLD;
+    const int y = y0 + py, x = x0 + px;
+    long lab = -1;
+    if (py < ny && px < nx) lab = label[((long)b * H + y) * W + x];
+    const bool valid = lab != ignore && lab >= 0 && lab < ncls;
+    if (valid) {
       float z[MAXC];
-      int h0, h1, w0, w1;
-      float lh, lw;
-      interp(lg, b, h, w, ncls, y, x, H, W, z, h0, h1, w0, w1, lh, lw);
+      interp(lg, b, h, w, ncls, y, x, H, W, z);
       float m = -INFINITY;
-      for (int c = 0; c < ncls; ++c) m = fmaxf(m, z[c]);
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) m = fmaxf(m, z[c]);
       float se = 0.f;
-      for (int c = 0; c < ncls; ++c) {
-        z[c] = __expf(z[c] - m);
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        z[c] = c < ncls ? __expf(z[c] - m) : 0.f;
         se += z[c];
       }
-      const float rs = 1.f / se;
-      const float wt[4] = {(1.f - lh) * (1.f - lw), (1.f - lh) * lw, lh * (1.f - lw), lh * lw};
-      const int hh[4] = {h0, h0, h1, h1}, ww[4] = {w0, w1, w0, w1};
-      for (int c = 0; c < ncls; ++c) {
-        const float g = (z[c] * rs - (c == lab ? 1.f : 0.f)) * inv;
-        for (int k = 0; k < 4; ++k) {
-          if (wt[k] == 0.f) continue;
-          if (use_lds) atomicAdd(&patch[((hh[k] - a0) * pc + (ww[k] - b0)) * ncls + c], g * wt[k]);
-          else atomicAdd(&dlg[(((long)b * h + hh[k]) * w + ww[k]) * ncls + c], g * wt[k]);
-        }
-      }
+      const float rs = inv / se;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncls) row[c] = z[c] * rs - (c == lab ? inv : 0.f);
+    } else {
+      for (int c = 0; c < ncls; ++c) row[c] = 0.f;
     }
   }
-  if (use_lds) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < pr * pc * ncls; e += 256) {
-      const float v = patch[e];
-      if (v != 0.f) {
-        const int c = e % ncls, cell = e / ncls;
-        const int i = a0 + cell / pc, j = b0 + cell % pc;
-        atomicAdd(&dlg[(((long)b * h + i) * w + j) * ncls + c], v);
+  __syncthreads();
+  // phase 2: gather per (low-res cell, class) of the patch
+  int a0, a1, b0, b1, t0;
+  float tl;
+  src_idx(y0, h, H, a0, t0, tl);
+  src_idx(y0 + ny - 1, h, H, t0, a1, tl);
+  src_idx(x0, w, W, b0, t0, tl);
+  src_idx(x0 + nx - 1, w, W, t0, b1, tl);
+  const int pr = a1 - a0 + 1, pc = b1 - b0 + 1;
+  const float sx = (float)W / (float)w;
+  for (int e = threadIdx.x; e < pr * pc * ncls; e += 256) {
+    const int c = e % ncls, cell = e / ncls;
+    const int i = a0 + cell / pc, j = b0 + cell % pc;
+    const int xlo = max(0, (int)floorf((j - 0.5f) * sx - 0.5f) - 1 - x0);
+    const int xhi = min(nx - 1, (int)ceilf((j + 1.5f) * sx - 0.5f) + 1 - x0);
+    float acc = 0.f;
+    for (int py = 0; py < ny; ++py) {
+      const float wy = tap_w(y0 + py, i, h, H);
+      if (wy == 0.f) continue;
+      float r = 0.f;
+      for (int px = xlo; px <= xhi; ++px) {
+        const float wx = tap_w(x0 + px, j, w, W);
+        if (wx != 0.f) r += wx * gt[(py * TX + px) * GLD + c];
       }
+      acc += wy * r;
     }
+    if (acc != 0.f) atomicAdd(&dlg[(((long)b * h + i) * w + j) * ncls + c], acc);
   }
 }
 
@@ -180,21 +199,31 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
 }
 
 extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
-                                const long* label, int ignore, const float* lse, const float* loss_out, const float* gscale,
-                                float* dlogits, dfm_stream_t stream) {
+                                const long* label, int ignore, const float* lse, const float* loss_out,
+                                const float* gscale, float* dlogits, dfm_stream_t stream) {
   (void)lse;
-  DFM_CHECK_ARG(logits && label && loss_out && dlogits && ncls <= MAXC, "dfm_seg_loss_bwd: bad argument");
+  DFM_CHECK_ARG(logits && label && loss_out && dlogits && ncls <= MAXC && h <= H && w <= W,
+                "dfm_seg_loss_bwd: bad argument (needs ncls <= 64 and an upsampling resize)");
   hipStream_t s = (hipStream_t)stream;
   const long nl = (long)B * h * w * ncls;
   hipLaunchKernelGGL(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
   DFM_LAUNCH_CHECK();
   const unsigned nblk = B * ((H + TY - 1) / TY) * ((W + TX - 1) / TX);
+  const size_t lds = (size_t)TY * TX * (ncls + 1) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H,
-                       W, label, ignore, loss_out, gscale, dlogits);
+    hipLaunchKernelGGL(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
+                       H, W, label, ignore, loss_out, gscale, dlogits);
   else
-    hipLaunchKernelGGL(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H,
-                       W, label, ignore, loss_out, gscale, dlogits);
+    hipLaunchKernelGGL(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,
+                       H, W, label, ignore, loss_out, gscale, dlogits);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -1,0 +1,491 @@
+"""Segmentation decoders on HIP kernels with the reference's module tree / state_dict keys.
+
+  LightHamHead (+ Hamburger, NMF2D)   models/decoders/ham_head.py:11-240, decode_head.py:55-231
+  DecoderHead (MLPDecoder)            models/decoders/MLPDecoder.py:8-81
+  seg_loss                            models/builder.py:203,230
+
+Feature maps are NHWC rows [B*h*w, C] in the compute dtype. BatchNorm runs in training mode on
+batch statistics; with a multi-rank process group and SyncBN, the (sum, sumsq) and the backward
+(sum dy, sum dy*xhat) statistics are all-reduced (SyncBatchNorm semantics).
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import kernels as K
+from .functional import wcast
+
+
+def _allreduce(t, sync):
+    if sync and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t)
+    return t
+
+
+def _world(sync):
+    if sync and dist.is_available() and dist.is_initialized():
+        return dist.get_world_size()
+    return 1
+
+
+# ============================================================================ building blocks
+class ConvBNActFn(torch.autograd.Function):
+    """y = act(BN(x @ W^T) [+ res])  — mmcv ConvModule(1x1 conv, BN, ReLU) (ham_head.py:204-220)."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, gamma, beta, bn, act, sync):
+        dt = x.dtype
+        Wc = wcast(dt, w)
+        y0 = K.linear(x, Wc)
+        rows = x.shape[0]
+        if bn.training:
+            st = _allreduce(K.bn_stats(y0), sync)
+            count = rows * _world(sync)
+            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
+                                       bn.running_mean, bn.running_var)
+            bn.num_batches_tracked.add_(1)
+        else:
+            mean = bn.running_mean
+            rstd = torch.rsqrt(bn.running_var + bn.eps)
+            count = rows
+        y = K.bn_apply(y0, mean, rstd, gamma, beta, res=res, act=act)
+        ctx.save_for_backward(x, w, y0, y, mean, rstd, gamma)
+        ctx.act, ctx.sync, ctx.count, ctx.has_res = act, sync, count, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y0, y, mean, rstd, gamma = ctx.saved_tensors
+        dy = dy.contiguous()
+        if ctx.act == 2:
+            dy = K.relu_bwd(dy, y)
+        st2 = _allreduce(K.bn_bwd_stats(y0, dy, mean, rstd), ctx.sync)
+        dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
+        dW = K.linear_wgrad(dy0, x)
+        dx = K.linear_dgrad(dy0, wcast(x.dtype, w))
+        dres = dy if ctx.has_res else None
+        return dx, dres, dW.view_as(w), st2[1].clone(), st2[0].clone(), None, None, None
+
+
+class LinearActFn(torch.autograd.Function):
+    """y = act(x @ W^T + b), optional float32 output (ham_in: ConvModule(bias, no norm) + ReLU)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, act, out_f32):
+        Wc = wcast(x.dtype, w)
+        out = torch.empty(x.shape[0], w.shape[0], device=x.device,
+                          dtype=torch.float32 if out_f32 else x.dtype)
+        K.linear(x, Wc, b, act=act, out=out)
+        ctx.save_for_backward(x, w, out)
+        ctx.act = act
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        if ctx.act == 2:
+            dy = K.relu_bwd(dy, y)
+        if dy.dtype != x.dtype:
+            dy = K.cast(dy, x.dtype)
+        dW, db = K.linear_wgrad(dy, x, bias_grad=True)
+        dx = K.linear_dgrad(dy, wcast(x.dtype, w))
+        return dx, dW.view_as(w), db, None, None
+
+
+class CastFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return x if x.dtype == dtype else K.cast(x.contiguous(), dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        return (g if g.dtype == ctx.src else K.cast(g, ctx.src)), None
+
+
+class ResizeCatFn(torch.autograd.Function):
+    """cat([resize(f_i, size of f_0, bilinear, align_corners=False)], channels)  (ham_head.py:226-233,
+    MLPDecoder.py:67-77). feats: NHWC rows; hw: list of (h, w)."""
+
+    @staticmethod
+    def forward(ctx, B, hw, *feats):
+        H0, W0 = hw[0]
+        widths = [f.shape[1] for f in feats]
+        out = torch.empty(B * H0 * W0, sum(widths), device=feats[0].device, dtype=feats[0].dtype)
+        c = 0
+        for f, (h, w), cw in zip(feats, hw, widths):
+            if (h, w) == (H0, W0):
+                K.scale_mul(f, out=out[:, c:c + cw])
+            else:
+                K.bilinear(f, (h, w), (H0, W0), B, out=out[:, c:c + cw])
+            c += cw
+        ctx.B, ctx.hw, ctx.widths = B, hw, widths
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        H0, W0 = ctx.hw[0]
+        grads = []
+        c = 0
+        for (h, w), cw in zip(ctx.hw, ctx.widths):
+            sl = dout[:, c:c + cw]
+            if (h, w) == (H0, W0):
+                grads.append(K.scale_mul(sl))
+            else:
+                grads.append(K.bilinear_bwd(sl, (h, w), (H0, W0), ctx.B))
+            c += cw
+        return (None, None, *grads)
+
+
+class ChannelDropoutLinearFn(torch.autograd.Function):
+    """logits = (x * mask[b, c] / keep) @ W^T + b   — Dropout2d + 1x1 conv (decode_head.py:226-231)."""
+
+    @staticmethod
+    def forward(ctx, x, scale, B, w, b):
+        dt = x.dtype
+        xs = x
+        if scale is not None:  # [B, C] per-image channel scale
+            xs = torch.empty_like(x)
+            rows = x.shape[0] // B
+            for i in range(B):
+                K.scale_mul(x[i * rows:(i + 1) * rows], colscale=scale[i], out=xs[i * rows:(i + 1) * rows])
+        y = K.linear(xs, wcast(dt, w), b)
+        ctx.save_for_backward(xs, w, scale)
+        ctx.B = B
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, w, scale = ctx.saved_tensors
+        dy = dy.contiguous()
+        if dy.dtype != xs.dtype:
+            dy = K.cast(dy, xs.dtype)
+        dW, db = K.linear_wgrad(dy, xs, bias_grad=True)
+        dx = K.linear_dgrad(dy, wcast(xs.dtype, w))
+        if scale is not None:
+            rows = dx.shape[0] // ctx.B
+            for i in range(ctx.B):
+                K.scale_mul(dx[i * rows:(i + 1) * rows], colscale=scale[i], out=dx[i * rows:(i + 1) * rows])
+        return dx, None, None, dW.view_as(w), db
+
+
+# ======================================================================================= NMF
+class NMF2DFn(torch.autograd.Function):
+    """NMF2D.forward (ham_head.py:60-145) on NHWC: x [B, N, D] float32 (= the reference's x^T),
+    bases [B, D, R] injected or freshly drawn; gradients flow through every multiplicative step."""
+
+    @staticmethod
+    def forward(ctx, x, bases, steps, eps):
+        x = x.contiguous()
+        B0 = bases.contiguous()
+        coef = K.softmax_rows(K.bmm(x, B0))                      # softmax(x^T B)
+        hist = []
+        Bt, Ct = B0, coef
+        for _ in range(steps):
+            num1 = K.bmm(x, Bt)                                   # x^T B        [N,R]
+            M = K.bmm(Bt, Bt, a_t=True)                           # B^T B        [R,R]
+            den1 = K.bmm(Ct, M)                                   # C (B^T B)
+            Cn = K.nmf_update(Ct, num1, den1, eps)
+            num2 = K.bmm(x, Cn, a_t=True)                         # x C          [D,R]
+            Q = K.bmm(Cn, Cn, a_t=True)                           # C^T C        [R,R]
+            den2 = K.bmm(Bt, Q)                                   # B (C^T C)
+            Bn = K.nmf_update(Bt, num2, den2, eps)
+            hist.append((Bt, Ct, num1, M, den1, Cn, num2, Q, den2, Bn))
+            Bt, Ct = Bn, Cn
+        num = K.bmm(x, Bt)
+        M = K.bmm(Bt, Bt, a_t=True)
+        den = K.bmm(Ct, M)
+        Cf = K.nmf_update(Ct, num, den, eps)
+        y = K.bmm(Cf, Bt, b_t=True)                               # (B C^T)^T    [N,D]
+        ctx.hist = hist
+        ctx.final = (Bt, Ct, num, M, den, Cf)
+        ctx.eps = eps
+        ctx.save_for_backward(x, B0, coef)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, B0, coef0 = ctx.saved_tensors
+        eps = ctx.eps
+        gy = gy.contiguous()
+        Bt, Ct, num, M, den, Cf = ctx.final
+        gC = K.bmm(gy, Bt)                                        # gy B         [N,R]
+        gB = K.bmm(gy, Cf, a_t=True)                              # gy^T C       [D,R]
+        gx = torch.zeros_like(x)
+
+        def upd_bwd(g, a, nm, dn, out, gnum_sinks, gden_sink):
+            return K.nmf_update_bwd(g, a, nm, dn, out, eps=eps)
+
+        # final coef update: Cf = Ct * num / (Ct M + eps), num = x B, M = B^T B
+        gCt, gnum, gden = K.nmf_update_bwd(gC, Ct, num, den, Cf, eps=eps)
+        _acc_xB(gx, gB, x, Bt, gnum)
+        _acc_CM(gCt, gB, Ct, Bt, M, gden)
+        gC = gCt
+        for (Bp, Cp, num1, M1, den1, Cn, num2, Q, den2, Bn) in reversed(ctx.hist):
+            # B-update: Bn = Bp * num2 / (Bp Q + eps), num2 = x^T-side (x C_n), Q = Cn^T Cn
+            gBp, gnum2, gden2 = K.nmf_update_bwd(gB, Bp, num2, den2, Bn, eps=eps)
+            K.bmm(Cn, gnum2, b_t=True, out=gx, beta=1.0)          # gx += Cn gnum2^T
+            K.bmm(x, gnum2, out=gC, beta=1.0)                     # gCn += x gnum2
+            K.bmm(gden2, Q, out=gBp, beta=1.0)                    # gBp += gden2 Q
+            gQ = K.bmm(Bp, gden2, a_t=True)                       # Bp^T gden2
+            K.bmm(Cn, gQ, out=gC, beta=1.0)
+            K.bmm(Cn, gQ, b_t=True, out=gC, beta=1.0)
+            # C-update: Cn = Cp * num1 / (Cp M1 + eps), num1 = x B_p, M1 = Bp^T Bp
+            gCp, gnum1, gden1 = K.nmf_update_bwd(gC, Cp, num1, den1, Cn, eps=eps)
+            _acc_xB(gx, gBp, x, Bp, gnum1)
+            _acc_CM(gCp, gBp, Cp, Bp, M1, gden1)
+            gB, gC = gBp, gCp
+        # coef0 = softmax(x B0)  (B0 is a random constant)
+        gS = K.softmax_rows_bwd(coef0, gC)
+        K.bmm(gS, B0, b_t=True, out=gx, beta=1.0)
+        ctx.hist = ctx.final = None
+        return gx, None, None, None
+
+
+def _acc_xB(gx, gB, x, Bt, gnum):
+    """num = x B (x [N,D], B [D,R]):  gx += gnum B^T ; gB += x^T gnum."""
+    K.bmm(gnum, Bt, b_t=True, out=gx, beta=1.0)
+    K.bmm(x, gnum, a_t=True, out=gB, beta=1.0)
+
+
+def _acc_CM(gC, gB, C, Bt, M, gden):
+    """den = C M, M = B^T B (symmetric):  gC += gden M ; gB += B (gM + gM^T), gM = C^T gden."""
+    K.bmm(gden, M, out=gC, beta=1.0)
+    gM = K.bmm(C, gden, a_t=True)
+    K.bmm(Bt, gM, out=gB, beta=1.0)
+    K.bmm(Bt, gM, b_t=True, out=gB, beta=1.0)
+
+
+# ============================================================================ mmcv-like modules
+class ConvModule(nn.Module):
+    """1x1 ConvModule parameter container: `conv` (+ `bn`), keys as mmcv (ham_head.py:156-220)."""
+
+    def __init__(self, cin, cout, norm=True, bias=None, bn_eps=1e-5):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, 1, bias=(not norm) if bias is None else bias)
+        if norm:
+            self.bn = nn.BatchNorm2d(cout, eps=bn_eps)
+
+    def fused(self, x, act, res=None, sync=False):
+        return ConvBNActFn.apply(x, res, self.conv.weight, self.bn.weight, self.bn.bias, self.bn, act, sync)
+
+
+class NMF2D(nn.Module):
+    """NMF2D (ham_head.py:103-145): S=1, D=C, R=64, 6 train / 7 eval steps, inv_t=1, eps 1e-6."""
+
+    def __init__(self, args=None):
+        super().__init__()
+        args = dict(args or {})
+        self.S = args.get("MD_S", 1)
+        self.R = args.get("MD_R", 64)
+        self.train_steps = args.get("TRAIN_STEPS", 6)
+        self.eval_steps = args.get("EVAL_STEPS", 7)
+        self.injected_bases = None  # parity runs inject the reference's random bases
+        self.generator = None
+
+    def _build_bases(self, B, D, device):
+        if self.injected_bases is not None:
+            return self.injected_bases.to(device=device, dtype=torch.float32)
+        b = torch.rand(B * self.S, D, self.R, device=device, generator=self.generator)
+        return b / b.norm(dim=1, keepdim=True).clamp_min(1e-12)  # F.normalize(dim=1)
+
+    def fused(self, x, B, N):
+        """x: [B*N, D] float32 rows -> [B*N, D] float32."""
+        D = x.shape[1]
+        bases = self._build_bases(B, D, x.device)
+        steps = self.train_steps if self.training else self.eval_steps
+        y = NMF2DFn.apply(x.view(B, N, D), bases, steps, 1e-6)
+        return y.view(B * N, D)
+
+
+class Hamburger(nn.Module):
+    def __init__(self, ham_channels=512, ham_kwargs=None, norm_cfg=None, bn_eps=1e-5, **kwargs):
+        super().__init__()
+        self.ham_in = ConvModule(ham_channels, ham_channels, norm=False)
+        self.ham = NMF2D(ham_kwargs)
+        self.ham_out = ConvModule(ham_channels, ham_channels, norm=True, bn_eps=bn_eps)
+
+    def fused(self, x, B, N, sync):
+        enjoy = LinearActFn.apply(x, self.ham_in.conv.weight, self.ham_in.conv.bias, 2, True)
+        enjoy = self.ham.fused(enjoy, B, N)
+        enjoy = CastFn.apply(enjoy, x.dtype)
+        return self.ham_out.fused(enjoy, act=2, res=x, sync=sync)  # relu(x + BN(conv(enjoy)))
+
+
+def _nhwc_rows(t):
+    """NCHW view of a channels-last buffer (or NHWC tensor) -> ([B*H*W, C] rows, (B, H, W))."""
+    if t.dim() == 4 and t.shape[1] != t.shape[-1] and t.permute(0, 2, 3, 1).is_contiguous():
+        B, C, H, W = t.shape
+        return t.permute(0, 2, 3, 1).reshape(B * H * W, C), (B, H, W)
+    B, C, H, W = t.shape
+    return t.permute(0, 2, 3, 1).contiguous().view(B * H * W, C), (B, H, W)
+
+
+class LightHamHead(nn.Module):
+    """LightHamHead (ham_head.py:184-240) + BaseDecodeHead pieces (decode_head.py:55-231).
+    forward(list of 4 NCHW maps) -> logits NCHW view of NHWC rows [B, ncls, H/8, W/8]."""
+
+    def __init__(self, ham_channels=512, ham_kwargs=None, in_channels=(128, 256, 512), channels=512, num_classes=40,
+                 dropout_ratio=0.1, norm_cfg=None, in_index=(1, 2, 3), align_corners=False, bn_eps=1e-3,
+                 bn_momentum=0.1, device=None, **kwargs):
+        super().__init__()
+        self.in_channels = list(in_channels)
+        self.in_index = list(in_index)
+        self.channels = channels
+        self.num_classes = num_classes
+        self.dropout_ratio = dropout_ratio
+        self.ham_channels = ham_channels
+        self.syncbn = bool(norm_cfg) and norm_cfg.get("type") == "SyncBN"
+        self.squeeze = ConvModule(sum(self.in_channels), ham_channels, norm=True, bn_eps=bn_eps)
+        self.hamburger = Hamburger(ham_channels, ham_kwargs, bn_eps=bn_eps)
+        self.align = ConvModule(ham_channels, channels, norm=True, bn_eps=bn_eps)
+        self.conv_seg = nn.Conv2d(channels, num_classes, kernel_size=1)
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.momentum = bn_momentum
+        self.dropout_masks = None  # tests may inject Dropout2d keep masks [B, channels]
+
+    def forward(self, inputs):
+        feats = [inputs[i] for i in self.in_index]
+        rows, hw = [], []
+        B = feats[0].shape[0]
+        for f in feats:
+            r, (b, h, w) = _nhwc_rows(f)
+            rows.append(r)
+            hw.append((h, w))
+        x = ResizeCatFn.apply(B, hw, *rows)
+        x = self.squeeze.fused(x, act=2, sync=self.syncbn)
+        H, W = hw[0]
+        x = self.hamburger.fused(x, B, H * W, self.syncbn)
+        x = self.align.fused(x, act=2, sync=self.syncbn)
+        scale = None
+        if self.training and self.dropout_ratio > 0:
+            keep = 1.0 - self.dropout_ratio
+            mask = self.dropout_masks if self.dropout_masks is not None else \
+                (torch.rand(B, self.channels, device=x.device) < keep)
+            scale = mask.to(device=x.device, dtype=torch.float32) / keep
+        logits = ChannelDropoutLinearFn.apply(x, scale, B, self.conv_seg.weight, self.conv_seg.bias)
+        return logits.view(B, H, W, self.num_classes).permute(0, 3, 1, 2)
+
+
+class _Proj(nn.Module):
+    """MLPDecoder.MLP: Linear embedding (MLPDecoder.py:8-19), key `proj`."""
+
+    def __init__(self, input_dim, embed_dim):
+        super().__init__()
+        self.proj = nn.Linear(input_dim, embed_dim)
+
+
+class DecoderHead(nn.Module):
+    """SegFormer-style all-MLP head (MLPDecoder.py:22-81) -> logits at 1/4 resolution."""
+
+    def __init__(self, in_channels=(64, 128, 320, 512), num_classes=40, dropout_ratio=0.1, norm_layer=nn.BatchNorm2d,
+                 embed_dim=768, align_corners=False, bn_eps=1e-3, bn_momentum=0.1, syncbn=False):
+        super().__init__()
+        self.num_classes = num_classes
+        self.dropout_ratio = dropout_ratio
+        self.in_channels = list(in_channels)
+        self.embed_dim = embed_dim
+        self.syncbn = syncbn
+        c1, c2, c3, c4 = self.in_channels
+        self.linear_c4 = _Proj(c4, embed_dim)
+        self.linear_c3 = _Proj(c3, embed_dim)
+        self.linear_c2 = _Proj(c2, embed_dim)
+        self.linear_c1 = _Proj(c1, embed_dim)
+        self.linear_fuse = nn.Sequential(nn.Conv2d(embed_dim * 4, embed_dim, kernel_size=1),
+                                         nn.BatchNorm2d(embed_dim, eps=bn_eps, momentum=bn_momentum),
+                                         nn.ReLU(inplace=True))
+        self.linear_pred = nn.Conv2d(embed_dim, num_classes, kernel_size=1)
+        self.dropout_masks = None
+
+    def forward(self, inputs):
+        B = inputs[0].shape[0]
+        embs, hw = [], []
+        for i in (3, 2, 1, 0):
+            r, (b, h, w) = _nhwc_rows(inputs[i])
+            lin = getattr(self, f"linear_c{i + 1}").proj
+            embs.append(LinearActFn.apply(r, lin.weight, lin.bias, 0, False))
+            hw.append((h, w))
+        H, W = hw[-1]
+        order = [3, 0, 1, 2]  # resize target = c1 size: put c1 first for ResizeCatFn, then restore order
+        cat = ResizeCatFn.apply(B, [hw[3], hw[0], hw[1], hw[2]], embs[3], embs[0], embs[1], embs[2])
+        E = self.embed_dim
+        # channel order of the reference cat is [_c4, _c3, _c2, _c1]: permute the fuse weight columns
+        x = FuseBNReLUFn.apply(cat, self.linear_fuse[0].weight, self.linear_fuse[0].bias,
+                               self.linear_fuse[1].weight, self.linear_fuse[1].bias, self.linear_fuse[1], E,
+                               self.syncbn)
+        scale = None
+        if self.training and self.dropout_ratio > 0:
+            keep = 1.0 - self.dropout_ratio
+            mask = self.dropout_masks if self.dropout_masks is not None else \
+                (torch.rand(B, E, device=x.device) < keep)
+            scale = mask.to(device=x.device, dtype=torch.float32) / keep
+        logits = ChannelDropoutLinearFn.apply(x, scale, B, self.linear_pred.weight, self.linear_pred.bias)
+        del order
+        return logits.view(B, H, W, self.num_classes).permute(0, 3, 1, 2)
+
+
+class FuseBNReLUFn(torch.autograd.Function):
+    """linear_fuse: 1x1 conv(4E->E, bias) + BN + ReLU over cat rows ordered [c1 | c4 | c3 | c2];
+    the reference concatenates [c4 | c3 | c2 | c1] (MLPDecoder.py:77), so the weight's column blocks
+    are permuted accordingly (the conv bias cancels in train-mode BN but is kept for parity)."""
+
+    @staticmethod
+    def forward(ctx, cat, w, b, gamma, beta, bn, E, sync):
+        dt = cat.dtype
+        w2 = w.detach().reshape(E, 4 * E)
+        wperm = torch.cat([w2[:, 3 * E:], w2[:, :3 * E]], 1).contiguous()
+        Wc = K.cast(wperm, dt) if dt != torch.float32 else wperm
+        y0 = K.linear(cat, Wc, b)
+        rows = cat.shape[0]
+        if bn.training:
+            st = _allreduce(K.bn_stats(y0), sync)
+            count = rows * _world(sync)
+            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
+                                       bn.running_mean, bn.running_var)
+            bn.num_batches_tracked.add_(1)
+        else:
+            mean, rstd, count = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps), rows
+        y = K.bn_apply(y0, mean, rstd, gamma, beta, act=2)
+        ctx.save_for_backward(cat, Wc, y0, y, mean, rstd, gamma)
+        ctx.E, ctx.count, ctx.sync, ctx.wshape = E, count, sync, w.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cat, Wc, y0, y, mean, rstd, gamma = ctx.saved_tensors
+        E = ctx.E
+        dy = K.relu_bwd(dy.contiguous(), y)
+        st2 = _allreduce(K.bn_bwd_stats(y0, dy, mean, rstd), ctx.sync)
+        dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
+        dWp, db = K.linear_wgrad(dy0, cat, bias_grad=True)  # columns [c1 | c4 | c3 | c2]
+        dW = torch.cat([dWp[:, E:], dWp[:, :E]], 1).reshape(ctx.wshape)
+        dcat = K.linear_dgrad(dy0, Wc)
+        return dcat, dW, db, st2[1].clone(), st2[0].clone(), None, None, None
+
+
+# ========================================================================================== loss
+class SegLossFn(torch.autograd.Function):
+    """CE(bilinear_up(logits), label, ignore_index)[valid].mean() (builder.py:203,230), fused."""
+
+    @staticmethod
+    def forward(ctx, logits_rows, B, h, w, label, ignore):
+        ncls = logits_rows.shape[1]
+        label = label.contiguous()
+        out = K.seg_loss_fwd(logits_rows, B, h, w, ncls, label, ignore)
+        ctx.save_for_backward(logits_rows, label, out)
+        ctx.meta = (B, h, w, ncls, ignore)
+        return out[0] / out[1].clamp_min(1.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        logits_rows, label, out = ctx.saved_tensors
+        B, h, w, ncls, ignore = ctx.meta
+        gs = g.reshape(1).float().contiguous()
+        dl = K.seg_loss_bwd(logits_rows, B, h, w, ncls, label, out, gscale=gs, ignore=ignore)
+        if logits_rows.dtype != torch.float32:
+            dl = K.cast(dl, logits_rows.dtype)
+        return dl, None, None, None, None, None

@@ -92,14 +92,12 @@ class ConvFFNFn(torch.autograd.Function):
         rps = H * W
         dls = K.colsum(dout, mul=f, rowscale=rowscale, rows_per_scale=rps)
         df = K.scale_mul(dout, colscale=ls, rowscale=rowscale, rows_per_scale=rps)
-        db2 = K.colsum(df)
-        dW2 = K.linear_wgrad(df, g)
+        dW2, db2 = K.linear_wgrad(df, g, bias_grad=True)
         dg = K.linear_dgrad(df, W2)
         dhpre = K.gelu_bwd(dg, hpre)
         dwpos, dbpos = K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3)
         dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
-        db1 = K.colsum(dh)
-        dW1 = K.linear_wgrad(dh, xn)
+        dW1, db1 = K.linear_wgrad(dh, xn, bias_grad=True)
         dxn = K.linear_dgrad(dh, W1)
         dx = dout.clone()
         _, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dx=dx, accumulate=True)
@@ -193,8 +191,7 @@ class AttentionFn(torch.autograd.Function):
         # projections
         grads["ls1"] = K.colsum(dx1, mul=p1, rowscale=rowscale, rows_per_scale=rps)
         dp1 = K.scale_mul(dx1, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
-        grads["bp"] = K.colsum(dp1)
-        grads["wp"] = K.linear_wgrad(dp1, f)
+        grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, bias_grad=True)
         df = K.linear_dgrad(dp1, wcast(dt, wp))
         if drop_depth:
             dxe = dxe1.contiguous().clone() if dxe1 is not None else torch.zeros_like(xe)
@@ -202,8 +199,7 @@ class AttentionFn(torch.autograd.Function):
             dxe1 = dxe1.contiguous()
             grads["ls1e"] = K.colsum(dxe1, mul=p1e, rowscale=rowscale_e, rows_per_scale=rps)
             dp1e = K.scale_mul(dxe1, colscale=ls1e, rowscale=rowscale_e, rows_per_scale=rps)
-            grads["bpe"] = K.colsum(dp1e)
-            grads["wpe"] = K.linear_wgrad(dp1e, f)
+            grads["wpe"], grads["bpe"] = K.linear_wgrad(dp1e, f, bias_grad=True)
             K.linear_dgrad(dp1e, wcast(dt, wpe), out=df, accumulate=True)
             dxe = dxe1.clone()
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
@@ -213,13 +209,11 @@ class AttentionFn(torch.autograd.Function):
         dcxe = df[:, fw - Ch:]
         K.scale_mul(dcxe, mul=xep, out=dcx)
         dxep = K.scale_mul(dcxe, mul=cx)
-        grads["beb"] = K.colsum(dxep)
-        grads["web"] = K.linear_wgrad(dxep, e2)
+        grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, bias_grad=True)
         de2 = K.linear_dgrad(dxep, wcast(dt, web))
         grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7)
         de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
-        grads["bef"] = K.colsum(de1)
-        grads["wef"] = K.linear_wgrad(de1, xen)
+        grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, bias_grad=True)
         dxen = K.linear_dgrad(de1, wcast(dt, wef))
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
@@ -231,27 +225,23 @@ class AttentionFn(torch.autograd.Function):
             dkv = torch.empty(P, C, device=dev, dtype=dt)
             K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
                               dkv[:, :Ch], dkv[:, Ch:])
-            grads["bsc"] = K.colsum(dm)
-            grads["wsc"] = K.linear_wgrad(dm, pooled)
+            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, bias_grad=True)
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
             K.pool7_bwd(dpooled[:, C:], shape, dx=dxen, accumulate=True)
-            grads["bkv"] = K.colsum(dkv)
-            grads["wkv"] = K.linear_wgrad(dkv, g)
+            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, bias_grad=True)
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
         K.scale_mul(dqa, mul=a, out=dq)
         da = K.scale_mul(dqa, mul=q)
-        grads["ba"] = K.colsum(da)
-        grads["wa"] = K.linear_wgrad(da, apre)
+        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, bias_grad=True)
         dapre = K.linear_dgrad(da, wcast(dt, wa))
         grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7)
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.gelu_bwd(dg, lpre, out=dl)
         # q | q_cut | l
-        dbqcl = K.colsum(dqcl)
-        dWqcl = K.linear_wgrad(dqcl, xn)
+        dWqcl, dbqcl = K.linear_wgrad(dqcl, xn, bias_grad=True)
         grads["bq"], grads["bqc"], grads["bl"] = dbqcl[:C], dbqcl[C:C + Ch], dbqcl[C + Ch:]
         grads["wq"], grads["wqc"], grads["wl"] = dWqcl[:C], dWqcl[C:C + Ch], dWqcl[C + Ch:]
         Wqcl = wcast(dt, wq, wqc, wl)

@@ -35,7 +35,8 @@ def rows_of(t):
 # ------------------------------------------------------------------------------------------ GEMM
 def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
-         ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0):
+         ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
+         colsum_accumulate=False):
     dt = dtype_code(a)
     assert b.dtype == a.dtype, (a.dtype, b.dtype)
     c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
@@ -43,7 +44,8 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
         assert out.dtype == a.dtype
     d = _lib.GemmDesc(M, N, K, batch, int(a_kcontig), int(b_kcontig), lda, ldb, ldc, stride_a, stride_b, stride_c,
                       alpha, beta, c_f32, ptr(bias), act, ptr(preact), ldpre, ptr(mul), ldmul, ptr(res), ldres,
-                      ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0)
+                      ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0, ptr(colsum),
+                      int(colsum_accumulate))
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
@@ -73,18 +75,21 @@ def linear_dgrad(dy, w, out=None, accumulate=False, mul=None):
                 beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0)
 
 
-def linear_wgrad(dy, x, out=None, accumulate=False):
-    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]  (float32 output, split-K over M)."""
+def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False):
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]  (float32 output, split-K over M).
+    bias_grad=True also returns db[N] = sum_M dy (fused: virtual all-ones column of x)."""
     M, N = dy.shape
     K = x.shape[1]
     if out is None:
         out = torch.empty(N, K, device=dy.device, dtype=torch.float32)
-    return gemm(dy, x, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=ld(dy), ldb=ld(x), out=out,
-                ldc=ld(out), beta=1.0 if accumulate else 0.0)
+    db = torch.empty(N, device=dy.device, dtype=torch.float32) if bias_grad else None
+    gemm(dy, x, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=ld(dy), ldb=ld(x), out=out,
+         ldc=ld(out), beta=1.0 if accumulate else 0.0, colsum=db)
+    return (out, db) if bias_grad else out
 
 
-def bmm(a, b, *, a_t=False, b_t=False, out=None, alpha=1.0):
-    """Batched out[b] = op(a[b]) @ op(b[b]) for contiguous 3-D tensors (op = transpose if *_t)."""
+def bmm(a, b, *, a_t=False, b_t=False, out=None, alpha=1.0, beta=0.0):
+    """Batched out[b] (= or +=) op(a[b]) @ op(b[b]) for contiguous 3-D tensors (op = transpose if *_t)."""
     B = a.shape[0]
     M = a.shape[2] if a_t else a.shape[1]
     K = a.shape[1] if a_t else a.shape[2]
@@ -96,7 +101,7 @@ def bmm(a, b, *, a_t=False, b_t=False, out=None, alpha=1.0):
     # B(k,n): b[k][n] (row-contig, ldb=N) or b[n][k] (b_t: k-contig, ldb=K)
     return gemm(a, b, M=M, N=N, K=K, a_kcontig=not a_t, b_kcontig=b_t, lda=a.shape[2], ldb=b.shape[2], out=out,
                 ldc=N, batch=B, stride_a=a.shape[1] * a.shape[2], stride_b=b.shape[1] * b.shape[2],
-                stride_c=M * N, alpha=alpha)
+                stride_c=M * N, alpha=alpha, beta=beta)
 
 
 # ------------------------------------------------------------------------------------ LayerNorm

@@ -1,0 +1,180 @@
+"""One data-parallel training step of utils/train.py:309-383 on HIP kernels + RCCL.
+
+  group_weight      utils/init_func.py:26-70 (decay / no-decay groups; layer_scale_* and the custom
+                    LayerNorm params fall in no group and are never updated — reproduced)
+  FusedAdamW        torch.optim.AdamW(lr, betas=(0.9, 0.999), wd) of train.py:210-216 as one HIP launch
+                    per group over flat float32 buffers, also refreshing the bf16 GEMM weight copies
+  WarmUpPolyLR      utils/lr_policy.py:22-36
+  GradBuckets       DDP-style bucketed gradient all-reduce (SUM, /world folded into AdamW), launched
+                    from post-accumulate-grad hooks so RCCL overlaps the rest of the backward pass
+"""
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import kernels as K
+from .functional import invalidate_weights, register_shadow
+
+
+def group_weight(module, norm_layer=nn.BatchNorm2d):
+    """(decay, no_decay) parameter lists exactly as init_func.group_weight builds them."""
+    decay, no_decay = [], []
+    for m in module.modules():
+        if isinstance(m, nn.Linear):
+            decay.append(m.weight)
+            if m.bias is not None:
+                no_decay.append(m.bias)
+        elif isinstance(m, (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose2d, nn.ConvTranspose3d)):
+            decay.append(m.weight)
+            if m.bias is not None:
+                no_decay.append(m.bias)
+        elif isinstance(m, (norm_layer, nn.BatchNorm1d, nn.BatchNorm2d, nn.BatchNorm3d, nn.GroupNorm, nn.LayerNorm,
+                            nn.SyncBatchNorm)):
+            if m.weight is not None:
+                no_decay.append(m.weight)
+            if m.bias is not None:
+                no_decay.append(m.bias)
+    return decay, no_decay
+
+
+class WarmUpPolyLR:
+    def __init__(self, start_lr, lr_power, total_iters, warmup_steps):
+        self.start_lr, self.lr_power = start_lr, lr_power
+        self.total_iters, self.warmup_steps = total_iters + 0.0, warmup_steps
+
+    def get_lr(self, cur_iter):
+        if cur_iter < self.warmup_steps:
+            return self.start_lr * (cur_iter / self.warmup_steps)
+        return self.start_lr * ((1 - float(cur_iter) / self.total_iters) ** self.lr_power)
+
+
+class _FlatGroup:
+    """Parameters of one optimizer group re-homed into one flat float32 buffer (+ grad, m, v, bf16)."""
+
+    def __init__(self, params, wd, device, shadow_dtype):
+        self.params = [p for p in params if p.requires_grad]
+        self.wd = wd
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        self.m = torch.zeros(n, device=device, dtype=torch.float32)
+        self.v = torch.zeros(n, device=device, dtype=torch.float32)
+        self.shadow = torch.empty(n, device=device, dtype=shadow_dtype) if shadow_dtype != torch.float32 else None
+        self.slots = {}
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            self.slots[p] = (off, k)
+            off += k
+        if self.shadow is not None:
+            self.shadow.copy_(self.flat)
+
+    def register_shadows(self):
+        if self.shadow is None:
+            return
+        for p, (off, k) in self.slots.items():
+            if p.dim() >= 2:
+                register_shadow(p, self.shadow[off:off + k].view(p.shape[0], -1))
+
+
+class GradBuckets:
+    """Copies each parameter's finished gradient into its group's flat buffer; with world > 1 it
+    launches an async all-reduce per ~25 MB bucket as soon as the bucket is complete."""
+
+    def __init__(self, groups, world, bucket_bytes=25 << 20):
+        self.world = world
+        self.handles = []
+        self.buckets = []  # (tensor view, set(params))
+        self.owner = {}
+        for gi, g in enumerate(groups):
+            start, cur, members = None, 0, []
+            order = sorted(g.slots.items(), key=lambda kv: -kv[1][0])  # reverse registration ~ backward order
+            for p, (off, k) in order:
+                members.append(p)
+                cur += k * 4
+                start = off if start is None else min(start, off)
+                if cur >= bucket_bytes:
+                    self._add(g, members, start)
+                    start, cur, members = None, 0, []
+            if members:
+                self._add(g, members, start)
+        self.pending = [len(b[1]) for b in self.buckets]
+        for p in self.owner:
+            p.register_post_accumulate_grad_hook(self._hook)
+
+    def _add(self, g, members, start):
+        end = max(g.slots[p][0] + g.slots[p][1] for p in members)
+        bi = len(self.buckets)
+        self.buckets.append((g.grad[start:end], set(members)))
+        for p in members:
+            self.owner[p] = (bi, g)
+
+    def _hook(self, p):
+        bi, g = self.owner[p]
+        off, k = g.slots[p]
+        g.grad[off:off + k].copy_(p.grad.reshape(-1))
+        p.grad = None
+        self.pending[bi] -= 1
+        if self.pending[bi] == 0 and self.world > 1:
+            self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
+
+    def finish(self):
+        for h in self.handles:
+            h.wait()
+        self.handles = []
+        self.pending = [len(b[1]) for b in self.buckets]
+
+
+class FusedAdamW:
+    """torch.optim.AdamW semantics over the two group_weight groups (decay wd, no-decay 0)."""
+
+    def __init__(self, model, lr=6e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, world=1,
+                 compute_dtype=torch.float32, bucket_bytes=25 << 20):
+        decay, no_decay = group_weight(model)
+        dev = next(model.parameters()).device
+        self.groups = [_FlatGroup(decay, weight_decay, dev, compute_dtype),
+                       _FlatGroup(no_decay, 0.0, dev, torch.float32)]
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.world = world
+        self.step_count = 0
+        self.buckets = GradBuckets(self.groups, world, bucket_bytes)
+        grouped = {id(p) for g in self.groups for p in g.params}
+        # layer_scale_* and the custom LayerNorm params: in no group (never updated, like the reference)
+        self.ungrouped = [p for p in model.parameters() if p.requires_grad and id(p) not in grouped]
+        invalidate_weights()
+        for g in self.groups:
+            g.register_shadows()
+
+    def step(self, lr=None):
+        self.buckets.finish()
+        for p in self.ungrouped:
+            p.grad = None
+        self.step_count += 1
+        lr = self.lr if lr is None else lr
+        for g in self.groups:
+            K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, self.step_count,
+                    1.0 / self.world, g.shadow)
+        invalidate_weights()
+        for g in self.groups:
+            g.register_shadows()
+
+
+def all_reduce_mean(t, world):
+    """pyt_utils.all_reduce_tensor (SUM then /world), async-free for the scalar loss."""
+    if world > 1:
+        t = t.clone()
+        dist.all_reduce(t)
+        t = t / world
+    return t
+
+
+def train_step(model, opt, rgb, depth, label, lr=None):
+    """One reference training iteration (train.py:318-357): forward + loss, backward (bucketed
+    RCCL all-reduce overlapping it), loss all-reduce, AdamW step. Returns the (device) mean loss."""
+    loss, _ = model(rgb, depth, label)
+    reduce_loss = all_reduce_mean(loss.detach(), opt.world)
+    loss.backward()
+    opt.step(lr)
+    return reduce_loss

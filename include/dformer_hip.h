@@ -76,6 +76,9 @@ typedef struct DfmGemmDesc {
   long rows_per_scale;
   int split_k;  /* 0 = auto, 1 = off, >1 = forced */
   int act_col0; /* act / preact apply to columns n >= act_col0; preact[m, n - act_col0] */
+  float* colsum; /* optional float32 [M]: (+)= alpha * sum_k A(m,k) — the bias gradient of a wgrad
+                    GEMM, computed as a virtual all-ones column of B (batch must be 1) */
+  int colsum_accumulate;
 } DfmGemmDesc;
 
 size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);

@@ -49,6 +49,9 @@ def test_gemm_layouts(dt, M, N, Kd):
     dw = k.linear_wgrad(dy, x)
     assert dw.dtype == torch.float32
     assert rel(dw, dy.float().t() @ x.float()) < TOL[dt]
+    dw2, db = k.linear_wgrad(dy, x, bias_grad=True)
+    assert rel(dw2, dy.float().t() @ x.float()) < TOL[dt]
+    assert rel(db, dy.float().sum(0)) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)

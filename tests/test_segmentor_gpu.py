@@ -1,0 +1,174 @@
+"""End-to-end parity of the HIP segmentor (encoder + decoder + fused loss) with the reference
+goldens, plus decoder-module goldens (NMF2D, LightHamHead, MLPDecoder) and a DDP-style step."""
+import numpy as np
+import pytest
+import torch
+
+import dformer_ref as R
+import gen
+from goldens import check_param_grads, fp_rel_err, load, rel_err
+
+
+class Cfg(dict):
+    __getattr__ = dict.__getitem__
+
+
+def build(arch, dec, ncls, device="cpu"):
+    from dformer_amd.segmentor import EncoderDecoder
+    cfg = Cfg(backbone=arch, decoder=dec, decoder_embed_dim=512, num_classes=ncls, drop_path_rate=0.0,
+              bn_eps=1e-3, bn_momentum=0.1, background=255)
+    model = EncoderDecoder(cfg=cfg, syncbn=False)
+    model.decode_head.dropout_ratio = 0.0
+    sd = model.state_dict()
+    vals = gen.state_dict_values([(k, v.shape) for k, v in sd.items()])
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)).to(sd[k].dtype) for k, v in vals.items()})
+    return model.to(device)
+
+
+E2E = [("e2e_tiny_small", "DFormer-Tiny", "ham", 40), ("e2e_base_small", "DFormer-Base", "ham", 40),
+       ("e2e_large_mlp_small", "DFormer-Large", "MLPDecoder", 37)]
+
+
+@pytest.mark.parametrize("name,arch,dec,ncls", E2E)
+def test_segmentor_state_dict_matches_reference(name, arch, dec, ncls):
+    model = build(arch, dec, ncls)
+    shapes = R.segmentor_shapes(arch, dec, ncls)
+    sd = {k: tuple(v.shape) for k, v in model.state_dict().items() if not k.endswith("num_batches_tracked")}
+    assert sd == shapes
+    g = load(name)
+    names = {k[4:] for k in g if k.startswith("gfp/")}
+    assert names <= set(sd)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,arch,dec,ncls", E2E)
+def test_segmentor_fp32_vs_reference(name, arch, dec, ncls):
+    g = load(name)
+    B, H, W, _ = [int(v) for v in g["meta"]]
+    model = build(arch, dec, ncls, "cuda")
+    model.train()
+    if dec == "ham":
+        model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
+            gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
+    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb = torch.from_numpy(rgb_np).float().cuda().requires_grad_()
+    dep = torch.from_numpy(dep_np).float().cuda().requires_grad_()
+    lab = torch.from_numpy(gen.labels(B, H, W, ncls)).cuda()
+    feats = model.encoder_backbone(rgb, dep)[0]
+    low = model.decode_head(feats)
+    from dformer_amd.decoders import SegLossFn, _nhwc_rows
+    rows, (b, h, w) = _nhwc_rows(low)
+    loss = SegLossFn.apply(rows.contiguous(), b, h, w, lab, 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    for i, f in enumerate(feats):
+        assert rel_err(f.float().cpu(), g[f"feat{i}"]) < 1e-3, i
+    assert rel_err(low.float().cpu(), g["low"]) < 1e-3
+    assert abs(loss.item() - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
+    assert fp_rel_err(gen.fingerprint(rgb.grad.cpu().double().numpy()), g["grgb_fp"]) < 1e-3
+    bad = []
+    for k, v in g.items():
+        if k.startswith("gfp/"):
+            p = dict(model.named_parameters())[k[4:]]
+            e = fp_rel_err(gen.fingerprint(p.grad.cpu().double().numpy(), 16), v, atol=1e-4)
+            if e > 2e-3:
+                bad.append((k, e))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("train", [True, False])
+def test_nmf2d_vs_reference(train):
+    from dformer_amd.decoders import NMF2D
+    name = "nmf_train" if train else "nmf_eval"
+    g = load(name)
+    B, C, H, W, _ = [int(v) for v in g["meta"]]
+    nmf = NMF2D()
+    nmf.train(train)
+    nmf.injected_bases = torch.from_numpy(gen.nmf_bases(B, C, 64, name=name + "/bases")).float()
+    x = torch.from_numpy(gen.uniform(name + "/x", (B, C, H, W))).float().cuda()
+    xr = x.permute(0, 2, 3, 1).contiguous().view(B * H * W, C).requires_grad_()
+    y = nmf.fused(xr, B, H * W)
+    gy = torch.from_numpy(gen.normal(name + "/gy", (B, C, H, W))).float().cuda()
+    y.backward(gy.permute(0, 2, 3, 1).reshape(B * H * W, C))
+    yy = y.detach().view(B, H, W, C).permute(0, 3, 1, 2).cpu()
+    assert rel_err(yy, g["y"]) < 1e-4
+    gx = xr.grad.view(B, H, W, C).permute(0, 3, 1, 2).cpu()
+    assert rel_err(gx, g["gx"]) < 1e-3
+
+
+@pytest.mark.gpu
+def test_ham_head_vs_reference():
+    from dformer_amd.decoders import LightHamHead
+    name = "ham_tiny"
+    g = load(name)
+    B, H, W, ncls, train, *in_ch = [int(v) for v in g["meta"]]
+    head = LightHamHead(in_channels=in_ch, num_classes=ncls, channels=512, norm_cfg=dict(type="BN"))
+    head.dropout_ratio = 0.0
+    sd = head.state_dict()
+    vals = gen.state_dict_values([(k, v.shape) for k, v in sd.items()])
+    head.load_state_dict({k: torch.from_numpy(np.asarray(v)).to(sd[k].dtype) for k, v in vals.items()})
+    head = head.cuda().train()
+    from dformer_amd.functional import invalidate_weights
+    invalidate_weights()
+    head.hamburger.ham.injected_bases = torch.from_numpy(gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
+    feats = [torch.from_numpy(gen.normal(name + f"/f{i}", (B, c, H >> i, W >> i))).float().cuda()
+             for i, c in enumerate(in_ch)]
+    leaves = [f.permute(0, 2, 3, 1).contiguous().requires_grad_() for f in feats]
+    y = head([None] + [t.permute(0, 3, 1, 2) for t in leaves])
+    gy = torch.from_numpy(gen.normal(name + "/gy", tuple(y.shape))).float().cuda()
+    y.backward(gy)
+    assert rel_err(y.detach().cpu(), g["y"]) < 1e-3
+    for i, t in enumerate(leaves):
+        assert rel_err(t.grad.permute(0, 3, 1, 2).cpu(), g[f"gf{i + 1}"]) < 1e-3
+    grads = {k: p.grad.cpu() for k, p in head.named_parameters() if p.grad is not None}
+    check_param_grads(g, grads, 2e-3, atol=1e-6)
+    for k, v in g.items():
+        if k.startswith("buf/"):
+            assert rel_err(dict(head.named_buffers())[k[4:]].cpu(), v) < 1e-4
+
+
+@pytest.mark.gpu
+def test_mlp_decoder_vs_reference():
+    from dformer_amd.decoders import DecoderHead
+    from dformer_amd.functional import invalidate_weights
+    name = "mlpdec_small"
+    g = load(name)
+    B, H, W, ncls, embed, *in_ch = [int(v) for v in g["meta"]]
+    head = DecoderHead(in_channels=in_ch, num_classes=ncls, embed_dim=embed)
+    head.dropout_ratio = 0.0
+    sd = head.state_dict()
+    vals = gen.state_dict_values([(k, v.shape) for k, v in sd.items()])
+    head.load_state_dict({k: torch.from_numpy(np.asarray(v)).to(sd[k].dtype) for k, v in vals.items()})
+    head = head.cuda().train()
+    invalidate_weights()
+    sizes = [(H, W)]
+    for _ in range(3):
+        sizes.append(((sizes[-1][0] - 1) // 2 + 1, (sizes[-1][1] - 1) // 2 + 1))
+    leaves = [torch.from_numpy(gen.normal(name + f"/f{i}", (B, c, *sizes[i]))).float().cuda()
+              .permute(0, 2, 3, 1).contiguous().requires_grad_() for i, c in enumerate(in_ch)]
+    y = head([t.permute(0, 3, 1, 2) for t in leaves])
+    gy = torch.from_numpy(gen.normal(name + "/gy", tuple(y.shape))).float().cuda()
+    y.backward(gy)
+    assert rel_err(y.detach().cpu(), g["y"]) < 1e-3
+    for i, t in enumerate(leaves):
+        assert rel_err(t.grad.permute(0, 3, 1, 2).cpu(), g[f"gf{i}"]) < 1e-3
+    grads = {k: p.grad.cpu() for k, p in head.named_parameters() if p.grad is not None}
+    check_param_grads(g, grads, 2e-3, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_train_step_bf16_runs_and_decreases_loss():
+    """Tiny bf16 training steps through FusedAdamW: finite loss that drops on a fixed batch."""
+    from dformer_amd.train import FusedAdamW, train_step
+    torch.manual_seed(0)
+    model = build("DFormer-Tiny", "ham", 40, "cuda").set_compute_dtype(torch.bfloat16)
+    model.return_logits = False
+    model.train()
+    opt = FusedAdamW(model, lr=1e-3, compute_dtype=torch.bfloat16)
+    rgb = torch.randn(2, 3, 96, 128, device="cuda")
+    dep = torch.randn(2, 1, 96, 128, device="cuda")
+    lab = torch.randint(0, 40, (2, 96, 128), device="cuda")
+    losses = [train_step(model, opt, rgb, dep, lab).item() for _ in range(8)]
+    assert all(np.isfinite(losses)), losses
+    assert losses[-1] < losses[0], losses
