@@ -29,7 +29,7 @@ class GemmDesc(ctypes.Structure):
                 ("bias", P), ("act", c_int), ("preact", P), ("ldpre", c_long),
                 ("mul", P), ("ldmul", c_long), ("res", P), ("ldres", c_long),
                 ("colscale", P), ("rowscale", P), ("rows_per_scale", c_long), ("split_k", c_int),
-                ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int)]
+                ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int), ("mul_gelu_grad", c_int)]
 
 
 # name -> (restype, argtypes)
@@ -40,8 +40,10 @@ _SIGS = {
     "dfm_gemm": (c_int, [c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
     "dfm_layernorm_fwd": (c_int, [c_int, c_long, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P]),
     "dfm_layernorm_bwd_workspace": (c_size_t, [c_long, c_int]),
-    "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, c_int, P, P, P,
-                                  P]),
+    "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, P, c_long, c_int,
+                                  P, P, P, P]),
+    "dfm_residual_bwd_workspace": (c_size_t, [c_long, c_int]),
+    "dfm_residual_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, P]),
     "dfm_dwconv_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, c_int, P, c_long, P, c_long,
                                P]),
     "dfm_dwconv_bwd_data": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_int, P, c_long,

@@ -57,6 +57,34 @@ template <int G> DFM_INLINE float group_sum(float v) {
   return v;
 }
 
+// 8 consecutive T elements <-> floats
+template <typename T> DFM_INLINE void ld8(const T* p, float* v);
+template <> DFM_INLINE void ld8<bf16_t>(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+template <> DFM_INLINE void ld8<float>(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <typename T> DFM_INLINE void st8(T* p, const float* v);
+template <> DFM_INLINE void st8<bf16_t>(bf16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+template <> DFM_INLINE void st8<float>(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+
 // ---- second stage of the deterministic two-stage column reductions:
 // out[e] (+)= sum_{b < nblk} part[b * n + e], fixed summation order; 64 columns x 16 row-lanes
 // per 1024-thread block so the nblk partials of a column are read by 16 lanes in parallel.

@@ -1,173 +1,266 @@
 // Depthwise k x k convolution over NHWC (DFormer.py:80-81 7x7 conv/e_conv, DFormer.py:54,62 3x3
-// pos + identity). HBM-bound: a (TH+k-1) x (TW+k-1) x CB halo tile is staged in LDS once and
-// every thread produces a TW-pixel output row of one channel from register sliding windows.
-// The weight gradient is reduced deterministically: per-block partials [block][C][k*k+1] and a
-// second pass that sums them in a fixed order.
+// pos + identity), forward / input-gradient / weight-gradient.
+//
+// HBM-bound. Every thread owns CPT consecutive channels (one 16-byte vector: 8 bf16 or 4 fp32)
+// of a TW-pixel strip of one output row; input rows are streamed as 16-byte vectors through a
+// register sliding window (neighbouring strips share their halo through L1/L2, so HBM sees each
+// byte about once). A block covers GPB channel groups x SPB strips; the block's k*k weights live
+// in LDS transposed to [k*k][channels] so each tap is one vector LDS read.
+// The weight gradient accumulates per thread over many strips, reduces across the block's strip
+// lanes in LDS, writes per-block partials [block][C][k*k+1] (last column: bias grad) and sums
+// them in a fixed order (deterministic, no float atomics).
 #include "common.h"
 
 namespace {
-constexpr int TH = 8, TW = 16;
+constexpr int TW = 4;
 
-template <typename T, int K, int CB, bool FLIP>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(int B, int H, int W, int C, const T* __restrict__ x, long ldx,
-                                                     const float* __restrict__ w, const float* __restrict__ bias,
-                                                     int add_identity, T* __restrict__ y, long ldy, int accumulate,
-                                                     T* __restrict__ gout, long ldg) {
-  constexpr int R = K / 2, IH = TH + K - 1, IW = TW + K - 1;
-  constexpr int RG = 256 / CB;  // row groups
-  static_assert(RG == TH, "thread layout: one output row per thread");
-  __shared__ float tile[IH * IW * CB];
-  const int tiles_w = (W + TW - 1) / TW, tiles_h = (H + TH - 1) / TH;
-  int bid = blockIdx.x;
-  const int tw = bid % tiles_w; bid /= tiles_w;
-  const int th = bid % tiles_h; bid /= tiles_h;
-  const int b = bid;
-  const int c0 = blockIdx.y * CB;
-  const int h0 = th * TH, w0 = tw * TW;
-  const long img = (long)b * H * W;
-  for (int e = threadIdx.x; e < IH * IW * CB; e += 256) {
-    const int c = e % CB, pix = e / CB;
-    const int ih = pix / IW, iw = pix % IW;
-    const int hh = h0 + ih - R, ww = w0 + iw - R;
-    float v = 0.f;
-    if (hh >= 0 && hh < H && ww >= 0 && ww < W && c0 + c < C) v = ldf(x + (img + (long)hh * W + ww) * ldx + c0 + c);
-    tile[e] = v;
+template <typename T> struct DwCfg { static constexpr int CPT = 16 / sizeof(T); };
+
+template <typename T>
+DFM_INLINE void ldv(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    ld8<T>(p, v);
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
   }
-  __syncthreads();
-  const int c = threadIdx.x % CB, r = threadIdx.x / CB;
-  const int cc = c0 + c;
-  if (cc >= C || h0 + r >= H) return;
-  float wk[K * K];
-#pragma unroll
-  for (int i = 0; i < K * K; ++i) wk[i] = w[(long)cc * K * K + (FLIP ? (K * K - 1 - i) : i)];
-  float acc[TW];
-  const float b0 = bias ? bias[cc] : 0.f;
-#pragma unroll
-  for (int j = 0; j < TW; ++j) acc[j] = b0;
-#pragma unroll
-  for (int i = 0; i < K; ++i) {
-    float row[IW];
-#pragma unroll
-    for (int j = 0; j < IW; ++j) row[j] = tile[((r + i) * IW + j) * CB + c];
-#pragma unroll
-    for (int kj = 0; kj < K; ++kj)
-#pragma unroll
-      for (int j = 0; j < TW; ++j) acc[j] += wk[i * K + kj] * row[j + kj];
-  }
-  if (add_identity) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) acc[j] += tile[((r + R) * IW + j + R) * CB + c];
-  }
-  T* yr = y + (img + (long)(h0 + r) * W + w0) * ldy + cc;
-#pragma unroll
-  for (int j = 0; j < TW; ++j) {
-    if (w0 + j < W) {
-      float v = acc[j];
-      if (accumulate) v += ldf(yr + (long)j * ldy);
-      stf(yr + (long)j * ldy, v);
-      if (gout) stf(gout + (img + (long)(h0 + r) * W + w0 + j) * ldg + cc, gelu_f(v));
-    }
+}
+template <typename T>
+DFM_INLINE void stv(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    st8<T>(p, v);
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
-// dW partials. Block (tile_chunk, cblock) loops over `tpb` output tiles of one channel block.
-template <typename T, int K, int CB>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(int B, int H, int W, int C, const T* __restrict__ x, long ldx,
-                                                       const T* __restrict__ dy, long lddy, int tpb,
-                                                       float* __restrict__ part) {
-  constexpr int R = K / 2, IH = TH + K - 1, IW = TW + K - 1, KK = K * K;
-  __shared__ float tile[IH * IW * CB];
-  __shared__ float red[4][KK + 1][CB];
-  const int tiles_w = (W + TW - 1) / TW, tiles_h = (H + TH - 1) / TH;
-  const int ntiles = B * tiles_h * tiles_w;
-  const int c0 = blockIdx.y * CB;
-  const int c = threadIdx.x % CB, r = threadIdx.x / CB;
-  const int cc = c0 + c;
-  float acc[KK + 1];
+struct DwGeom {
+  int G;       // channel groups (C / CPT)
+  int GPB;     // groups per block
+  int SPB;     // strip lanes per block
+  int nstrip;  // strips per row
+  long strips; // B * H * nstrip
+};
+
+template <typename T>
+DwGeom dw_geom(int B, int H, int W, int C) {
+  constexpr int CPT = DwCfg<T>::CPT;
+  DwGeom g;
+  g.G = C / CPT;
+  g.GPB = g.G < 32 ? g.G : 32;
+  g.SPB = 256 / g.GPB;
+  g.nstrip = (W + TW - 1) / TW;
+  g.strips = (long)B * H * g.nstrip;
+  return g;
+}
+
+template <typename T, int K, bool FLIP>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(int B, int H, int W, int C, DwGeom gm, const T* __restrict__ x,
+                                                     long ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, int add_identity,
+                                                     T* __restrict__ y, long ldy, int accumulate, T* __restrict__ gout,
+                                                     long ldg) {
+  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, WIN = TW + K - 1;
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [K*K][GPB*CPT]
+  const int CW = gm.GPB * CPT;
+  const int cbase = blockIdx.y * CW;
+  for (int e = threadIdx.x; e < K * K * CW; e += 256) {
+    const int tap = e / CW, cl = e % CW, c = cbase + cl;
+    wl[e] = c < C ? w[(long)c * K * K + (FLIP ? K * K - 1 - tap : tap)] : 0.f;
+  }
+  __syncthreads();
+  const int cg = threadIdx.x % gm.GPB, lane = threadIdx.x / gm.GPB;
+  if (lane >= gm.SPB) return;
+  const int c0 = cbase + cg * CPT;
+  if (c0 >= C) return;
+  float bv[CPT];
 #pragma unroll
-  for (int i = 0; i <= KK; ++i) acc[i] = 0.f;
-  for (int t = blockIdx.x * tpb; t < min(ntiles, (int)(blockIdx.x + 1) * tpb); ++t) {
-    int bid = t;
-    const int tw = bid % tiles_w; bid /= tiles_w;
-    const int th = bid % tiles_h; bid /= tiles_h;
-    const int b = bid;
-    const int h0 = th * TH, w0 = tw * TW;
-    const long img = (long)b * H * W;
-    __syncthreads();
-    for (int e = threadIdx.x; e < IH * IW * CB; e += 256) {
-      const int ce = e % CB, pix = e / CB;
-      const int ih = pix / IW, iw = pix % IW;
-      const int hh = h0 + ih - R, ww = w0 + iw - R;
-      float v = 0.f;
-      if (hh >= 0 && hh < H && ww >= 0 && ww < W && c0 + ce < C) v = ldf(x + (img + (long)hh * W + ww) * ldx + c0 + ce);
-      tile[e] = v;
-    }
-    __syncthreads();
-    if (cc < C && h0 + r < H) {
-      float g[TW];
-      const T* gr = dy + (img + (long)(h0 + r) * W + w0) * lddy + cc;
+  for (int e = 0; e < CPT; ++e) bv[e] = bias ? bias[c0 + e] : 0.f;
+  for (long s = (long)blockIdx.x * gm.SPB + lane; s < gm.strips; s += (long)gridDim.x * gm.SPB) {
+    const int ws = s % gm.nstrip;
+    const long bh = s / gm.nstrip;
+    const int h = bh % H;
+    const long img_row0 = (bh - h) * W;  // b * H * W
+    const int w0 = ws * TW;
+    float acc[TW][CPT];
 #pragma unroll
-      for (int j = 0; j < TW; ++j) g[j] = (w0 + j < W) ? ldf(gr + (long)j * lddy) : 0.f;
+    for (int t = 0; t < TW; ++t)
 #pragma unroll
-      for (int j = 0; j < TW; ++j) acc[KK] += g[j];
+      for (int e = 0; e < CPT; ++e) acc[t][e] = bv[e];
+    constexpr int UI = K == 7 ? 1 : K;  // keep the 7x7 window's live range to one input row
+#pragma unroll UI
+    for (int i = 0; i < K; ++i) {
+      const int hh = h + i - R;
+      if (hh < 0 || hh >= H) continue;
+      const T* row = x + (img_row0 + (long)hh * W) * ldx + c0;
+      float win[WIN][CPT];
 #pragma unroll
-      for (int i = 0; i < K; ++i) {
-        float row[IW];
+      for (int u = 0; u < WIN; ++u) {
+        const int ww = w0 + u - R;
+        if (ww >= 0 && ww < W) ldv<T>(row + (long)ww * ldx, win[u]);
+        else {
 #pragma unroll
-        for (int j = 0; j < IW; ++j) row[j] = tile[((r + i) * IW + j) * CB + c];
-#pragma unroll
-        for (int kj = 0; kj < K; ++kj) {
-          float s = 0.f;
-#pragma unroll
-          for (int j = 0; j < TW; ++j) s += g[j] * row[j + kj];
-          acc[i * K + kj] += s;
+          for (int e = 0; e < CPT; ++e) win[u][e] = 0.f;
         }
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        float wv[CPT];
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) wv[e] = wl[(i * K + j) * CW + cg * CPT + e];
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) acc[t][e] += wv[e] * win[t + j][e];
+      }
+    }
+    const long orow = img_row0 + (long)h * W;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) {
+      const int ww = w0 + t;
+      if (ww >= W) break;
+      if (add_identity) {
+        float xi[CPT];
+        ldv<T>(x + (orow + ww) * ldx + c0, xi);
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) acc[t][e] += xi[e];
+      }
+      T* yp = y + (orow + ww) * ldy + c0;
+      if (accumulate) {
+        float o[CPT];
+        ldv<T>(yp, o);
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) acc[t][e] += o[e];
+      }
+      stv<T>(yp, acc[t]);
+      if (gout) {
+        float gv[CPT];
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) gv[e] = gelu_f(acc[t][e]);
+        stv<T>(gout + (orow + ww) * ldg + c0, gv);
       }
     }
   }
-  // reduce over the TH row-threads of each channel: lanes c and c+32 share a wave when CB == 32
-  const int wave = threadIdx.x >> 6;
-  __syncthreads();
-  for (int i = 0; i <= KK; ++i) {
-    float v = acc[i];
-    v += __shfl_xor(v, 32, 64);  // the wave holds rows r = 2*wave, 2*wave+1 of the same 32 channels
-    if ((threadIdx.x & 63) < CB) red[wave][i][c] = v;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < (KK + 1) * CB; e += 256) {
-    const int ce = e % CB, i = e / CB;
-    if (c0 + ce < C) {
-      const float v = red[0][i][ce] + red[1][i][ce] + red[2][i][ce] + red[3][i][ce];
-      part[((long)blockIdx.x * C + c0 + ce) * (KK + 1) + i] = v;
+}
+
+// dW partials: block (strip block bx, channel chunk by, kernel-row group bz); each thread accumulates
+// KI kernel rows x K columns x CPT channels over its strips.
+template <typename T, int K, int KI>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(int B, int H, int W, int C, DwGeom gm, const T* __restrict__ x,
+                                                       long ldx, const T* __restrict__ dy, long lddy,
+                                                       float* __restrict__ part) {
+  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, WIN = TW + K - 1, KK1 = K * K + 1;
+  __shared__ float red[256][CPT + 1];
+  const int CW = gm.GPB * CPT;
+  const int cbase = blockIdx.y * CW;
+  const int cg = threadIdx.x % gm.GPB, lane = threadIdx.x / gm.GPB;
+  const int c0 = cbase + cg * CPT;
+  const bool active = lane < gm.SPB && c0 < C;
+  const int i0 = blockIdx.z * KI;
+  float acc[KI][K][CPT];
+  float dbs[CPT];
+#pragma unroll
+  for (int e = 0; e < CPT; ++e) dbs[e] = 0.f;
+#pragma unroll
+  for (int a = 0; a < KI; ++a)
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) acc[a][j][e] = 0.f;
+  if (active) {
+    for (long s = (long)blockIdx.x * gm.SPB + lane; s < gm.strips; s += (long)gridDim.x * gm.SPB) {
+      const int ws = s % gm.nstrip;
+      const long bh = s / gm.nstrip;
+      const int h = bh % H;
+      const long img_row0 = (bh - h) * W;
+      const int w0 = ws * TW;
+      float g[TW][CPT];
+      const long orow = img_row0 + (long)h * W;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        if (w0 + t < W) ldv<T>(dy + (orow + w0 + t) * lddy + c0, g[t]);
+        else {
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) g[t][e] = 0.f;
+        }
+      }
+      if (i0 == 0) {
+#pragma unroll
+        for (int t = 0; t < TW; ++t)
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) dbs[e] += g[t][e];
+      }
+#pragma unroll
+      for (int a = 0; a < KI; ++a) {
+        const int hh = h + i0 + a - R;
+        if (hh < 0 || hh >= H) continue;
+        const T* row = x + (img_row0 + (long)hh * W) * ldx + c0;
+        float win[WIN][CPT];
+#pragma unroll
+        for (int u = 0; u < WIN; ++u) {
+          const int ww = w0 + u - R;
+          if (ww >= 0 && ww < W) ldv<T>(row + (long)ww * ldx, win[u]);
+          else {
+#pragma unroll
+            for (int e = 0; e < CPT; ++e) win[u][e] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+#pragma unroll
+          for (int t = 0; t < TW; ++t)
+#pragma unroll
+            for (int e = 0; e < CPT; ++e) acc[a][j][e] += g[t][e] * win[t + j][e];
+      }
     }
   }
+  // reduce across the strip lanes of each channel group, one (a, j) tap at a time
+  const long pbase = (long)blockIdx.x * C * KK1;
+#pragma unroll
+  for (int tap = 0; tap <= KI * K; ++tap) {
+    if (tap == KI * K && i0 != 0) break;
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) {
+      float v = 0.f;
+      if (active) v = tap < KI * K ? acc[tap / K][tap % K][e] : dbs[e];
+      red[threadIdx.x][e] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < gm.GPB * CPT) {
+      const int g2 = threadIdx.x / CPT, e = threadIdx.x % CPT;
+      const int c = cbase + g2 * CPT + e;
+      if (c < C) {
+        float s = 0.f;
+        for (int l = 0; l < gm.SPB; ++l) s += red[l * gm.GPB + g2][e];
+        const int col = tap < KI * K ? (i0 + tap / K) * K + tap % K : K * K;
+        part[pbase + (long)c * KK1 + col] = s;
+      }
+    }
+    __syncthreads();
+  }
 }
 
-__global__ void dw_wgrad_sum_kernel(int nblk, int C, int KK1, const float* __restrict__ part, float* __restrict__ dw,
-                                    float* __restrict__ db) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= C * KK1) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * C * KK1 + e];
-  const int c = e / KK1, i = e % KK1;
-  if (i < KK1 - 1) dw[c * (KK1 - 1) + i] = s;
-  else if (db) db[c] = s;
+template <typename T>
+bool dw_aligned(int C, const void* p, long ld) {
+  constexpr int CPT = DwCfg<T>::CPT;
+  return C % CPT == 0 && ld % CPT == 0 && ((uintptr_t)p % 16) == 0;
 }
-
-int pick_cb(int) { return 32; }  // channels beyond C are masked
-
-int tiles_of(int B, int H, int W) { return B * ((H + TH - 1) / TH) * ((W + TW - 1) / TW); }
 
 template <typename T, bool FLIP>
 int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const float* w, const float* bias, int id,
            void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
-  const int CB = pick_cb(C);
-  dim3 grid(tiles_of(B, H, W), cdiv(C, CB));
-#define GO(KK, CBB)                                                                                             \
-  hipLaunchKernelGGL((dw_fwd_kernel<T, KK, CBB, FLIP>), grid, dim3(256), 0, s, B, H, W, C, (const T*)x, ldx, w, \
+  DFM_CHECK_ARG(dw_aligned<T>(C, x, ldx) && dw_aligned<T>(C, y, ldy) && (!gout || dw_aligned<T>(C, gout, ldg)),
+                "dwconv: C, row strides and pointers must be 16-byte vector aligned");
+  const DwGeom gm = dw_geom<T>(B, H, W, C);
+  const unsigned chunks = cdiv(gm.G, gm.GPB);
+  const long want = (long)min(cdiv(gm.strips, gm.SPB), 8192u);
+  dim3 grid((unsigned)want, chunks);
+  const size_t lds = (size_t)k * k * gm.GPB * DwCfg<T>::CPT * sizeof(float);
+#define GO(KK)                                                                                                   \
+  hipLaunchKernelGGL((dw_fwd_kernel<T, KK, FLIP>), grid, dim3(256), lds, s, B, H, W, C, gm, (const T*)x, ldx, w, \
                      bias, id, (T*)y, ldy, acc, (T*)gout, ldg)
-  if (k == 7) GO(7, 32);
-  else if (k == 3) GO(3, 32);
+  if (k == 7) GO(7);
+  else if (k == 3) GO(3);
   else {
     dfm_set_error("dwconv: k=%d unsupported", k);
     return DFM_ERR_ARG;
@@ -175,6 +268,18 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
 #undef GO
   DFM_LAUNCH_CHECK();
   return DFM_OK;
+}
+
+template <typename T>
+int wgrad_grid(int B, int H, int W, int C, int k, DwGeom& gm, dim3& grid) {
+  gm = dw_geom<T>(B, H, W, C);
+  const int KI = k == 3 ? 3 : 1;
+  const unsigned chunks = cdiv(gm.G, gm.GPB);
+  const unsigned zdim = k / KI;
+  long nsb = (1024 + (long)chunks * zdim - 1) / ((long)chunks * zdim);
+  nsb = max(1L, min(nsb, (long)cdiv(gm.strips, gm.SPB)));
+  grid = dim3((unsigned)nsb, chunks, zdim);
+  return (int)nsb;
 }
 }  // namespace
 
@@ -202,16 +307,14 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
   return DFM_ERR_DTYPE;
 }
 
-static int wgrad_blocks(int B, int H, int W, int& tpb) {
-  const int nt = tiles_of(B, H, W);
-  tpb = max(1, (nt + 255) / 256);  // ~256 blocks per channel block
-  return (nt + tpb - 1) / tpb;
-}
-
 extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k) {
-  int tpb;
-  const int nb = wgrad_blocks(B, H, W, tpb);
-  return (size_t)nb * C * (k * k + 1) * sizeof(float);
+  DwGeom gm;
+  dim3 grid;
+  const int nsb = wgrad_grid<float>(B, H, W, C, k, gm, grid);  // fp32 geometry has the most strip blocks
+  DwGeom gm2;
+  dim3 grid2;
+  const int nsb2 = wgrad_grid<bf16_t>(B, H, W, C, k, gm2, grid2);
+  return (size_t)max(nsb, nsb2) * C * (k * k + 1) * sizeof(float);
 }
 
 extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
@@ -220,25 +323,26 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   DFM_CHECK_ARG(x && dy && dw && workspace, "dfm_dwconv_bwd_weight: null argument");
   DFM_CHECK_ARG(k == 3 || k == 7, "dfm_dwconv_bwd_weight: k=%d unsupported", k);
   hipStream_t s = (hipStream_t)stream;
-  int tpb;
-  const int nb = wgrad_blocks(B, H, W, tpb);
-  const int CB = 32;
-  dim3 grid(nb, cdiv(C, CB));
   float* part = (float*)workspace;
-#define GO(TT, KK)                                                                                            \
-  hipLaunchKernelGGL((dw_wgrad_kernel<TT, KK, 32>), grid, dim3(256), 0, s, B, H, W, C, (const TT*)x, ldx,      \
-                     (const TT*)dy, lddy, tpb, part)
+  DwGeom gm;
+  dim3 grid;
+  int nsb;
   if (dtype == DFM_BF16) {
-    if (k == 7) GO(bf16_t, 7); else GO(bf16_t, 3);
+    DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
+    nsb = wgrad_grid<bf16_t>(B, H, W, C, k, gm, grid);
+    if (k == 7) hipLaunchKernelGGL((dw_wgrad_kernel<bf16_t, 7, 1>), grid, dim3(256), 0, s, B, H, W, C, gm, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, part);
+    else hipLaunchKernelGGL((dw_wgrad_kernel<bf16_t, 3, 3>), grid, dim3(256), 0, s, B, H, W, C, gm, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, part);
   } else if (dtype == DFM_F32) {
-    if (k == 7) GO(float, 7); else GO(float, 3);
+    DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
+    nsb = wgrad_grid<float>(B, H, W, C, k, gm, grid);
+    if (k == 7) hipLaunchKernelGGL((dw_wgrad_kernel<float, 7, 1>), grid, dim3(256), 0, s, B, H, W, C, gm, (const float*)x, ldx, (const float*)dy, lddy, part);
+    else hipLaunchKernelGGL((dw_wgrad_kernel<float, 3, 3>), grid, dim3(256), 0, s, B, H, W, C, gm, (const float*)x, ldx, (const float*)dy, lddy, part);
   } else {
     dfm_set_error("dfm_dwconv_bwd_weight: bad dtype");
     return DFM_ERR_DTYPE;
   }
-#undef GO
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, nb,
+  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, nsb,
                      (long)C * (k * k + 1), (const float*)part, dw, db, (long)(k * k + 1), 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

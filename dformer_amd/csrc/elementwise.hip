@@ -394,3 +394,82 @@ extern "C" int dfm_adamw(long n, float* p, const float* g, float* m, float* v, f
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
+
+// ================================================================ residual / layer-scale backward
+namespace {
+constexpr int RES_BLOCKS = 512;
+
+// One pass over dout and f: df = dout * colscale * rowscale (written) and per-block partial column
+// sums of dout * f * rowscale. Thread layout: 8 consecutive columns per thread (16-byte vectors for
+// bf16), TPR = C/8 threads per row, 256/TPR rows in flight per block.
+template <typename T>
+__global__ __launch_bounds__(256) void residual_bwd_kernel(long rows, int C, const T* __restrict__ dout, long ldo,
+                                                           const T* __restrict__ f, long ldf_,
+                                                           const float* __restrict__ colscale,
+                                                           const float* __restrict__ rowscale, long rps,
+                                                           T* __restrict__ df, long lddf, float* __restrict__ part) {
+  const int TPR = C / 8;
+  const int RL = 256 / TPR;
+  const int tc = threadIdx.x % TPR, rl = threadIdx.x / TPR;
+  const int c0 = tc * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float cs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = colscale ? colscale[c0 + e] : 1.f;
+  const long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
+  if (rl < RL) {
+    for (long r = r0 + rl; r < r1; r += RL) {
+      const float rs = rowscale ? rowscale[r / rps] : 1.f;
+      float d[8], fv[8], o[8];
+      ld8<T>(dout + r * ldo + c0, d);
+      ld8<T>(f + r * ldf_ + c0, fv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[e] += d[e] * fv[e] * rs;
+        o[e] = d[e] * cs[e] * rs;
+      }
+      st8<T>(df + r * lddf + c0, o);
+    }
+  }
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int t = c / 8, e = c % 8;
+    float s = 0.f;
+    for (int q = 0; q < RL; ++q) s += red[q * TPR + t][e];
+    part[(long)blockIdx.x * C + c] = s;
+  }
+}
+}  // namespace
+
+extern "C" size_t dfm_residual_bwd_workspace(long rows, int C) { return (size_t)RES_BLOCKS * C * sizeof(float); }
+
+extern "C" int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout, const void* f, long ldf_,
+                                const float* colscale, const float* rowscale, long rps, void* df, long lddf,
+                                float* dscale, void* ws, dfm_stream_t stream) {
+  DFM_CHECK_ARG(dout && f && df && dscale && ws && C % 8 == 0 && C <= 2048, "dfm_residual_bwd: bad argument");
+  DFM_CHECK_ARG(lddout % 8 == 0 && ldf_ % 8 == 0 && lddf % 8 == 0 && (uintptr_t)dout % 16 == 0 &&
+                    (uintptr_t)f % 16 == 0 && (uintptr_t)df % 16 == 0,
+                "dfm_residual_bwd: rows must be 16-byte aligned");
+  if (rows == 0) return DFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = (int)min((long)RES_BLOCKS, max(1L, rows / 64));
+  if (dtype == DFM_BF16)
+    hipLaunchKernelGGL(residual_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, rows, C, (const bf16_t*)dout, lddout,
+                       (const bf16_t*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (bf16_t*)df, lddf, (float*)ws);
+  else if (dtype == DFM_F32)
+    hipLaunchKernelGGL(residual_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, rows, C, (const float*)dout, lddout,
+                       (const float*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (float*)df, lddf, (float*)ws);
+  else {
+    dfm_set_error("dfm_residual_bwd: bad dtype");
+    return DFM_ERR_DTYPE;
+  }
+  DFM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(partial_sum_kernel<0>, dim3(cdiv(C, 64)), dim3(1024), 0, s, nblk, (long)C, (const float*)ws, dscale,
+                     (float*)nullptr, 0L, 0);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}

@@ -12,6 +12,8 @@
 // The epilogue stages the fp32 accumulator tile through LDS (two row halves) and applies bias /
 // activation / multiplier / residual on 8-column vectors, so every global read and write of the
 // output side is a coalesced 16-byte access (these GEMMs are mostly HBM-bound: K <= 2048).
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -41,6 +43,7 @@ struct GemmArgs {
   int colsum_acc;
   int ala, alb;    // operand rows 16-byte aligned (vector loads)
   int vec_ok;      // output-side rows 16-byte aligned (vector epilogue)
+  int mul_gelu_grad;
 };
 
 template <typename T> struct Mf;
@@ -175,7 +178,10 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
     if (a.act == 1) v = gelu_f(v);
     else if (a.act == 2) v = fmaxf(v, 0.0f);
   }
-  if (a.mul) v *= ldf((const TO*)a.mul + (long)m * a.ldmul + n);
+  if (a.mul) {
+    const float mv = ldf((const TO*)a.mul + (long)m * a.ldmul + n);
+    v *= a.mul_gelu_grad ? gelu_grad_f(mv) : mv;
+  }
   if (a.res) {
     float s = a.colscale ? a.colscale[n] : 1.0f;
     if (a.rowscale) s *= a.rowscale[m / a.rps];
@@ -183,33 +189,6 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
   }
   if (a.c_f32) ((float*)a.C)[ci] = v;
   else stf((TO*)a.C + ci, v);
-}
-
-// 8 consecutive T elements <-> floats
-template <typename T> DFM_INLINE void ld8(const T* p, float* v);
-template <> DFM_INLINE void ld8<bf16_t>(const bf16_t* p, float* v) {
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-template <> DFM_INLINE void ld8<float>(const float* p, float* v) {
-  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-template <typename T> DFM_INLINE void st8(T* p, const float* v);
-template <> DFM_INLINE void st8<bf16_t>(bf16_t* p, const float* v) {
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
-  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
-}
-template <> DFM_INLINE void st8<float>(float* p, const float* v) {
-  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
 template <typename TO>
@@ -238,8 +217,13 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
   }
   if (a.mul) {
     ld8<TO>((const TO*)a.mul + (long)m * a.ldmul + n, t);
+    if (a.mul_gelu_grad) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= t[e];
+      for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(t[e]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= t[e];
+    }
   }
   if (a.res) {
     ld8<TO>((const TO*)a.res + (long)m * a.ldres + n, t);
@@ -434,16 +418,21 @@ void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
   BN = Nw <= 32 ? 32 : (Nw <= 64 ? 64 : 128);
 }
 
-int choose_splits(const DfmGemmDesc* d) {
+int choose_splits(const DfmGemmDesc* d, int elem_bytes) {
   if (d->split_k >= 1) return d->split_k;
   int BM, BN;
   pick_tile(d, BM, BN);
   const int Nw = d->N + (d->colsum ? 1 : 0);
   const long tiles = (long)cdiv(d->M, BM) * cdiv(Nw, BN) * (d->batch > 0 ? d->batch : 1);
-  if (tiles >= 256 || d->K < 2048) return 1;
-  int s = (int)((512 + tiles - 1) / tiles);
-  s = min(s, d->K / 1024);
-  return max(1, min(s, 64));
+  if (tiles >= 512 || d->K < 2048) return 1;
+  // ~512 blocks, >= 1024 reduction elements per split, and fp32 partial traffic (write + read)
+  // at most ~1/4 of the operand bytes the GEMM streams
+  long s = (512 + tiles - 1) / tiles;
+  s = std::min(s, (long)d->K / 1024);
+  const double operand = (double)d->K * (d->M + d->N) * elem_bytes;
+  const double per_split = 2.0 * d->M * Nw * 4.0;
+  s = std::min(s, (long)(0.25 * operand / per_split));
+  return (int)std::max(1L, std::min(s, 1024L));
 }
 
 template <typename T>
@@ -462,13 +451,13 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.sa = d->stride_a; a.sb = d->stride_b; a.sc = d->stride_c;
   a.alpha = d->alpha; a.beta = d->beta; a.c_f32 = d->c_f32;
   a.bias = d->bias; a.act = d->act; a.preact = d->preact; a.ldpre = d->ldpre;
-  a.mul = d->mul; a.ldmul = d->ldmul; a.res = d->res; a.ldres = d->ldres;
+  a.mul = d->mul; a.ldmul = d->ldmul; a.res = d->res; a.ldres = d->ldres; a.mul_gelu_grad = d->mul_gelu_grad;
   a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
   a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
   int BM, BN;
   pick_tile(d, BM, BN);
-  a.splits = choose_splits(d);
+  a.splits = choose_splits(d, sizeof(T));
   if (a.splits > 1) DFM_CHECK_ARG(ws != nullptr, "dfm_gemm: split-K needs a workspace");
   a.ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0);
   a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0);
@@ -491,7 +480,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 }  // namespace
 
 extern "C" size_t dfm_gemm_workspace_size(const DfmGemmDesc* d) {
-  const int s = choose_splits(d);
+  const int s = std::max(choose_splits(d, 2), choose_splits(d, 4));
   if (s <= 1) return 0;
   return (size_t)s * (d->batch > 0 ? d->batch : 1) * d->M * (d->N + (d->colsum ? 1 : 0)) * sizeof(float);
 }

@@ -53,6 +53,7 @@ template <typename T, int G>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, int C, const T* __restrict__ x, long ldx,
                                                      const T* __restrict__ dy, long lddy, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const T* __restrict__ dres, long lddres,
                                                      T* __restrict__ dx, long lddx, int accumulate,
                                                      float* __restrict__ part) {
   constexpr int RPB = 256 / G;
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(long rows, int C, const T* 
       const int c = j * G + lg;
       if (c < C) {
         float v = rs * (g[j] - sa - xh[j] * sb);
+        if (dres) v += ldf(dres + row * lddres + c);
         if (accumulate) v += ldf(dr + c);
         stf(dr + c, v);
       }
@@ -158,14 +160,15 @@ int ln_fwd(long rows, int C, const void* x, long ldx, const float* gamma, const 
 
 template <typename T>
 int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy, const float* gamma,
-           const float* mean, const float* rstd, void* dx, long lddx, int acc, float* dg, float* db, void* ws,
+           const float* mean, const float* rstd, const void* dres, long lddres, void* dx, long lddx, int acc,
+           float* dg, float* db, void* ws,
            hipStream_t s) {
   const int G = pick_g(C);
   const unsigned grid = min((unsigned)LN_BWD_BLOCKS, cdiv(rows, 256 / G));
   float* part = (float*)ws;
 #define GO(GG)                                                                                             \
   hipLaunchKernelGGL((ln_bwd_kernel<T, GG>), dim3(grid), dim3(256), 0, s, rows, C, (const T*)x, ldx,         \
-                     (const T*)dy, lddy, gamma, mean, rstd, (T*)dx, lddx, acc, part)
+                     (const T*)dy, lddy, gamma, mean, rstd, (const T*)dres, lddres, (T*)dx, lddx, acc, part)
   switch (G) {
     case 8: GO(8); break;
     case 16: GO(16); break;
@@ -199,17 +202,18 @@ extern "C" size_t dfm_layernorm_bwd_workspace(long rows, int C) {
 }
 
 extern "C" int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
-                                 const float* gamma, const float* mean, const float* rstd, void* dx, long lddx,
-                                 int accumulate, float* dgamma, float* dbeta, void* workspace, dfm_stream_t stream) {
+                                 const float* gamma, const float* mean, const float* rstd, const void* dres,
+                                 long lddres, void* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
+                                 void* workspace, dfm_stream_t stream) {
   DFM_CHECK_ARG(C > 0 && C <= 1024, "dfm_layernorm_bwd: C=%d unsupported", C);
   DFM_CHECK_ARG(x && dy && dx && gamma && mean && rstd && dgamma && dbeta && workspace,
                 "dfm_layernorm_bwd: null argument");
   if (rows == 0) return DFM_OK;
   if (dtype == DFM_BF16)
-    return ln_bwd<bf16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dx, lddx, accumulate, dgamma, dbeta,
+    return ln_bwd<bf16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
                           workspace, (hipStream_t)stream);
   if (dtype == DFM_F32)
-    return ln_bwd<float>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dx, lddx, accumulate, dgamma, dbeta,
+    return ln_bwd<float>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
                          workspace, (hipStream_t)stream);
   dfm_set_error("dfm_layernorm_bwd: bad dtype");
   return DFM_ERR_DTYPE;

@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
-from .functional import wcast
+from .functional import gslot, gslot2, wcast
 
 
 def _allreduce(t, sync):
@@ -61,7 +61,7 @@ class ConvBNActFn(torch.autograd.Function):
             dy = K.relu_bwd(dy, y)
         st2 = _allreduce(K.bn_bwd_stats(y0, dy, mean, rstd), ctx.sync)
         dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
-        dW = K.linear_wgrad(dy0, x)
+        dW = K.linear_wgrad(dy0, x, out=gslot2(w))
         dx = K.linear_dgrad(dy0, wcast(x.dtype, w))
         dres = dy if ctx.has_res else None
         return dx, dres, dW.view_as(w), st2[1].clone(), st2[0].clone(), None, None, None
@@ -76,19 +76,19 @@ class LinearActFn(torch.autograd.Function):
         out = torch.empty(x.shape[0], w.shape[0], device=x.device,
                           dtype=torch.float32 if out_f32 else x.dtype)
         K.linear(x, Wc, b, act=act, out=out)
-        ctx.save_for_backward(x, w, out)
+        ctx.save_for_backward(x, w, b, out)
         ctx.act = act
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
+        x, w, b, y = ctx.saved_tensors
         dy = dy.contiguous()
         if ctx.act == 2:
             dy = K.relu_bwd(dy, y)
         if dy.dtype != x.dtype:
             dy = K.cast(dy, x.dtype)
-        dW, db = K.linear_wgrad(dy, x, bias_grad=True)
+        dW, db = K.linear_wgrad(dy, x, out=gslot2(w), bias_grad=True, bias_out=gslot(b))
         dx = K.linear_dgrad(dy, wcast(x.dtype, w))
         return dx, dW.view_as(w), db, None, None
 
@@ -153,17 +153,17 @@ class ChannelDropoutLinearFn(torch.autograd.Function):
             for i in range(B):
                 K.scale_mul(x[i * rows:(i + 1) * rows], colscale=scale[i], out=xs[i * rows:(i + 1) * rows])
         y = K.linear(xs, wcast(dt, w), b)
-        ctx.save_for_backward(xs, w, scale)
+        ctx.save_for_backward(xs, w, b, scale)
         ctx.B = B
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xs, w, scale = ctx.saved_tensors
+        xs, w, b, scale = ctx.saved_tensors
         dy = dy.contiguous()
         if dy.dtype != xs.dtype:
             dy = K.cast(dy, xs.dtype)
-        dW, db = K.linear_wgrad(dy, xs, bias_grad=True)
+        dW, db = K.linear_wgrad(dy, xs, out=gslot2(w), bias_grad=True, bias_out=gslot(b))
         dx = K.linear_dgrad(dy, wcast(xs.dtype, w))
         if scale is not None:
             rows = dx.shape[0] // ctx.B

@@ -47,6 +47,35 @@ def wcast(dtype, *params):
     return w
 
 
+_GSLOT = {}
+
+
+def register_grad_slot(p, flat, offset):
+    """Weight gradients of `p` are written straight into flat[offset:offset+numel] (the optimizer's
+    flat gradient buffer); autograd then adopts that view as p.grad without a copy."""
+    _GSLOT[id(p)] = (flat, offset, tuple(p.shape))
+
+
+def clear_grad_slots():
+    _GSLOT.clear()
+
+
+def gslot(p):
+    s = _GSLOT.get(id(p))
+    if s is None:
+        return None
+    flat, off, shape = s
+    n = 1
+    for d in shape:
+        n *= d
+    return flat[off:off + n].view(shape)
+
+
+def gslot2(p):
+    t = gslot(p)
+    return None if t is None else t.view(t.shape[0], -1)
+
+
 def _cat1(*vs):
     """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
     key = tuple(id(v) for v in vs) + ("bias",)
@@ -78,30 +107,28 @@ class ConvFFNFn(torch.autograd.Function):
         hpre = K.dwconv(h, shape, wpos, bpos, 3, add_identity=True, gelu_out=g)
         f = torch.empty(P, C, device=x.device, dtype=dt)
         out = K.linear(g, W2, b2, preact=f, res=x, colscale=ls, rowscale=rowscale, rows_per_scale=H * W)
-        ctx.save_for_backward(x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, wpos, w2, ls)
+        ctx.save_for_backward(x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
         ctx.shape = shape
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, wpos, w2, ls = ctx.saved_tensors
+        x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
         B, H, W = ctx.shape
         dt = x.dtype
         dout = dout.contiguous()
         W1, W2 = wcast(dt, w1), wcast(dt, w2)
         rps = H * W
-        dls = K.colsum(dout, mul=f, rowscale=rowscale, rows_per_scale=rps)
-        df = K.scale_mul(dout, colscale=ls, rowscale=rowscale, rows_per_scale=rps)
-        dW2, db2 = K.linear_wgrad(df, g, bias_grad=True)
-        dg = K.linear_dgrad(df, W2)
-        dhpre = K.gelu_bwd(dg, hpre)
-        dwpos, dbpos = K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3)
+        df, dls = K.residual_bwd(dout, f, ls, rowscale, rps)
+        dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
+        dhpre = K.linear_dgrad(df, W2, gelu_grad_of=hpre)  # GELU backward fused into the epilogue
+        dwpos, dbpos = K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=gslot(wpos), db=gslot(bpos))
         dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
-        dW1, db1 = K.linear_wgrad(dh, xn, bias_grad=True)
+        dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
         dxn = K.linear_dgrad(dh, W1)
-        dx = dout.clone()
-        _, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dx=dx, accumulate=True)
-        return dx, None, None, dlnw, dlnb, dW1, db1, dwpos.view_as(wpos), dbpos, dW2, db2, dls
+        dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
+        return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
+                dls)
 
 
 # ====================================================================== Attention (+ residuals)
@@ -189,19 +216,18 @@ class AttentionFn(torch.autograd.Function):
         grads = {}
         dx1 = dx1.contiguous()
         # projections
-        grads["ls1"] = K.colsum(dx1, mul=p1, rowscale=rowscale, rows_per_scale=rps)
-        dp1 = K.scale_mul(dx1, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
-        grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, bias_grad=True)
+        dp1, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps)
+        grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, out=gslot2(wp), bias_grad=True, bias_out=gslot(bp))
         df = K.linear_dgrad(dp1, wcast(dt, wp))
         if drop_depth:
-            dxe = dxe1.contiguous().clone() if dxe1 is not None else torch.zeros_like(xe)
+            dxe_res = dxe1.contiguous() if dxe1 is not None else None
         else:
             dxe1 = dxe1.contiguous()
-            grads["ls1e"] = K.colsum(dxe1, mul=p1e, rowscale=rowscale_e, rows_per_scale=rps)
-            dp1e = K.scale_mul(dxe1, colscale=ls1e, rowscale=rowscale_e, rows_per_scale=rps)
-            grads["wpe"], grads["bpe"] = K.linear_wgrad(dp1e, f, bias_grad=True)
+            dp1e, grads["ls1e"] = K.residual_bwd(dxe1, p1e, ls1e, rowscale_e, rps)
+            grads["wpe"], grads["bpe"] = K.linear_wgrad(dp1e, f, out=gslot2(wpe), bias_grad=True,
+                                                        bias_out=gslot(bpe))
             K.linear_dgrad(dp1e, wcast(dt, wpe), out=df, accumulate=True)
-            dxe = dxe1.clone()
+            dxe_res = dxe1
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
@@ -209,11 +235,11 @@ class AttentionFn(torch.autograd.Function):
         dcxe = df[:, fw - Ch:]
         K.scale_mul(dcxe, mul=xep, out=dcx)
         dxep = K.scale_mul(dcxe, mul=cx)
-        grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, bias_grad=True)
+        grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=gslot2(web), bias_grad=True, bias_out=gslot(beb))
         de2 = K.linear_dgrad(dxep, wcast(dt, web))
-        grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7)
+        grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7, dw=gslot(wec), db=gslot(bec))
         de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
-        grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, bias_grad=True)
+        grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, out=gslot2(wef), bias_grad=True, bias_out=gslot(bef))
         dxen = K.linear_dgrad(de1, wcast(dt, wef))
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
@@ -225,19 +251,20 @@ class AttentionFn(torch.autograd.Function):
             dkv = torch.empty(P, C, device=dev, dtype=dt)
             K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
                               dkv[:, :Ch], dkv[:, Ch:])
-            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, bias_grad=True)
+            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, out=gslot2(wsc), bias_grad=True,
+                                                        bias_out=gslot(bsc))
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
             K.pool7_bwd(dpooled[:, C:], shape, dx=dxen, accumulate=True)
-            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, bias_grad=True)
+            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, out=gslot2(wkv), bias_grad=True, bias_out=gslot(bkv))
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
         K.scale_mul(dqa, mul=a, out=dq)
         da = K.scale_mul(dqa, mul=q)
-        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, bias_grad=True)
+        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=gslot2(wa), bias_grad=True, bias_out=gslot(ba))
         dapre = K.linear_dgrad(da, wcast(dt, wa))
-        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7)
+        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=gslot(wconv), db=gslot(bconv))
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.gelu_bwd(dg, lpre, out=dl)
         # q | q_cut | l
@@ -249,9 +276,8 @@ class AttentionFn(torch.autograd.Function):
             dxn = K.linear_dgrad(dqcl, Wqcl)
         else:
             K.linear_dgrad(dqcl, Wqcl, out=dxn, accumulate=True)
-        dx = dx1.clone()
-        _, grads["n_w"], grads["n_b"] = K.layernorm_bwd(x, dxn, n_w, mu1, rs1, dx=dx, accumulate=True)
-        _, grads["ne_w"], grads["ne_b"] = K.layernorm_bwd(xe, dxen, ne_w, mu2, rs2, dx=dxe, accumulate=True)
+        dx, grads["n_w"], grads["n_b"] = K.layernorm_bwd(x, dxn, n_w, mu1, rs1, dres=dx1)
+        dxe, grads["ne_w"], grads["ne_b"] = K.layernorm_bwd(xe, dxen, ne_w, mu2, rs2, dres=dxe_res)
         out = []
         for name, p in zip(ATTN_PARAM_NAMES, params):
             gr = grads.get(name)

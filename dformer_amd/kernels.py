@@ -36,7 +36,7 @@ def rows_of(t):
 def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
          ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
-         colsum_accumulate=False):
+         colsum_accumulate=False, mul_gelu_grad=False):
     dt = dtype_code(a)
     assert b.dtype == a.dtype, (a.dtype, b.dtype)
     c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
@@ -45,7 +45,7 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     d = _lib.GemmDesc(M, N, K, batch, int(a_kcontig), int(b_kcontig), lda, ldb, ldc, stride_a, stride_b, stride_c,
                       alpha, beta, c_f32, ptr(bias), act, ptr(preact), ldpre, ptr(mul), ldmul, ptr(res), ldres,
                       ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0, ptr(colsum),
-                      int(colsum_accumulate))
+                      int(colsum_accumulate), int(mul_gelu_grad))
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
@@ -65,26 +65,32 @@ def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=
                 colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0)
 
 
-def linear_dgrad(dy, w, out=None, accumulate=False, mul=None):
-    """dx[M,K] (+)= dy[M,N] @ w[N,K]   (optionally times `mul` elementwise)."""
+def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None):
+    """dx[M,K] (+)= dy[M,N] @ w[N,K]   (times `mul` elementwise, or times gelu'(gelu_grad_of))."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
+    if gelu_grad_of is not None:
+        mul = gelu_grad_of
     return gemm(dy, w, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=ld(dy), ldb=ld(w), out=out, ldc=ld(out),
-                beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0)
+                beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0,
+                mul_gelu_grad=gelu_grad_of is not None)
 
 
-def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False):
+def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False, bias_out=None):
     """dW[N,K] (+)= dy[M,N]^T @ x[M,K]  (float32 output, split-K over M).
-    bias_grad=True also returns db[N] = sum_M dy (fused: virtual all-ones column of x)."""
+    bias_grad=True also returns db[N] = sum_M dy (fused: virtual all-ones column of x), written
+    into `bias_out` when given (e.g. a slot of the optimizer's flat gradient buffer)."""
     M, N = dy.shape
     K = x.shape[1]
     if out is None:
         out = torch.empty(N, K, device=dy.device, dtype=torch.float32)
-    db = torch.empty(N, device=dy.device, dtype=torch.float32) if bias_grad else None
+    db = None
+    if bias_grad:
+        db = bias_out if bias_out is not None else torch.empty(N, device=dy.device, dtype=torch.float32)
     gemm(dy, x, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=ld(dy), ldb=ld(x), out=out,
-         ldc=ld(out), beta=1.0 if accumulate else 0.0, colsum=db)
+         ldc=ld(out), beta=1.0 if accumulate else 0.0, colsum=db, colsum_accumulate=accumulate)
     return (out, db) if bias_grad else out
 
 
@@ -116,7 +122,8 @@ def layernorm(x, gamma, beta, eps=1e-6, out=None):
     return out, mean, rstd
 
 
-def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False):
+def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dres=None):
+    """dx = LN'(dy) [+ dres] [+ dx when accumulate]; returns (dx, dgamma, dbeta)."""
     rows, C = x.shape
     if dx is None:
         dx = torch.empty(rows, C, device=x.device, dtype=x.dtype)
@@ -125,9 +132,22 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False):
     db = torch.empty(C, device=x.device, dtype=torch.float32)
     ws = _ws(lib.dfm_layernorm_bwd_workspace(rows, C), x.device)
     check(lib.dfm_layernorm_bwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(gamma), ptr(mean),
-                                ptr(rstd), ptr(dx), ld(dx), int(accumulate), ptr(dg), ptr(db), ptr(ws), stream()),
-          "dfm_layernorm_bwd")
+                                ptr(rstd), ptr(dres), ld(dres) if dres is not None else 0, ptr(dx), ld(dx),
+                                int(accumulate), ptr(dg), ptr(db), ptr(ws), stream()), "dfm_layernorm_bwd")
     return dx, dg, db
+
+
+def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
+    """Block residual x + rowscale*ls*f backward: returns (df = dout*ls*rowscale, dls = sum dout*f*rowscale)."""
+    rows, C = dout.shape
+    if df is None:
+        df = torch.empty(rows, C, device=dout.device, dtype=dout.dtype)
+    dls = torch.empty(C, device=dout.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_residual_bwd_workspace(rows, C), dout.device)
+    check(lib.dfm_residual_bwd(dtype_code(dout), rows, C, ptr(dout), ld(dout), ptr(f), ld(f), ptr(colscale),
+                               ptr(rowscale), rows_per_scale, ptr(df), ld(df), ptr(dls), ptr(ws), stream()),
+          "dfm_residual_bwd")
+    return df, dls
 
 
 # ---------------------------------------------------------------------------- depthwise conv
@@ -154,11 +174,13 @@ def dwconv_bwd_data(dy, shape, w, k, add_identity=False, dx=None, accumulate=Fal
     return dx
 
 
-def dwconv_bwd_weight(x, dy, shape, k):
+def dwconv_bwd_weight(x, dy, shape, k, dw=None, db=None):
     B, H, W = shape
     C = x.shape[1]
-    dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
-    db = torch.empty(C, device=x.device, dtype=torch.float32)
+    if dw is None:
+        dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(C, device=x.device, dtype=torch.float32)
     ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
     check(lib.dfm_dwconv_bwd_weight(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(dw), ptr(db),
                                     ptr(ws), stream()), "dfm_dwconv_bwd_weight")

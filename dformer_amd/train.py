@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
-from .functional import invalidate_weights, register_shadow
+from .functional import invalidate_weights, register_grad_slot, register_shadow
 
 
 def group_weight(module, norm_layer=nn.BatchNorm2d):
@@ -67,6 +67,7 @@ class _FlatGroup:
             self.flat[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.flat[off:off + k].view_as(p)
             self.slots[p] = (off, k)
+            register_grad_slot(p, self.grad, off)
             off += k
         if self.shadow is not None:
             self.shadow.copy_(self.flat)
@@ -114,7 +115,8 @@ class GradBuckets:
     def _hook(self, p):
         bi, g = self.owner[p]
         off, k = g.slots[p]
-        g.grad[off:off + k].copy_(p.grad.reshape(-1))
+        if p.grad.data_ptr() != g.grad.data_ptr() + 4 * off:  # kernels usually wrote the slot directly
+            g.grad[off:off + k].copy_(p.grad.reshape(-1))
         p.grad = None
         self.pending[bi] -= 1
         if self.pending[bi] == 0 and self.world > 1:

@@ -79,6 +79,7 @@ typedef struct DfmGemmDesc {
   float* colsum; /* optional float32 [M]: (+)= alpha * sum_k A(m,k) — the bias gradient of a wgrad
                     GEMM, computed as a virtual all-ones column of B (batch must be 1) */
   int colsum_accumulate;
+  int mul_gelu_grad; /* 1: the multiplier is gelu'(mul[m,n]) (GELU backward fused into a dgrad GEMM) */
 } DfmGemmDesc;
 
 size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);
@@ -93,9 +94,20 @@ int dfm_layernorm_fwd(int dtype, long rows, int C, const void* x, long ldx, cons
                       const float* beta, float eps, void* y, long ldy, float* mean, float* rstd,
                       dfm_stream_t stream);
 size_t dfm_layernorm_bwd_workspace(long rows, int C);
+/* dx = LN-backward(dy) [+ dres] [+ dx when accumulate]  (dres: the residual branch's gradient) */
 int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
-                      const float* gamma, const float* mean, const float* rstd, void* dx, long lddx,
-                      int accumulate, float* dgamma, float* dbeta, void* workspace, dfm_stream_t stream);
+                      const float* gamma, const float* mean, const float* rstd, const void* dres, long lddres,
+                      void* dx, long lddx, int accumulate, float* dgamma, float* dbeta, void* workspace,
+                      dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- residual / layer-scale backward
+ * Block.forward's x + DropPath(ls * f) (DFormer.py:173-179), backward in one pass over dout and f:
+ *   df[r,c] = dout[r,c] * colscale[c] * rowscale[r/rps];   dscale[c] = sum_r dout * f * rowscale[r/rps]
+ * (rowscale NULL = 1; dscale overwritten; workspace from dfm_residual_bwd_workspace). */
+size_t dfm_residual_bwd_workspace(long rows, int C);
+int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout, const void* f, long ldf,
+                     const float* colscale, const float* rowscale, long rows_per_scale, void* df, long lddf,
+                     float* dscale, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- depthwise conv k x k, NHWC
  * DFormer.py:80-81 (7x7 conv/e_conv, pad 3) and DFormer.py:54,62 (3x3 pos + identity).

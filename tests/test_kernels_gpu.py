@@ -304,3 +304,36 @@ def test_adamw_matches_torch():
         k.adamw(p, g * step, m, v, 6e-5, 0.9, 0.999, 1e-8, 0.01, step, 1.0, copy)
     assert rel(p, pr.detach()) < 1e-6
     assert rel(copy.float(), p) < 1e-2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("C", [32, 64, 256, 576])
+def test_residual_bwd_and_ln_dres(dt, C):
+    k = K()
+    rows, B = 4000, 4
+    dout = torch.randn(rows, C, device=DEV).to(dt)
+    f = torch.randn(rows, C, device=DEV).to(dt)
+    ls = torch.rand(C, device=DEV)
+    rs = torch.rand(B, device=DEV)
+    df, dls = k.residual_bwd(dout, f, ls, rs, rows // B)
+    rsx = rs.repeat_interleave(rows // B)[:, None]
+    assert rel(df.float(), dout.float() * ls * rsx) < TOL[dt]
+    assert rel(dls, (dout.float() * f.float() * rsx).sum(0)) < TOL[dt]
+    x = torch.randn(rows, C, device=DEV).to(dt)
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    _, mean, rstd = k.layernorm(x, g, b)
+    dx_a, _, _ = k.layernorm_bwd(x, f, g, mean, rstd, dres=dout)
+    dx_b, _, _ = k.layernorm_bwd(x, f, g, mean, rstd)
+    assert rel(dx_a.float(), dx_b.float() + dout.float()) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_dgrad_gelu_grad_epilogue(dt):
+    k = K()
+    dy = torch.randn(3000, 64, device=DEV).to(dt)
+    w = torch.randn(64, 512, device=DEV).to(dt)
+    pre = torch.randn(3000, 512, device=DEV).to(dt)
+    out = k.linear_dgrad(dy, w, gelu_grad_of=pre)
+    pr = pre.float().requires_grad_()
+    torch.nn.functional.gelu(pr).backward(dy.float() @ w.float())
+    assert rel(out.float(), pr.grad) < TOL[dt]
