@@ -33,11 +33,33 @@ template <> struct Num<bf16_t> {
 template <typename T> DFM_INLINE float ldf(const T* p) { return Num<T>::load(p); }
 template <typename T> DFM_INLINE void stf(T* p, float v) { *p = Num<T>::from_f(v); }
 
-DFM_INLINE float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU (nn.GELU() default, DFormer.py:51,78) without the branchy libm erff: the
+// normal CDF from Abramowitz & Stegun 7.1.26 (|erf error| <= 1.5e-7, one v_rcp + one v_exp),
+// evaluated on the tail side so Phi(x) for x << 0 keeps its relative accuracy; the same
+// exponential gives the normal pdf for the derivative.
+DFM_INLINE void normal_cdf_pdf(float x, float& cdf, float& pdf) {
+  const float u = x * 0.70710678118654752f;
+  const float au = fabsf(u);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, au, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __expf(-au * au);
+  const float tail = 0.5f * p * e;  // Phi(-|x|)
+  cdf = u < 0.0f ? tail : 1.0f - tail;
+  pdf = 0.39894228040143268f * e;
+}
+DFM_INLINE float gelu_f(float x) {
+  float c, d;
+  normal_cdf_pdf(x, c, d);
+  return x * c;
+}
 DFM_INLINE float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float c, d;
+  normal_cdf_pdf(x, c, d);
+  return fmaf(x, d, c);
 }
 
 DFM_INLINE float wave_sum(float v) {
@@ -72,6 +94,30 @@ template <> DFM_INLINE void ld8<float>(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
+// 8 consecutive elements as raw 16-byte words (one for bf16, two for float): lets a kernel issue
+// all of its loads before it unpacks and uses any of them.
+template <typename T> struct Raw8 { uint4 w[sizeof(T) / 2]; };
+template <typename T> DFM_INLINE Raw8<T> ldraw8(const T* p) {
+  Raw8<T> r;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 2); ++i) r.w[i] = reinterpret_cast<const uint4*>(p)[i];
+  return r;
+}
+DFM_INLINE void unpack8(const Raw8<bf16_t>& r, float* v) {
+  const uint32_t w[4] = {r.w[0].x, r.w[0].y, r.w[0].z, r.w[0].w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+DFM_INLINE void unpack8(const Raw8<float>& r, float* v) {
+  v[0] = __uint_as_float(r.w[0].x); v[1] = __uint_as_float(r.w[0].y);
+  v[2] = __uint_as_float(r.w[0].z); v[3] = __uint_as_float(r.w[0].w);
+  v[4] = __uint_as_float(r.w[1].x); v[5] = __uint_as_float(r.w[1].y);
+  v[6] = __uint_as_float(r.w[1].z); v[7] = __uint_as_float(r.w[1].w);
+}
+
 template <typename T> DFM_INLINE void st8(T* p, const float* v);
 template <> DFM_INLINE void st8<bf16_t>(bf16_t* p, const float* v) {
   uint32_t w[4];

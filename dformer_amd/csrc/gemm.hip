@@ -23,7 +23,7 @@ struct GemmArgs {
   const void* B;
   void* C;
   float* ws;
-  int M, N, K, batch, splits, Nw;
+  int M, N, K, batch, splits, Nw, ldw;  // ldw: split-K workspace row stride (Nw rounded up to 8)
   long lda, ldb, ldc, sa, sb, sc;
   float alpha, beta;
   int c_f32;
@@ -92,25 +92,26 @@ DFM_INLINE uint4 load_vec(const T* __restrict__ p, long ld, int r, int k, int ro
   }
 }
 
-template <typename T, int R, int BK, bool KC>
+template <typename T, int R, int BK, bool KC, int NT>
 struct TileGeom {
   static constexpr int VEC = Mf<T>::VEC;
   // k-contiguous: [R][BK+PADK]; row-contiguous: [BK][R+PADR]
   static constexpr int LD = KC ? (BK + Mf<T>::PADK) : (R + Mf<T>::PADR);
   static constexpr int ELEMS = KC ? R * LD : BK * LD;
   static constexpr int TOTAL = R * BK / VEC;        // 16-byte vectors per tile
-  static constexpr int NVEC = (TOTAL + 255) / 256;  // vectors per thread (last one partial)
+  static constexpr int NVEC = (TOTAL + NT - 1) / NT;  // vectors per thread (last one partial)
 };
 
-template <typename T, int R, int BK, bool KC>
+// Guarded tile load: zero fill outside [0, rows) x [0, K), scalar fallback for unaligned rows.
+template <typename T, int R, int BK, bool KC, int NT>
 DFM_INLINE void stage_load(uint4* regs, const T* __restrict__ base, long ld, int r0, int k0, int rows, int K,
                            bool aligned, int ones_r = -1) {
-  using G = TileGeom<T, R, BK, KC>;
+  using G = TileGeom<T, R, BK, KC, NT>;
   constexpr int VEC = G::VEC;
 #pragma unroll
   for (int i = 0; i < G::NVEC; ++i) {
-    const int v = threadIdx.x + i * 256;
-    if (G::TOTAL % 256 != 0 && v >= G::TOTAL) break;
+    const int v = threadIdx.x + i * NT;
+    if (G::TOTAL % NT != 0 && v >= G::TOTAL) break;
     if (KC) {
       const int r = v / (BK / VEC), kc = (v % (BK / VEC)) * VEC;
       regs[i] = load_vec<T, true>(base, ld, r0 + r, k0 + kc, rows, K, aligned, ones_r);
@@ -121,14 +122,86 @@ DFM_INLINE void stage_load(uint4* regs, const T* __restrict__ base, long ld, int
   }
 }
 
-template <typename T, int R, int BK, bool KC>
-DFM_INLINE void stage_store(const uint4* regs, T* lds) {
-  using G = TileGeom<T, R, BK, KC>;
+// Branch-free tile loads for a k-range fully inside [0, K) with 16-byte aligned rows. Each
+// thread's byte offsets inside the tile are computed once per block (rows past the edge point
+// at a clamped in-bounds row instead of being zero-filled: they only feed output rows / columns
+// that are never stored); per k-slice only the wave-uniform tile base moves, so every load is
+// one unconditional `global_load_dwordx4 v, v_off, s_base`.
+template <typename T, int R, int BK, bool KC, int NT>
+DFM_INLINE void fast_offsets(unsigned* off, long ld, int r0, int rows) {
+  using G = TileGeom<T, R, BK, KC, NT>;
   constexpr int VEC = G::VEC;
 #pragma unroll
   for (int i = 0; i < G::NVEC; ++i) {
-    const int v = threadIdx.x + i * 256;
-    if (G::TOTAL % 256 != 0 && v >= G::TOTAL) break;
+    int v = threadIdx.x + i * NT;
+    if (G::TOTAL % NT != 0 && v >= G::TOTAL) v = 0;
+    if (KC) {
+      const int r = r0 + v / (BK / VEC), kc = (v % (BK / VEC)) * VEC;
+      const int rr = r < rows ? r : rows - 1;
+      off[i] = (unsigned)(((long)rr * ld + kc) * sizeof(T));
+    } else {
+      const int k = v / (R / VEC), rc = r0 + (v % (R / VEC)) * VEC;
+      const int rr = rc < rows ? rc : 0;
+      off[i] = (unsigned)(((long)k * ld + rr) * sizeof(T));
+    }
+  }
+}
+
+template <typename T, int R, int BK, bool KC, int NT>
+DFM_INLINE void stage_load_fast(uint4* regs, __amdgpu_buffer_rsrc_t rsrc, int soff, const unsigned* off) {
+  using G = TileGeom<T, R, BK, KC, NT>;
+#pragma unroll
+  for (int i = 0; i < G::NVEC; ++i) {
+    if (G::TOTAL % NT != 0 && threadIdx.x + i * NT >= G::TOTAL) break;
+    regs[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[i], soff, 0));
+  }
+}
+
+// After a fast load: write the virtual all-ones operand row `ones_r` (fused bias gradient) into
+// the staged registers. Applied right before the LDS store, when the loads have landed anyway.
+template <typename T>
+DFM_INLINE unsigned one_bits() { return sizeof(T) == 2 ? 0x3f80u : 0x3f800000u; }
+
+template <typename T>
+DFM_INLINE uint4 set_one(uint4 u, int e) {  // element e (0 <= e < VEC, or no-op) := 1.0
+  unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (sizeof(T) == 2) {
+      w[j] = (e == 2 * j) ? ((w[j] & 0xffff0000u) | 0x3f80u) : w[j];
+      w[j] = (e == 2 * j + 1) ? ((w[j] & 0x0000ffffu) | 0x3f800000u) : w[j];
+    } else {
+      w[j] = (e == j) ? 0x3f800000u : w[j];
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <typename T, int R, int BK, bool KC, int NT>
+DFM_INLINE void patch_ones(uint4* regs, int r0, int ones_r) {
+  using G = TileGeom<T, R, BK, KC, NT>;
+  constexpr int VEC = G::VEC;
+  const unsigned one = sizeof(T) == 2 ? 0x3f803f80u : 0x3f800000u;
+#pragma unroll
+  for (int i = 0; i < G::NVEC; ++i) {
+    const int v = threadIdx.x + i * NT;
+    if (G::TOTAL % NT != 0 && v >= G::TOTAL) break;
+    if (KC) {
+      if (r0 + v / (BK / VEC) == ones_r) regs[i] = make_uint4(one, one, one, one);
+    } else {
+      regs[i] = set_one<T>(regs[i], ones_r - (r0 + (v % (R / VEC)) * VEC));
+    }
+  }
+}
+
+template <typename T, int R, int BK, bool KC, int NT>
+DFM_INLINE void stage_store(const uint4* regs, T* lds) {
+  using G = TileGeom<T, R, BK, KC, NT>;
+  constexpr int VEC = G::VEC;
+#pragma unroll
+  for (int i = 0; i < G::NVEC; ++i) {
+    const int v = threadIdx.x + i * NT;
+    if (G::TOTAL % NT != 0 && v >= G::TOTAL) break;
     if (KC) {
       const int r = v / (BK / VEC), kc = (v % (BK / VEC)) * VEC;
       *reinterpret_cast<uint4*>(lds + r * G::LD + kc) = regs[i];
@@ -191,13 +264,27 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
   else stf((TO*)a.C + ci, v);
 }
 
+// Epilogue inputs of one 8-column vector, loaded ahead of use (bf16 path) so a thread's loads for
+// all of its vectors are in flight together.
 template <typename TO>
-DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
+struct EpiIn {
+  Raw8<TO> mul, res, c;
+};
+
+template <typename TO>
+DFM_INLINE void epi_load(const GemmArgs& a, int b, int m, int n, EpiIn<TO>& in) {
+  if (a.beta != 0.0f && !a.c_f32) in.c = ldraw8<TO>((const TO*)a.C + b * a.sc + (long)m * a.ldc + n);
+  if (a.mul) in.mul = ldraw8<TO>((const TO*)a.mul + (long)m * a.ldmul + n);
+  if (a.res) in.res = ldraw8<TO>((const TO*)a.res + (long)m * a.ldres + n);
+}
+
+template <typename TO>
+DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v, const EpiIn<TO>& in) {
   const long ci = b * a.sc + (long)m * a.ldc + n;
   float t[8];
   if (a.beta != 0.0f) {
     if (a.c_f32) ld8<float>((const float*)a.C + ci, t);
-    else ld8<TO>((const TO*)a.C + ci, t);
+    else unpack8(in.c, t);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += a.beta * t[e];
   }
@@ -216,7 +303,7 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
     }
   }
   if (a.mul) {
-    ld8<TO>((const TO*)a.mul + (long)m * a.ldmul + n, t);
+    unpack8(in.mul, t);
     if (a.mul_gelu_grad) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(t[e]);
@@ -226,7 +313,7 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
     }
   }
   if (a.res) {
-    ld8<TO>((const TO*)a.res + (long)m * a.ldres + n, t);
+    unpack8(in.res, t);
     const float rs = a.rowscale ? a.rowscale[m / a.rps] : 1.0f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = t[e] + (a.colscale ? a.colscale[n + e] : 1.0f) * rs * v[e];
@@ -235,14 +322,17 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v) {
   else st8<TO>((TO*)a.C + ci, v);
 }
 
-template <typename T, int BM, int BN, int WAVES_M, int BK, bool AK, bool BKC>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
-  constexpr int WAVES_N = 4 / WAVES_M;
+// DEPTH 1: one register set (tile t+1 is requested while tile t is multiplied); DEPTH 2: two
+// sets, for long k-loops where one tile of MFMA work cannot cover a global-load round trip.
+template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
+__global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int KSTEP = Mf<T>::KSTEP;
-  using GA = TileGeom<T, BM, BK, AK>;
-  using GB = TileGeom<T, BN, BK, BKC>;
+  using GA = TileGeom<T, BM, BK, AK, NT>;
+  using GB = TileGeom<T, BN, BK, BKC, NT>;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* const lds_base = reinterpret_cast<T*>(smem);
@@ -268,24 +358,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[GA::NVEC], rb[GB::NVEC];
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  if (nk > 0) {
-    stage_load<T, BM, BK, AK>(ra, A, a.lda, bm, kbeg, a.M, kend, a.ala);
-    stage_load<T, BN, BK, BKC>(rb, Bp, a.ldb, bn, kbeg, a.N, kend, a.alb, ones_r);
-    stage_store<T, BM, BK, AK>(ra, LDS_A(0));
-    stage_store<T, BN, BK, BKC>(rb, LDS_B(0));
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      stage_load<T, BM, BK, AK>(ra, A, a.lda, bm, kbeg + (kt + 1) * BK, a.M, kend, a.ala);
-      stage_load<T, BN, BK, BKC>(rb, Bp, a.ldb, bn, kbeg + (kt + 1) * BK, a.N, kend, a.alb, ones_r);
-    }
-    const T* la = LDS_A(cur);
-    const T* lb = LDS_B(cur);
+  // tiles [0, nfull) are whole BK slices of aligned operands: branch-free loads, two register
+  // sets in flight (tile t+1 lands while tile t is multiplied, tile t+2 is already requested)
+  const int nfull = (a.ala && a.alb) ? (kend - kbeg) / BK : 0;
+  const bool patch = ones_r >= bn && ones_r < bn + BN;  // block holds the virtual ones column
+
+  auto compute = [&](const T* la, const T* lb) {
 #pragma unroll
     for (int ks = 0; ks < BK; ks += KSTEP) {
       if constexpr (sizeof(T) == 2) {
@@ -312,104 +391,241 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (more) {
-      stage_store<T, BM, BK, AK>(ra, LDS_A(cur ^ 1));
-      stage_store<T, BN, BK, BKC>(rb, LDS_B(cur ^ 1));
-    }
-    __syncthreads();
-    cur ^= 1;
+  };
+  unsigned offa[GA::NVEC], offb[GB::NVEC];
+  if (nfull > 0) {
+    fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
+    fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
   }
+  // buffer descriptors over the operands: 32-bit per-lane offsets, the k-slice in soffset
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, 0, 0x7fffffff, 0x00020000);
+  auto load_fast = [&](uint4* xa, uint4* xb, int kt) {
+    const int k0 = kbeg + kt * BK;
+    stage_load_fast<T, BM, BK, AK, NT>(xa, rsa, (int)((AK ? k0 : (long)k0 * a.lda) * sizeof(T)), offa);
+    stage_load_fast<T, BN, BK, BKC, NT>(xb, rsb, (int)((BKC ? k0 : (long)k0 * a.ldb) * sizeof(T)), offb);
+  };
+  auto store_fast = [&](uint4* xa, uint4* xb, int buf) {
+    if (patch) patch_ones<T, BN, BK, BKC, NT>(xb, bn, ones_r);
+    stage_store<T, BM, BK, AK, NT>(xa, LDS_A(buf));
+    stage_store<T, BN, BK, BKC, NT>(xb, LDS_B(buf));
+  };
+
+  uint4 ra0[GA::NVEC], rb0[GB::NVEC];
+  uint4 ra1[DEPTH > 1 ? GA::NVEC : 1], rb1[DEPTH > 1 ? GB::NVEC : 1];
+  int done = 0;
+  if constexpr (DEPTH == 1) {
+    if (nfull >= 1) {
+      load_fast(ra0, rb0, 0);
+      store_fast(ra0, rb0, 0);
+      __syncthreads();
+      int cur = 0;
+      for (int kt = 0; kt + 1 < nfull; ++kt) {
+        load_fast(ra0, rb0, kt + 1);
+        compute(LDS_A(cur), LDS_B(cur));
+        store_fast(ra0, rb0, cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
+      }
+      compute(LDS_A(cur), LDS_B(cur));
+      done = nfull;
+    }
+  } else if (nfull == 1) {
+    load_fast(ra0, rb0, 0);
+    store_fast(ra0, rb0, 0);
+    __syncthreads();
+    compute(LDS_A(0), LDS_B(0));
+    done = 1;
+  } else if (nfull >= 2) {
+    load_fast(ra0, rb0, 0);
+    load_fast(ra1, rb1, 1);
+    store_fast(ra0, rb0, 0);
+    __syncthreads();
+    // invariant: LDS buffer 0 holds tile kt, set 1 holds tile kt+1 (in flight). Loads past the
+    // last whole tile re-read it (in-bounds, L2-hot) so every load is unconditional.
+    for (int kt = 0;; kt += 2) {
+      load_fast(ra0, rb0, min(kt + 2, nfull - 1));
+      compute(LDS_A(0), LDS_B(0));
+      store_fast(ra1, rb1, 1);
+      __syncthreads();
+      if (kt + 2 >= nfull) {
+        compute(LDS_A(1), LDS_B(1));
+        done = kt + 2;
+        break;
+      }
+      load_fast(ra1, rb1, min(kt + 3, nfull - 1));
+      compute(LDS_A(1), LDS_B(1));
+      store_fast(ra0, rb0, 0);
+      __syncthreads();
+      if (kt + 3 >= nfull) {
+        compute(LDS_A(0), LDS_B(0));
+        done = kt + 3;
+        break;
+      }
+    }
+  }
+  // guarded tail: the partial last slice, or every slice of unaligned operands
+  for (int kt = done; kt < nk; ++kt) {
+    uint4 rta[GA::NVEC], rtb[GB::NVEC];
+    __syncthreads();
+    const int k0 = kbeg + kt * BK;
+    stage_load<T, BM, BK, AK, NT>(rta, A, a.lda, bm, k0, a.M, kend, a.ala);
+    stage_load<T, BN, BK, BKC, NT>(rtb, Bp, a.ldb, bn, k0, a.N, kend, a.alb, ones_r);
+    stage_store<T, BM, BK, AK, NT>(rta, LDS_A(0));
+    stage_store<T, BN, BK, BKC, NT>(rtb, LDS_B(0));
+    __syncthreads();
+    compute(LDS_A(0), LDS_B(0));
+  }
+  __syncthreads();  // the epilogue reuses the operand LDS
 #undef LDS_A
 #undef LDS_B
 
-  // ---- epilogue: accumulator tile -> LDS (fp32, one row half at a time) -> 8-column vectors
-  constexpr int HALF = BM / 2;
+  // ---- epilogue: accumulator tile -> LDS (fp32, RP rows per pass: two 8-column vectors per
+  // thread per pass) -> 8-column vectors with all of a pass's global loads issued together
+  constexpr int TPR = BN / 8;  // threads per row
+  constexpr int RP = (2 * NT / TPR) < BM ? (2 * NT / TPR) : BM;
+  constexpr int HALF = RP;
   constexpr int CLD = BN + 4;
   float* cs = reinterpret_cast<float*>(smem);
-  constexpr int TPR = BN / 8;  // threads per row
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if ((wm * WM) / HALF == half) {
+  for (int half = 0; half < BM / RP; ++half) {
+    __builtin_amdgcn_sched_barrier(0);  // keep each pass's loads in their pass (register pressure)
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      if ((wm * WM + i * 16) / RP != half) continue;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = wn * WN + j * 16 + (lane & 15);
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + (lane & 15);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r - half * HALF;
-            cs[row * CLD + col] = acc[i][j][r] * a.alpha;
-          }
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r - half * RP;
+          cs[row * CLD + col] = acc[i][j][r] * a.alpha;
         }
+      }
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < HALF * TPR; idx += 256) {
-      const int row = idx / TPR, c8 = (idx % TPR) * 8;
-      const int m = bm + half * HALF + row, n = bn + c8;
-      if (m >= a.M || n >= a.Nw) continue;
-      float v[8];
+    constexpr int ITEMS = (HALF * TPR + NT - 1) / NT;
+    if (a.splits > 1) {  // fp32 partial tile -> workspace rows padded to ldw (16-byte stores)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = cs[row * CLD + c8 + e];
-      if (a.splits > 1) {
-        float* wp = a.ws + (((long)split * a.batch + b) * a.M + m) * a.Nw + n;
+      for (int it = 0; it < ITEMS; ++it) {
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
+        float4* wp = reinterpret_cast<float4*>(a.ws + (((long)split * a.batch + b) * a.M + m) * a.ldw + n);
+        const float* cv = cs + row * CLD + c8;
+        wp[0] = make_float4(cv[0], cv[1], cv[2], cv[3]);
+        wp[1] = make_float4(cv[4], cv[5], cv[6], cv[7]);
+      }
+    } else {
+      EpiIn<T> in[ITEMS];
+      bool vec[ITEMS];
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (n + e < a.Nw) wp[e] = v[e];
-      } else if (a.vec_ok && n + 8 <= a.N && (a.act_col0 <= n || a.act_col0 >= n + 8)) {
-        epilogue8<T>(a, b, m, n, v);
-      } else {
+      for (int it = 0; it < ITEMS; ++it) {  // issue every vector's loads first
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        vec[it] = idx < HALF * TPR && m < a.M && a.vec_ok && n + 8 <= a.N &&
+                  (a.act_col0 <= n || a.act_col0 >= n + 8);
+        if (vec[it]) epi_load<T>(a, b, m, n, in[it]);
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (n + e < a.Nw) epilogue_store<T>(a, b, m, n + e, v[e]);
+      for (int it = 0; it < ITEMS; ++it) {
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = cs[row * CLD + c8 + e];
+        if (vec[it]) {
+          epilogue8<T>(a, b, m, n, v, in[it]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.Nw) epilogue_store<T>(a, b, m, n + e, v[e]);
+        }
       }
     }
     __syncthreads();
   }
 }
 
-template <typename T>
-__global__ void splitk_reduce_kernel(GemmArgs a) {
-  const long total = (long)a.batch * a.M * a.Nw;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    float v = 0.f;
-    for (int s = 0; s < a.splits; ++s) v += a.ws[s * total + idx];
-    const int n = idx % a.Nw;
-    const long bm = idx / a.Nw;
-    const int m = bm % a.M, b = bm / a.M;
-    epilogue_store<T>(a, b, m, n, v);
+// Deterministic split-K combine: each block owns 256/G consecutive outputs and G lanes per output
+// walk the splits in a fixed order (G = 4 when there are many splits, so short outputs x long
+// split counts still fill the chip), then the G partial sums meet in LDS.
+template <typename T, int G>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a) {
+  constexpr int PER = 256 / G;
+  __shared__ float red[G][PER];
+  const long total = (long)a.batch * a.M * a.ldw;  // padded workspace elements per split
+  const int o = threadIdx.x % PER, g = threadIdx.x / PER;
+  const long idx = blockIdx.x * (long)PER + o;
+  float v = 0.f;
+  if (idx < total) {
+    const float* p = a.ws + idx;
+#pragma unroll 4
+    for (int s = g; s < a.splits; s += G) v += p[(long)s * total];
   }
+  if (G > 1) {
+    red[g][o] = v;
+    __syncthreads();
+    if (g != 0) return;
+#pragma unroll
+    for (int i = 1; i < G; ++i) v += red[i][o];
+  }
+  if (idx >= total) return;
+  const int n = idx % a.ldw;
+  if (n >= a.Nw) return;
+  const long bm = idx / a.ldw;
+  const int m = bm % a.M, b = bm / a.M;
+  epilogue_store<T>(a, b, m, n, v);
 }
 
-template <typename T, int BM, int BN, int WM_, int BK, bool AK, bool BKC>
+template <typename T, int BM, int BN, int NW, int WM_, int BK, bool AK, bool BKC, int DEPTH>
 int launch_cfg(GemmArgs& a, hipStream_t s) {
-  using GA = TileGeom<T, BM, BK, AK>;
-  using GB = TileGeom<T, BN, BK, BKC>;
+  using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
+  using GB = TileGeom<T, BN, BK, BKC, 64 * NW>;
   const size_t lds_op = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
-  const size_t lds_c = (size_t)(BM / 2) * (BN + 4) * sizeof(float);
+  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;  // epilogue rows per pass
+  const size_t lds_c = (size_t)RP * (BN + 4) * sizeof(float);
   const size_t lds = lds_op > lds_c ? lds_op : lds_c;
   dim3 grid(cdiv(a.M, BM), cdiv(a.Nw, BN), a.batch * a.splits);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, WM_, BK, AK, BKC>,
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WM_, BK, AK, BKC>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>), grid, dim3(64 * NW), lds, s, a);
   DFM_LAUNCH_CHECK();
   if (a.splits > 1) {
-    const long total = (long)a.batch * a.M * a.Nw;
-    hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3(min(cdiv(total, 256), 4096u)), dim3(256), 0, s, a);
+    const long total = (long)a.batch * a.M * a.ldw;
+    if (a.splits >= 8)
+      hipLaunchKernelGGL((splitk_reduce_kernel<T, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((splitk_reduce_kernel<T, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
     DFM_LAUNCH_CHECK();
   }
   return DFM_OK;
 }
 
-template <typename T, int BM, int BN, int WM_, int BK>
+template <typename T, int BM, int BN, int NW, int WM_, int BK, int DEPTH>
 int launch_layout(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
-  if (ak && bk) return launch_cfg<T, BM, BN, WM_, BK, true, true>(a, s);
-  if (ak && !bk) return launch_cfg<T, BM, BN, WM_, BK, true, false>(a, s);
-  if (!ak && bk) return launch_cfg<T, BM, BN, WM_, BK, false, true>(a, s);
-  return launch_cfg<T, BM, BN, WM_, BK, false, false>(a, s);
+  if (ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, true, DEPTH>(a, s);
+  if (ak && !bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, false, DEPTH>(a, s);
+  if (!ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, false, true, DEPTH>(a, s);
+  return launch_cfg<T, BM, BN, NW, WM_, BK, false, false, DEPTH>(a, s);
+}
+
+template <typename T, int BM, int BN, int NW, int WM_, int BK>
+int launch_depth(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
+  const int kper = (a.K + a.splits - 1) / a.splits;
+  const long blocks = (long)cdiv(a.M, BM) * cdiv(a.Nw, BN) * a.batch * a.splits;
+  // two register sets cost occupancy: only worth it for long k-loops on a grid that leaves CUs
+  // with a single block anyway
+  if (kper >= 8 * BK && blocks <= 512) return launch_layout<T, BM, BN, NW, WM_, BK, 2>(a, ak, bk, s);
+  return launch_layout<T, BM, BN, NW, WM_, BK, 1>(a, ak, bk, s);
 }
 
 void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
@@ -418,21 +634,21 @@ void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
   BN = Nw <= 32 ? 32 : (Nw <= 64 ? 64 : 128);
 }
 
+// Split-K: enough blocks to put one long-K block on every CU (~256), but at least 512 reduction
+// elements per split, rounded down to a power of two (fitted on the DFormer-B step's GEMM census,
+// tools/gemm_sweep.py).
 int choose_splits(const DfmGemmDesc* d, int elem_bytes) {
+  (void)elem_bytes;
   if (d->split_k >= 1) return d->split_k;
   int BM, BN;
   pick_tile(d, BM, BN);
   const int Nw = d->N + (d->colsum ? 1 : 0);
   const long tiles = (long)cdiv(d->M, BM) * cdiv(Nw, BN) * (d->batch > 0 ? d->batch : 1);
-  if (tiles >= 512 || d->K < 2048) return 1;
-  // ~512 blocks, >= 1024 reduction elements per split, and fp32 partial traffic (write + read)
-  // at most ~1/4 of the operand bytes the GEMM streams
-  long s = (512 + tiles - 1) / tiles;
-  s = std::min(s, (long)d->K / 1024);
-  const double operand = (double)d->K * (d->M + d->N) * elem_bytes;
-  const double per_split = 2.0 * d->M * Nw * 4.0;
-  s = std::min(s, (long)(0.25 * operand / per_split));
-  return (int)std::max(1L, std::min(s, 1024L));
+  if (d->K < 1024 || tiles >= 256) return 1;
+  long s = std::min((256 + tiles - 1) / tiles, (long)d->K / 512);
+  int p = 1;
+  while (2L * p <= s && p < 1024) p *= 2;
+  return p;
 }
 
 template <typename T>
@@ -447,6 +663,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.A = A; a.B = B; a.C = C; a.ws = (float*)ws;
   a.M = d->M; a.N = d->N; a.K = d->K; a.batch = d->batch > 0 ? d->batch : 1;
   a.Nw = d->N + (d->colsum ? 1 : 0);
+  a.ldw = (a.Nw + 7) & ~7;
   a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
   a.sa = d->stride_a; a.sb = d->stride_b; a.sc = d->stride_c;
   a.alpha = d->alpha; a.beta = d->beta; a.c_f32 = d->c_f32;
@@ -467,14 +684,14 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
   if (small_k) {
     constexpr int BKs = sizeof(T) == 2 ? 32 : 16;
-    if (BN == 32) return launch_layout<T, 128, 32, 4, BKs>(a, ak, bk, s);
-    if (BN == 64) return launch_layout<T, 128, 64, 2, BKs>(a, ak, bk, s);
-    return launch_layout<T, 128, 128, 2, BKs>(a, ak, bk, s);
+    if (BN == 32) return launch_layout<T, 128, 32, 4, 4, BKs, 1>(a, ak, bk, s);
+    if (BN == 64) return launch_layout<T, 128, 64, 4, 2, BKs, 1>(a, ak, bk, s);
+    return launch_layout<T, 128, 128, 8, 2, BKs, 1>(a, ak, bk, s);
   }
   constexpr int BKl = sizeof(T) == 2 ? 64 : 32;
-  if (BN == 32) return launch_layout<T, 128, 32, 4, BKl>(a, ak, bk, s);
-  if (BN == 64) return launch_layout<T, 128, 64, 2, BKl>(a, ak, bk, s);
-  return launch_layout<T, 128, 128, 2, BKl>(a, ak, bk, s);
+  if (BN == 32) return launch_depth<T, 128, 32, 4, 4, BKl>(a, ak, bk, s);
+  if (BN == 64) return launch_depth<T, 128, 64, 4, 2, BKl>(a, ak, bk, s);
+  return launch_depth<T, 128, 128, 8, 2, BKl>(a, ak, bk, s);
 }
 
 }  // namespace
@@ -482,7 +699,8 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 extern "C" size_t dfm_gemm_workspace_size(const DfmGemmDesc* d) {
   const int s = std::max(choose_splits(d, 2), choose_splits(d, 4));
   if (s <= 1) return 0;
-  return (size_t)s * (d->batch > 0 ? d->batch : 1) * d->M * (d->N + (d->colsum ? 1 : 0)) * sizeof(float);
+  const long ldw = (d->N + (d->colsum ? 1 : 0) + 7) & ~7L;
+  return (size_t)s * (d->batch > 0 ? d->batch : 1) * d->M * ldw * sizeof(float);
 }
 
 extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const void* B, void* C, void* ws,

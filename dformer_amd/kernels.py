@@ -11,6 +11,9 @@ from ._lib import check, dtype_code, lib, ptr, stream
 
 _ws_cache = {}
 
+# When set to a list, every GEMM launch appends its descriptor fields (tools/gemm_sweep.py)
+GEMM_TRACE = None
+
 
 def _ws(nbytes, dev):
     """Per-device scratch buffer that only grows (the library never allocates)."""
@@ -46,6 +49,9 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
                       alpha, beta, c_f32, ptr(bias), act, ptr(preact), ldpre, ptr(mul), ldmul, ptr(res), ldres,
                       ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0, ptr(colsum),
                       int(colsum_accumulate), int(mul_gelu_grad))
+    if GEMM_TRACE is not None:
+        GEMM_TRACE.append({f: getattr(d, f) for f, _ in d._fields_ if not f in ("alpha", "beta")} |
+                          {"dtype": dt, "beta": d.beta, "out_f32": out.dtype == torch.float32})
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
