@@ -47,37 +47,41 @@ def synthetic_batch(B, H, W, ncls, device, seed):
     return rgb, dep, lab
 
 
-def measure_dominant_kernel(device, iters=50):
-    """Roofline of the dominant kernel family (MFMA GEMM): the ConvFFN fc2 GEMM of stage 0
-    (M = 16*120*160 pixels, K = 512 hidden, N = 64) as launched in the step, bf16, timed with HIP
-    events on the launching stream. Algorithmic bytes = read A (M*K) + B (N*K) + residual (M*N)
-    + write C and preact (2*M*N), 2 B each."""
+def dominant_probe(model, batch, height, width):
+    """The dominant kernel whose roofline is reported: the ConvFFN fc2 GEMM of stage 0
+    (DFormer.py:55; M = batch*(H/4)*(W/4) pixels, K = 8*C hidden, N = C = 64 for Base), fused
+    bias + layer-scale residual epilogue that also writes the pre-residual branch output. Its
+    launches inside the timed steps are bracketed by HIP events on their own stream."""
     from dformer_amd import kernels as K
-    M, Kd, N = 16 * 120 * 160, 512, 64
-    a = torch.randn(M, Kd, device=device).to(torch.bfloat16)
-    w = torch.randn(N, Kd, device=device).to(torch.bfloat16)
-    b = torch.randn(N, device=device)
-    res = torch.randn(M, N, device=device).to(torch.bfloat16)
-    pre = torch.empty(M, N, device=device, dtype=torch.bfloat16)
-    ls = torch.rand(N, device=device)
-    out = torch.empty(M, N, device=device, dtype=torch.bfloat16)
-    for _ in range(5):
-        K.linear(a, w, b, preact=pre, res=res, colscale=ls, out=out)
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(iters):
-        K.linear(a, w, b, preact=pre, res=res, colscale=ls, out=out)
-    e1.record(s)
-    e1.synchronize()
-    sec = e0.elapsed_time(e1) / 1e3 / iters
+    enc = model.encoder_backbone
+    C = enc.dims[0]
+    M = batch * (height // 4) * (width // 4)
+    return K.LaunchProbe(M, C, C * enc.mlp_ratios[0], True, True)
+
+
+def roofline_of(probe):
+    """Algorithmic bytes per launch: read hidden A (M*K) + W (N*K) + residual (M*N), write the
+    output and the saved branch output (2*M*N); bf16 = 2 B. HBM traffic per launch comes from
+    the rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE x2 on gfx950 + WRITE_SIZE)."""
+    M, N, Kd = probe.key[:3]
+    us = probe.mean_us()
+    if us is None:
+        return None
     nbytes = 2 * (M * Kd + N * Kd + 3 * M * N)
     flops = 2 * M * N * Kd
-    ach = nbytes / sec / 1e9
+    ach = nbytes / (us * 1e-6) / 1e9
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "r01_dominant_pmc.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            rec = json.load(f)
+        if tuple(rec.get("key", ())) == probe.key:
+            traffic = rec.get("traffic_bytes_per_launch")
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "gemm_kernel<bf16,128x64> ConvFFN fc2 stage0 (M=307200,K=512,N=64)",
-            "avg_us": round(sec * 1e6, 2), "bytes_per_launch": nbytes, "tflops": round(flops / sec / 1e12, 1)}
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "kernel": f"gemm_kernel bf16 ConvFFN fc2 stage0 (M={M},K={Kd},N={N}), fused bias+residual epilogue",
+            "launches": len(probe.events), "avg_us": round(us, 2), "bytes_per_launch": nbytes,
+            "tflops": round(flops / (us * 1e-6) / 1e12, 1)}
 
 
 def cpu_baseline(model_sd, seconds=20.0):
@@ -156,6 +160,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    from dformer_amd import kernels as K
+    probe = dominant_probe(model, args.batch, args.height, args.width) if rank == 0 else None
+    K.GEMM_PROBE = probe
     t0 = time.perf_counter()
     loss = None
     for _ in range(args.steps):
@@ -165,6 +172,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    K.GEMM_PROBE = None
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = elapsed.item()
@@ -180,7 +188,7 @@ def main():
         "loss": round(float(loss.item()), 4) if loss is not None else None,
     }
     if rank == 0:
-        result["roofline"] = measure_dominant_kernel(dev)
+        result["roofline"] = roofline_of(probe)
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(sd_cpu, args.cpu_seconds)
         print(json.dumps(result), flush=True)

@@ -166,6 +166,7 @@ class DFormer(nn.Module):
             and torch.distributed.get_world_size() > 1
         self.depths = depths
         self.dims = dims
+        self.mlp_ratios = mlp_ratios
         self.out_indices = out_indices
         self.compute_dtype = torch.float32
         self.downsample_layers = nn.ModuleList()
