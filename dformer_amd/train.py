@@ -102,6 +102,7 @@ class GradBuckets:
             if members:
                 self._add(g, members, start)
         self.pending = [len(b[1]) for b in self.buckets]
+        self.copies = [[] for _ in self.buckets]
         for p in self.owner:
             p.register_post_accumulate_grad_hook(self._hook)
 
@@ -116,13 +117,29 @@ class GradBuckets:
         bi, g = self.owner[p]
         off, k = g.slots[p]
         if p.grad.data_ptr() != g.grad.data_ptr() + 4 * off:  # kernels usually wrote the slot directly
-            g.grad[off:off + k].copy_(p.grad.reshape(-1))
+            self.copies[bi].append((g.grad[off:off + k], p.grad.reshape(-1)))
         p.grad = None
         self.pending[bi] -= 1
-        if self.pending[bi] == 0 and self.world > 1:
-            self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
+        if self.pending[bi] == 0:
+            self._flush(bi)
+            if self.world > 1:
+                self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
+
+    def _flush(self, bi):
+        """Gradients autograd produced outside the slots (torch-managed stems, decoder BN affine
+        params): one multi-tensor copy launch per bucket instead of one copy per parameter."""
+        pairs = self.copies[bi]
+        if pairs:
+            torch._foreach_copy_([d for d, _ in pairs], [s for _, s in pairs])
+            self.copies[bi] = []
 
     def finish(self):
+        # buckets with a parameter that got no gradient this step (unused branch): reduce them now
+        for bi, b in enumerate(self.buckets):
+            if 0 < self.pending[bi] < len(b[1]) or (self.pending[bi] == len(b[1]) and self.copies[bi]):
+                self._flush(bi)
+                if self.world > 1:
+                    self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
             h.wait()
         self.handles = []
@@ -135,6 +152,7 @@ class FusedAdamW:
     def __init__(self, model, lr=6e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, world=1,
                  compute_dtype=torch.float32, bucket_bytes=25 << 20):
         decay, no_decay = group_weight(model)
+        self.full_groups = (decay, no_decay)  # reference group lists, incl. frozen params (state_dict indices)
         dev = next(model.parameters()).device
         self.groups = [_FlatGroup(decay, weight_decay, dev, compute_dtype),
                        _FlatGroup(no_decay, 0.0, dev, torch.float32)]
@@ -161,6 +179,61 @@ class FusedAdamW:
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
+
+
+    def refresh_shadows(self):
+        """After parameters were overwritten in place (load_state_dict): refresh the bf16 copies."""
+        for g in self.groups:
+            if g.shadow is not None:
+                g.shadow.copy_(g.flat)
+        invalidate_weights()
+        for g in self.groups:
+            g.register_shadows()
+
+    # ---- torch.optim.AdamW-compatible state (utils/engine/engine.py:101-186 save/restore)
+    def state_dict(self):
+        """The state_dict torch.optim.AdamW over group_weight's two groups would have: parameters
+        indexed in group order (frozen ones included, without state), exp_avg / exp_avg_sq / step."""
+        defaults = {k: v for k, v in torch.optim.AdamW([torch.zeros(1, requires_grad=True)]).param_groups[0].items()
+                    if k != "params"}
+        state, groups, idx = {}, [], 0
+        for plist, g in zip(self.full_groups, self.groups):
+            ids = []
+            for p in plist:
+                if p in g.slots and self.step_count > 0:
+                    off, k = g.slots[p]
+                    state[idx] = {"step": torch.tensor(float(self.step_count)),
+                                  "exp_avg": g.m[off:off + k].view_as(p).detach().clone(),
+                                  "exp_avg_sq": g.v[off:off + k].view_as(p).detach().clone()}
+                ids.append(idx)
+                idx += 1
+            grp = dict(defaults)
+            grp.update(lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=g.wd, params=ids)
+            groups.append(grp)
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        groups = sd["param_groups"]
+        if len(groups) != 2:
+            raise ValueError(f"expected the two group_weight groups, got {len(groups)}")
+        steps = set()
+        for plist, g, grp in zip(self.full_groups, self.groups, groups):
+            if len(grp["params"]) != len(plist):
+                raise ValueError(f"param group size mismatch: {len(grp['params'])} vs {len(plist)}")
+            for p, idx in zip(plist, grp["params"]):
+                st = sd["state"].get(idx, sd["state"].get(str(idx)))
+                if st is None or p not in g.slots:
+                    continue
+                off, k = g.slots[p]
+                g.m[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                g.v[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        self.lr = groups[0].get("lr", self.lr)
+        self.betas = tuple(groups[0].get("betas", self.betas))
+        self.eps = groups[0].get("eps", self.eps)
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter step counts differ: {sorted(steps)[:4]}")
+        self.step_count = steps.pop() if steps else 0
 
 
 def all_reduce_mean(t, world):
