@@ -1,19 +1,17 @@
 // Depthwise k x k convolution over NHWC (DFormer.py:80-81 7x7 conv/e_conv, DFormer.py:54,62 3x3
-// pos + identity), forward / input-gradient / weight-gradient.
+// pos + identity): forward (+ fused identity / GELU second output), input gradient (the forward
+// with flipped taps) and weight + bias gradient.
 //
-// HBM-bound. Every thread owns CPT consecutive channels (one 16-byte vector: 8 bf16 or 4 fp32)
-// of a TW-pixel strip of one output row; input rows are streamed as 16-byte vectors through a
-// register sliding window (neighbouring strips share their halo through L1/L2, so HBM sees each
-// byte about once). A block covers GPB channel groups x SPB strips; the block's k*k weights live
-// in LDS transposed to [k*k][channels] so each tap is one vector LDS read.
-// The weight gradient accumulates per thread over many strips, reduces across the block's strip
-// lanes in LDS, writes per-block partials [block][C][k*k+1] (last column: bias grad) and sums
-// them in a fixed order (deterministic, no float atomics).
+// HBM-bound. Both kernels stage an output tile's input window (tile + k-1 halo, zero-padded) in
+// LDS once with coalesced 16-byte channel vectors (8 bf16 / 4 fp32 per lane), then every thread
+// slides a register window along one LDS row for TWS consecutive outputs of one channel group.
+// The weight gradient keeps per-thread tap accumulators across all tiles a block visits and writes
+// one partial per block; a fixed-order second pass sums them (deterministic, no float atomics).
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
-constexpr int TW = 4;
-
 template <typename T> struct DwCfg { static constexpr int CPT = 16 / sizeof(T); };
 
 template <typename T>
@@ -34,129 +32,173 @@ DFM_INLINE void stv(T* p, const float* v) {
   }
 }
 
-struct DwGeom {
-  int G;       // channel groups (C / CPT)
-  int GPB;     // groups per block
-  int SPB;     // strip lanes per block
-  int nstrip;  // strips per row
-  long strips; // B * H * nstrip
-};
+// ---------------------------------------------------------------- LDS-tiled forward (v3)
+// A block owns an output tile of TH rows x TWT columns of one image and NG channel groups
+// (NG * CPT channels). The (TH+K-1) x (TWT+K-1) input tile (zero-padded at the image border) is
+// staged once into LDS as 16-byte vectors [row][col][group]; the block's K*K weights as fp32
+// [tap][channel]. Each thread then produces TWS consecutive outputs of one row for one channel
+// group, sliding a (TWS+K-1)-vector window along the LDS row for each of the K kernel rows.
+// Global traffic is the tile plus its halo (read once, coalesced along channels); the identity
+// term comes from the staged tile centre for free.
+template <typename T, int K>
+struct DwTile;
+template <typename T> struct DwTile<T, 3> { static constexpr int TWS = 4, STRIPS = 8; };
+template <typename T> struct DwTile<T, 7> { static constexpr int TWS = 4, STRIPS = 4; };
 
-template <typename T>
-DwGeom dw_geom(int B, int H, int W, int C) {
-  constexpr int CPT = DwCfg<T>::CPT;
-  DwGeom g;
-  g.G = C / CPT;
-  g.GPB = g.G < 32 ? g.G : 32;
-  g.SPB = 256 / g.GPB;
-  g.nstrip = (W + TW - 1) / TW;
-  g.strips = (long)B * H * g.nstrip;
-  return g;
-}
+template <typename T, int K, bool FLIP, int NG>
+__global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
+                                                          const T* __restrict__ x, long ldx,
+                                                          const float* __restrict__ w, const float* __restrict__ bias,
+                                                          int add_identity, T* __restrict__ y, long ldy,
+                                                          int accumulate, T* __restrict__ gout, long ldg) {
+  constexpr int CPT = DwCfg<T>::CPT, R = K / 2;
+  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
+  constexpr int IH = TH + K - 1, IW = TWT + K - 1, CW = NG * CPT;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  uint4* xs = reinterpret_cast<uint4*>(dsm);                    // [IH][IW][NG]
+  float* wl = reinterpret_cast<float*>(dsm + IH * IW * NG * 16);  // [K*K][CW]
 
-template <typename T, int K, bool FLIP>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(int B, int H, int W, int C, DwGeom gm, const T* __restrict__ x,
-                                                     long ldx, const float* __restrict__ w,
-                                                     const float* __restrict__ bias, int add_identity,
-                                                     T* __restrict__ y, long ldy, int accumulate, T* __restrict__ gout,
-                                                     long ldg) {
-  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, WIN = TW + K - 1;
-  extern __shared__ __attribute__((aligned(16))) float wl[];  // [K*K][GPB*CPT]
-  const int CW = gm.GPB * CPT;
+  const int tile = blockIdx.x;
+  const int tw = tile % tiles_w, th = (tile / tiles_w) % tiles_h, b = tile / (tiles_w * tiles_h);
+  const int h0 = th * TH, w0 = tw * TWT;
   const int cbase = blockIdx.y * CW;
+  const long img = (long)b * H * W;
+
   for (int e = threadIdx.x; e < K * K * CW; e += 256) {
-    const int tap = e / CW, cl = e % CW, c = cbase + cl;
+    const int tap = e / CW, c = cbase + e % CW;
     wl[e] = c < C ? w[(long)c * K * K + (FLIP ? K * K - 1 - tap : tap)] : 0.f;
   }
+  {  // all of a thread's tile loads in flight together, then one LDS write pass
+    constexpr int NV = IH * IW * NG, NL = (NV + 255) / 256;
+    uint4 buf[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int v = threadIdx.x + l * 256;
+      const int g = v % NG, col = (v / NG) % IW, row = v / (NG * IW);
+      const int hh = h0 + row - R, ww = w0 + col - R, c = cbase + g * CPT;
+      buf[l] = make_uint4(0, 0, 0, 0);
+      if (v < NV && hh >= 0 && hh < H && ww >= 0 && ww < W && c < C)
+        buf[l] = *reinterpret_cast<const uint4*>(x + (img + (long)hh * W + ww) * ldx + c);
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+      if (threadIdx.x + l * 256 < NV) xs[threadIdx.x + l * 256] = buf[l];
+  }
   __syncthreads();
-  const int cg = threadIdx.x % gm.GPB, lane = threadIdx.x / gm.GPB;
-  if (lane >= gm.SPB) return;
-  const int c0 = cbase + cg * CPT;
-  if (c0 >= C) return;
-  float bv[CPT];
+
+  const int g = threadIdx.x % NG, strip = (threadIdx.x / NG) % STRIPS, row = threadIdx.x / (NG * STRIPS);
+  const int c0 = cbase + g * CPT;
+  const int oh = h0 + row, ow0 = w0 + strip * TWS;
+  if (c0 >= C || oh >= H || ow0 >= W) return;
+  float acc[TWS][CPT];
 #pragma unroll
-  for (int e = 0; e < CPT; ++e) bv[e] = bias ? bias[c0 + e] : 0.f;
-  for (long s = (long)blockIdx.x * gm.SPB + lane; s < gm.strips; s += (long)gridDim.x * gm.SPB) {
-    const int ws = s % gm.nstrip;
-    const long bh = s / gm.nstrip;
-    const int h = bh % H;
-    const long img_row0 = (bh - h) * W;  // b * H * W
-    const int w0 = ws * TW;
-    float acc[TW][CPT];
+  for (int e = 0; e < CPT; ++e) {
+    const float bv = bias ? bias[c0 + e] : 0.f;
 #pragma unroll
-    for (int t = 0; t < TW; ++t)
+    for (int t = 0; t < TWS; ++t) acc[t][e] = bv;
+  }
+#pragma unroll 1
+  for (int i = 0; i < K; ++i) {
+    float win[TWS + K - 1][CPT];
+    const uint4* xr = xs + ((row + i) * IW + strip * TWS) * NG + g;
 #pragma unroll
-      for (int e = 0; e < CPT; ++e) acc[t][e] = bv[e];
-    constexpr int UI = K == 7 ? 1 : K;  // keep the 7x7 window's live range to one input row
-#pragma unroll UI
-    for (int i = 0; i < K; ++i) {
-      const int hh = h + i - R;
-      if (hh < 0 || hh >= H) continue;
-      const T* row = x + (img_row0 + (long)hh * W) * ldx + c0;
-      float win[WIN][CPT];
-#pragma unroll
-      for (int u = 0; u < WIN; ++u) {
-        const int ww = w0 + u - R;
-        if (ww >= 0 && ww < W) ldv<T>(row + (long)ww * ldx, win[u]);
-        else {
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) win[u][e] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        float wv[CPT];
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) wv[e] = wl[(i * K + j) * CW + cg * CPT + e];
-#pragma unroll
-        for (int t = 0; t < TW; ++t)
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) acc[t][e] += wv[e] * win[t + j][e];
+    for (int u = 0; u < TWS + K - 1; ++u) {
+      const uint4 q = xr[u * NG];
+      if constexpr (sizeof(T) == 2) {
+        Raw8<bf16_t> r8;
+        r8.w[0] = q;
+        unpack8(r8, win[u]);
+      } else {
+        win[u][0] = __uint_as_float(q.x); win[u][1] = __uint_as_float(q.y);
+        win[u][2] = __uint_as_float(q.z); win[u][3] = __uint_as_float(q.w);
       }
     }
-    const long orow = img_row0 + (long)h * W;
 #pragma unroll
-    for (int t = 0; t < TW; ++t) {
-      const int ww = w0 + t;
-      if (ww >= W) break;
-      if (add_identity) {
-        float xi[CPT];
-        ldv<T>(x + (orow + ww) * ldx + c0, xi);
+    for (int j = 0; j < K; ++j) {
+      float wv[CPT];
+      const float4* wp = reinterpret_cast<const float4*>(wl + (i * K + j) * CW + g * CPT);
 #pragma unroll
-        for (int e = 0; e < CPT; ++e) acc[t][e] += xi[e];
+      for (int q4 = 0; q4 < CPT / 4; ++q4) {
+        const float4 f = wp[q4];
+        wv[4 * q4] = f.x; wv[4 * q4 + 1] = f.y; wv[4 * q4 + 2] = f.z; wv[4 * q4 + 3] = f.w;
       }
-      T* yp = y + (orow + ww) * ldy + c0;
-      if (accumulate) {
-        float o[CPT];
-        ldv<T>(yp, o);
 #pragma unroll
-        for (int e = 0; e < CPT; ++e) acc[t][e] += o[e];
-      }
-      stv<T>(yp, acc[t]);
-      if (gout) {
-        float gv[CPT];
+      for (int t = 0; t < TWS; ++t)
 #pragma unroll
-        for (int e = 0; e < CPT; ++e) gv[e] = gelu_f(acc[t][e]);
-        stv<T>(gout + (orow + ww) * ldg + c0, gv);
+        for (int e = 0; e < CPT; ++e) acc[t][e] = fmaf(wv[e], win[t + j][e], acc[t][e]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TWS; ++t) {
+    const int ow = ow0 + t;
+    if (ow >= W) break;
+    const long p = img + (long)oh * W + ow;
+    if (add_identity) {
+      const uint4 q = xs[((row + R) * IW + strip * TWS + t + R) * NG + g];
+      float xi[CPT];
+      if constexpr (sizeof(T) == 2) {
+        Raw8<bf16_t> r8;
+        r8.w[0] = q;
+        unpack8(r8, xi);
+      } else {
+        xi[0] = __uint_as_float(q.x); xi[1] = __uint_as_float(q.y);
+        xi[2] = __uint_as_float(q.z); xi[3] = __uint_as_float(q.w);
       }
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) acc[t][e] += xi[e];
+    }
+    T* yp = y + p * ldy + c0;
+    if (accumulate) {
+      float o[CPT];
+      ldv<T>(yp, o);
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) acc[t][e] += o[e];
+    }
+    stv<T>(yp, acc[t]);
+    if (gout) {
+      float gv[CPT];
+#pragma unroll
+      for (int e = 0; e < CPT; ++e) gv[e] = gelu_f(acc[t][e]);
+      stv<T>(gout + p * ldg + c0, gv);
     }
   }
 }
 
-// dW partials: block (strip block bx, channel chunk by, kernel-row group bz); each thread accumulates
-// KI kernel rows x K columns x CPT channels over its strips.
-template <typename T, int K, int KI>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(int B, int H, int W, int C, DwGeom gm, const T* __restrict__ x,
-                                                       long ldx, const T* __restrict__ dy, long lddy,
-                                                       float* __restrict__ part) {
-  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, WIN = TW + K - 1, KK1 = K * K + 1;
-  __shared__ float red[256][CPT + 1];
-  const int CW = gm.GPB * CPT;
+// ---------------------------------------------------------------- LDS-tiled weight gradient (v3)
+// Block (spatial lane bx, channel block by, kernel-row group bz) walks tiles bx, bx+gridDim.x, ...
+// For each tile the dy tile [TH][TWT][NG] and the TH+KI-1 input rows its KI kernel rows touch
+// ([TH+KI-1][TWT+K-1][NG], zero-padded) are staged in LDS; every thread accumulates KI x K taps
+// x CPT channels over its TWS pixels with a sliding window. At the end the taps are reduced over
+// the threads of one channel group (wave shuffles, then LDS across waves) and written as the
+// block's partial [bx][C][K*K+1] (last column: bias gradient, from bz == 0); a fixed-order
+// second pass sums the partials (deterministic).
+template <typename T, int K>
+struct DwWTile;
+template <typename T> struct DwWTile<T, 3> { static constexpr int KI = 3; };
+template <typename T> struct DwWTile<T, 7> { static constexpr int KI = 1; };
+
+template <typename T, int K, int NG>
+__global__ __launch_bounds__(256) void dw_tile_wgrad_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
+                                                            const T* __restrict__ x, long ldx,
+                                                            const T* __restrict__ dy, long lddy,
+                                                            float* __restrict__ part) {
+  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, KI = DwWTile<T, K>::KI, KK1 = K * K + 1;
+  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
+  constexpr int IH = TH + KI - 1, IW = TWT + K - 1, CW = NG * CPT;
+  constexpr int NTAP = KI * K;
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  uint4* xs = reinterpret_cast<uint4*>(dsm);  // [IH][IW][NG]
+  uint4* ds = xs + IH * IW * NG;              // [TH][TWT][NG]
+  float* red = reinterpret_cast<float*>(dsm);  // reused after the tile loop: [4 waves][NTAP+1][CW]
+
   const int cbase = blockIdx.y * CW;
-  const int cg = threadIdx.x % gm.GPB, lane = threadIdx.x / gm.GPB;
-  const int c0 = cbase + cg * CPT;
-  const bool active = lane < gm.SPB && c0 < C;
   const int i0 = blockIdx.z * KI;
+  const int g = threadIdx.x % NG, strip = (threadIdx.x / NG) % STRIPS, row = threadIdx.x / (NG * STRIPS);
+  const int c0 = cbase + g * CPT;
+  const long ntiles = (long)B * tiles_h * tiles_w;
+
   float acc[KI][K][CPT];
   float dbs[CPT];
 #pragma unroll
@@ -167,76 +209,105 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(int B, int H, int W, int 
     for (int j = 0; j < K; ++j)
 #pragma unroll
       for (int e = 0; e < CPT; ++e) acc[a][j][e] = 0.f;
-  if (active) {
-    for (long s = (long)blockIdx.x * gm.SPB + lane; s < gm.strips; s += (long)gridDim.x * gm.SPB) {
-      const int ws = s % gm.nstrip;
-      const long bh = s / gm.nstrip;
-      const int h = bh % H;
-      const long img_row0 = (bh - h) * W;
-      const int w0 = ws * TW;
-      float g[TW][CPT];
-      const long orow = img_row0 + (long)h * W;
+
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tw = tile % tiles_w, th = (tile / tiles_w) % tiles_h;
+    const long b = tile / ((long)tiles_w * tiles_h);
+    const int h0 = th * TH, w0 = tw * TWT;
+    const long img = b * H * W;
+    {
+      constexpr int NX = IH * IW * NG, NDY = TH * TWT * NG, NL = (NX + NDY + 255) / 256;
+      uint4 buf[NL];
 #pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        if (w0 + t < W) ldv<T>(dy + (orow + w0 + t) * lddy + c0, g[t]);
-        else {
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) g[t][e] = 0.f;
+      for (int l = 0; l < NL; ++l) {
+        const int v = threadIdx.x + l * 256;
+        buf[l] = make_uint4(0, 0, 0, 0);
+        if (v < NX) {
+          const int gg = v % NG, col = (v / NG) % IW, r = v / (NG * IW);
+          const int hh = h0 + r + i0 - R, ww = w0 + col - R, c = cbase + gg * CPT;
+          if (hh >= 0 && hh < H && ww >= 0 && ww < W && c < C)
+            buf[l] = *reinterpret_cast<const uint4*>(x + (img + (long)hh * W + ww) * ldx + c);
+        } else if (v < NX + NDY) {
+          const int u = v - NX;
+          const int gg = u % NG, col = (u / NG) % TWT, r = u / (NG * TWT);
+          const int hh = h0 + r, ww = w0 + col, c = cbase + gg * CPT;
+          if (hh < H && ww < W && c < C)
+            buf[l] = *reinterpret_cast<const uint4*>(dy + (img + (long)hh * W + ww) * lddy + c);
         }
       }
-      if (i0 == 0) {
+      __syncthreads();  // the previous tile's LDS reads are done
 #pragma unroll
-        for (int t = 0; t < TW; ++t)
+      for (int l = 0; l < NL; ++l)
+        if (threadIdx.x + l * 256 < NX + NDY) xs[threadIdx.x + l * 256] = buf[l];
+    }
+    __syncthreads();
+    float gv[TWS][CPT];
 #pragma unroll
-          for (int e = 0; e < CPT; ++e) dbs[e] += g[t][e];
+    for (int t = 0; t < TWS; ++t) {
+      const uint4 q = ds[(row * TWT + strip * TWS + t) * NG + g];
+      if constexpr (sizeof(T) == 2) {
+        Raw8<bf16_t> r8;
+        r8.w[0] = q;
+        unpack8(r8, gv[t]);
+      } else {
+        gv[t][0] = __uint_as_float(q.x); gv[t][1] = __uint_as_float(q.y);
+        gv[t][2] = __uint_as_float(q.z); gv[t][3] = __uint_as_float(q.w);
       }
+    }
+    if (i0 == 0) {
 #pragma unroll
-      for (int a = 0; a < KI; ++a) {
-        const int hh = h + i0 + a - R;
-        if (hh < 0 || hh >= H) continue;
-        const T* row = x + (img_row0 + (long)hh * W) * ldx + c0;
-        float win[WIN][CPT];
+      for (int t = 0; t < TWS; ++t)
 #pragma unroll
-        for (int u = 0; u < WIN; ++u) {
-          const int ww = w0 + u - R;
-          if (ww >= 0 && ww < W) ldv<T>(row + (long)ww * ldx, win[u]);
-          else {
+        for (int e = 0; e < CPT; ++e) dbs[e] += gv[t][e];
+    }
 #pragma unroll
-            for (int e = 0; e < CPT; ++e) win[u][e] = 0.f;
-          }
+    for (int a = 0; a < KI; ++a) {
+      const uint4* xr = xs + ((row + a) * IW + strip * TWS) * NG + g;
+#pragma unroll
+      for (int u = 0; u < TWS + K - 1; ++u) {
+        const uint4 q = xr[u * NG];
+        float xv[CPT];
+        if constexpr (sizeof(T) == 2) {
+          Raw8<bf16_t> r8;
+          r8.w[0] = q;
+          unpack8(r8, xv);
+        } else {
+          xv[0] = __uint_as_float(q.x); xv[1] = __uint_as_float(q.y);
+          xv[2] = __uint_as_float(q.z); xv[3] = __uint_as_float(q.w);
         }
+        // input column u feeds output t with tap j = u - t
 #pragma unroll
-        for (int j = 0; j < K; ++j)
+        for (int t = 0; t < TWS; ++t) {
+          const int j = u - t;
+          if (j < 0 || j >= K) continue;
 #pragma unroll
-          for (int t = 0; t < TW; ++t)
-#pragma unroll
-            for (int e = 0; e < CPT; ++e) acc[a][j][e] += g[t][e] * win[t + j][e];
+          for (int e = 0; e < CPT; ++e) acc[a][j][e] = fmaf(gv[t][e], xv[e], acc[a][j][e]);
+        }
       }
     }
   }
-  // reduce across the strip lanes of each channel group, one (a, j) tap at a time
-  const long pbase = (long)blockIdx.x * C * KK1;
+  __syncthreads();  // LDS is reused for the reduction
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int tap = 0; tap <= KI * K; ++tap) {
-    if (tap == KI * K && i0 != 0) break;
+  for (int tap = 0; tap <= NTAP; ++tap) {
+    if (tap == NTAP && i0 != 0) break;
 #pragma unroll
     for (int e = 0; e < CPT; ++e) {
-      float v = 0.f;
-      if (active) v = tap < KI * K ? acc[tap / K][tap % K][e] : dbs[e];
-      red[threadIdx.x][e] = v;
+      float v = tap < NTAP ? acc[tap / K][tap % K][e] : dbs[e];
+#pragma unroll
+      for (int o = NG; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      if (lane < NG) red[(wave * (NTAP + 1) + tap) * CW + lane * CPT + e] = v;
     }
-    __syncthreads();
-    if (threadIdx.x < gm.GPB * CPT) {
-      const int g2 = threadIdx.x / CPT, e = threadIdx.x % CPT;
-      const int c = cbase + g2 * CPT + e;
-      if (c < C) {
-        float s = 0.f;
-        for (int l = 0; l < gm.SPB; ++l) s += red[l * gm.GPB + g2][e];
-        const int col = tap < KI * K ? (i0 + tap / K) * K + tap % K : K * K;
-        part[pbase + (long)c * KK1 + col] = s;
-      }
-    }
-    __syncthreads();
+  }
+  __syncthreads();
+  const long pbase = (long)blockIdx.x * C * KK1;
+  for (int idx = threadIdx.x; idx < (NTAP + 1) * CW; idx += 256) {
+    const int tap = idx / CW, cl = idx % CW, c = cbase + cl;
+    if (c >= C || (tap == NTAP && i0 != 0)) continue;
+    const float v = red[(0 * (NTAP + 1) + tap) * CW + cl] + red[(1 * (NTAP + 1) + tap) * CW + cl] +
+                    red[(2 * (NTAP + 1) + tap) * CW + cl] + red[(3 * (NTAP + 1) + tap) * CW + cl];
+    const int col = tap < NTAP ? (i0 + tap / K) * K + tap % K : K * K;
+    part[pbase + (long)c * KK1 + col] = v;
   }
 }
 
@@ -246,40 +317,106 @@ bool dw_aligned(int C, const void* p, long ld) {
   return C % CPT == 0 && ld % CPT == 0 && ((uintptr_t)p % 16) == 0;
 }
 
+template <typename T, int K, bool FLIP, int NG>
+int dw_tile_launch(int B, int H, int W, int C, const void* x, long ldx, const float* w, const float* bias, int id,
+                   void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
+  constexpr int CPT = DwCfg<T>::CPT, TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
+  const int tiles_h = (H + TH - 1) / TH, tiles_w = (W + TWT - 1) / TWT;
+  const int G = C / CPT;
+  dim3 grid((unsigned)((long)B * tiles_h * tiles_w), cdiv(G, NG));
+  const size_t lds = (size_t)(TH + K - 1) * (TWT + K - 1) * NG * 16 + (size_t)K * K * NG * CPT * sizeof(float);
+  hipLaunchKernelGGL((dw_tile_fwd_kernel<T, K, FLIP, NG>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
+                     (const T*)x, ldx, w, bias, id, (T*)y, ldy, acc, (T*)gout, ldg);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
 template <typename T, bool FLIP>
 int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const float* w, const float* bias, int id,
            void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
   DFM_CHECK_ARG(dw_aligned<T>(C, x, ldx) && dw_aligned<T>(C, y, ldy) && (!gout || dw_aligned<T>(C, gout, ldg)),
                 "dwconv: C, row strides and pointers must be 16-byte vector aligned");
-  const DwGeom gm = dw_geom<T>(B, H, W, C);
-  const unsigned chunks = cdiv(gm.G, gm.GPB);
-  const long want = (long)min(cdiv(gm.strips, gm.SPB), 8192u);
-  dim3 grid((unsigned)want, chunks);
-  const size_t lds = (size_t)k * k * gm.GPB * DwCfg<T>::CPT * sizeof(float);
-#define GO(KK)                                                                                                   \
-  hipLaunchKernelGGL((dw_fwd_kernel<T, KK, FLIP>), grid, dim3(256), lds, s, B, H, W, C, gm, (const T*)x, ldx, w, \
-                     bias, id, (T*)y, ldy, acc, (T*)gout, ldg)
-  if (k == 7) GO(7);
-  else if (k == 3) GO(3);
-  else {
-    dfm_set_error("dwconv: k=%d unsupported", k);
-    return DFM_ERR_ARG;
+  DFM_CHECK_ARG(k == 3 || k == 7, "dwconv: k=%d unsupported", k);
+  const int G = C / DwCfg<T>::CPT;
+  // channel groups per block: as many as the tile geometry allows without idling lanes
+#define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)
+  if (k == 3) {
+    if (G >= 4) GO(3, 4);
+    if (G >= 2) GO(3, 2);
+    GO(3, 1);
   }
+  if (G >= 8) GO(7, 8);
+  if (G >= 4) GO(7, 4);
+  if (G >= 2) GO(7, 2);
+  GO(7, 1);
 #undef GO
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
 }
 
-template <typename T>
-int wgrad_grid(int B, int H, int W, int C, int k, DwGeom& gm, dim3& grid) {
-  gm = dw_geom<T>(B, H, W, C);
-  const int KI = k == 3 ? 3 : 1;
-  const unsigned chunks = cdiv(gm.G, gm.GPB);
-  const unsigned zdim = k / KI;
-  long nsb = (1024 + (long)chunks * zdim - 1) / ((long)chunks * zdim);
-  nsb = max(1L, min(nsb, (long)cdiv(gm.strips, gm.SPB)));
+// Weight-gradient launch geometry: ~2048 blocks (spatial lanes x channel blocks x kernel-row
+// groups), each spatial lane walking its share of the tiles.
+template <typename T, int K, int NG>
+void wgrad_geom(int B, int H, int W, int C, int& tiles_h, int& tiles_w, dim3& grid) {
+  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS, KI = DwWTile<T, K>::KI;
+  tiles_h = (H + TH - 1) / TH;
+  tiles_w = (W + TWT - 1) / TWT;
+  const long ntiles = (long)B * tiles_h * tiles_w;
+  const unsigned chunks = cdiv(C / DwCfg<T>::CPT, NG), zdim = K / KI;
+  long nsb = (2048 + (long)chunks * zdim - 1) / ((long)chunks * zdim);
+  nsb = std::max(1L, std::min(nsb, ntiles));
   grid = dim3((unsigned)nsb, chunks, zdim);
-  return (int)nsb;
+}
+
+template <typename T, int K>
+int wgrad_ng(int C) {
+  const int G = C / DwCfg<T>::CPT;
+  if (K == 3) return G >= 4 ? 4 : (G >= 2 ? 2 : 1);
+  return G >= 8 ? 8 : (G >= 4 ? 4 : (G >= 2 ? 2 : 1));
+}
+
+template <typename T, int K, int NG>
+long wgrad_nsb(int B, int H, int W, int C) {
+  int th, tw;
+  dim3 grid;
+  wgrad_geom<T, K, NG>(B, H, W, C, th, tw, grid);
+  return grid.x;
+}
+
+template <typename T, int K>
+long wgrad_nsb_any(int B, int H, int W, int C) {
+  switch (wgrad_ng<T, K>(C)) {
+    case 8: return wgrad_nsb<T, K, 8>(B, H, W, C);
+    case 4: return wgrad_nsb<T, K, 4>(B, H, W, C);
+    case 2: return wgrad_nsb<T, K, 2>(B, H, W, C);
+    default: return wgrad_nsb<T, K, 1>(B, H, W, C);
+  }
+}
+
+template <typename T, int K, int NG>
+long wgrad_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
+                  hipStream_t s) {
+  constexpr int CPT = DwCfg<T>::CPT, TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS, KI = DwWTile<T, K>::KI;
+  int tiles_h, tiles_w;
+  dim3 grid;
+  wgrad_geom<T, K, NG>(B, H, W, C, tiles_h, tiles_w, grid);
+  const size_t lds_tile = ((size_t)(TH + KI - 1) * (TWT + K - 1) * NG + (size_t)TH * TWT * NG) * 16;
+  const size_t lds_red = (size_t)4 * (KI * K + 1) * NG * CPT * sizeof(float);
+  hipLaunchKernelGGL((dw_tile_wgrad_kernel<T, K, NG>), grid, dim3(256), std::max(lds_tile, lds_red), s, B, H, W, C,
+                     tiles_h, tiles_w, (const T*)x, ldx, (const T*)dy, lddy, part);
+  return grid.x;
+}
+
+template <typename T, int K>
+long wgrad_dispatch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
+                    hipStream_t s) {
+  switch (wgrad_ng<T, K>(C)) {
+    case 8: return wgrad_launch<T, K, 8>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    case 4: return wgrad_launch<T, K, 4>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    case 2: return wgrad_launch<T, K, 2>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    default: return wgrad_launch<T, K, 1>(B, H, W, C, x, ldx, dy, lddy, part, s);
+  }
 }
 }  // namespace
 
@@ -308,13 +445,10 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
 }
 
 extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k) {
-  DwGeom gm;
-  dim3 grid;
-  const int nsb = wgrad_grid<float>(B, H, W, C, k, gm, grid);  // fp32 geometry has the most strip blocks
-  DwGeom gm2;
-  dim3 grid2;
-  const int nsb2 = wgrad_grid<bf16_t>(B, H, W, C, k, gm2, grid2);
-  return (size_t)max(nsb, nsb2) * C * (k * k + 1) * sizeof(float);
+  long nsb = 1;
+  if (k == 3) nsb = std::max(wgrad_nsb_any<float, 3>(B, H, W, C), wgrad_nsb_any<bf16_t, 3>(B, H, W, C));
+  else if (k == 7) nsb = std::max(wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C));
+  return (size_t)nsb * C * (k * k + 1) * sizeof(float);
 }
 
 extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
@@ -322,27 +456,24 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
                                      dfm_stream_t stream) {
   DFM_CHECK_ARG(x && dy && dw && workspace, "dfm_dwconv_bwd_weight: null argument");
   DFM_CHECK_ARG(k == 3 || k == 7, "dfm_dwconv_bwd_weight: k=%d unsupported", k);
+  DFM_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd_weight: bad shape");
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
-  DwGeom gm;
-  dim3 grid;
-  int nsb;
+  long nsb;
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = wgrad_grid<bf16_t>(B, H, W, C, k, gm, grid);
-    if (k == 7) hipLaunchKernelGGL((dw_wgrad_kernel<bf16_t, 7, 1>), grid, dim3(256), 0, s, B, H, W, C, gm, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, part);
-    else hipLaunchKernelGGL((dw_wgrad_kernel<bf16_t, 3, 3>), grid, dim3(256), 0, s, B, H, W, C, gm, (const bf16_t*)x, ldx, (const bf16_t*)dy, lddy, part);
+    nsb = k == 7 ? wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                 : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = wgrad_grid<float>(B, H, W, C, k, gm, grid);
-    if (k == 7) hipLaunchKernelGGL((dw_wgrad_kernel<float, 7, 1>), grid, dim3(256), 0, s, B, H, W, C, gm, (const float*)x, ldx, (const float*)dy, lddy, part);
-    else hipLaunchKernelGGL((dw_wgrad_kernel<float, 3, 3>), grid, dim3(256), 0, s, B, H, W, C, gm, (const float*)x, ldx, (const float*)dy, lddy, part);
+    nsb = k == 7 ? wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                 : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else {
     dfm_set_error("dfm_dwconv_bwd_weight: bad dtype");
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, nsb,
+  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, (int)nsb,
                      (long)C * (k * k + 1), (const float*)part, dw, db, (long)(k * k + 1), 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

@@ -13,6 +13,7 @@
 // activation / multiplier / residual on 8-column vectors, so every global read and write of the
 // output side is a coalesced 16-byte access (these GEMMs are mostly HBM-bound: K <= 2048).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -44,6 +45,7 @@ struct GemmArgs {
   int ala, alb;    // operand rows 16-byte aligned (vector loads)
   int vec_ok;      // output-side rows 16-byte aligned (vector epilogue)
   int mul_gelu_grad;
+  int stream;      // host: take the M-streaming persistent kernel
 };
 
 template <typename T> struct Mf;
@@ -322,6 +324,87 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v, cons
   else st8<TO>((TO*)a.C + ci, v);
 }
 
+// Epilogue of one BM x BN accumulator tile: -> LDS (fp32, RP rows per pass: two 8-column vectors
+// per thread per pass) -> 8-column vectors with all of a pass's global loads issued together; or
+// the fp32 split-K partial tile into the workspace. Ends with the LDS free (trailing barrier).
+template <typename T, int BM, int BN, int NW, int WAVES_M>
+DFM_INLINE void gemm_epilogue(const GemmArgs& a, float4_t (&acc)[BM / WAVES_M / 16][BN / (NW / WAVES_M) / 16],
+                              char* smem, int bm, int bn, int b, int split) {
+  constexpr int NT = 64 * NW;
+  constexpr int WAVES_N = NW / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+  constexpr int TPR = BN / 8;  // threads per row
+  constexpr int RP = (2 * NT / TPR) < BM ? (2 * NT / TPR) : BM;
+  constexpr int HALF = RP;
+  constexpr int CLD = BN + 4;
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int half = 0; half < BM / RP; ++half) {
+    __builtin_amdgcn_sched_barrier(0);  // keep each pass's loads in their pass (register pressure)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if ((wm * WM + i * 16) / RP != half) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r - half * RP;
+          cs[row * CLD + col] = acc[i][j][r] * a.alpha;
+        }
+      }
+    }
+    __syncthreads();
+    constexpr int ITEMS = (HALF * TPR + NT - 1) / NT;
+    if (a.splits > 1) {  // fp32 partial tile -> workspace rows padded to ldw (16-byte stores)
+#pragma unroll
+      for (int it = 0; it < ITEMS; ++it) {
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
+        float4* wp = reinterpret_cast<float4*>(a.ws + (((long)split * a.batch + b) * a.M + m) * a.ldw + n);
+        const float* cv = cs + row * CLD + c8;
+        wp[0] = make_float4(cv[0], cv[1], cv[2], cv[3]);
+        wp[1] = make_float4(cv[4], cv[5], cv[6], cv[7]);
+      }
+    } else {
+      EpiIn<T> in[ITEMS];
+      bool vec[ITEMS];
+#pragma unroll
+      for (int it = 0; it < ITEMS; ++it) {  // issue every vector's loads first
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        vec[it] = idx < HALF * TPR && m < a.M && a.vec_ok && n + 8 <= a.N &&
+                  (a.act_col0 <= n || a.act_col0 >= n + 8);
+        if (vec[it]) epi_load<T>(a, b, m, n, in[it]);
+      }
+#pragma unroll
+      for (int it = 0; it < ITEMS; ++it) {
+        const int idx = threadIdx.x + it * NT;
+        const int row = idx / TPR, c8 = (idx % TPR) * 8;
+        const int m = bm + half * HALF + row, n = bn + c8;
+        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = cs[row * CLD + c8 + e];
+        if (vec[it]) {
+          epilogue8<T>(a, b, m, n, v, in[it]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (n + e < a.Nw) epilogue_store<T>(a, b, m, n + e, v[e]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // DEPTH 1: one register set (tile t+1 is requested while tile t is multiplied); DEPTH 2: two
 // sets, for long k-loops where one tile of MFMA work cannot cover a global-load round trip.
 template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
@@ -480,75 +563,116 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
 #undef LDS_A
 #undef LDS_B
 
-  // ---- epilogue: accumulator tile -> LDS (fp32, RP rows per pass: two 8-column vectors per
-  // thread per pass) -> 8-column vectors with all of a pass's global loads issued together
-  constexpr int TPR = BN / 8;  // threads per row
-  constexpr int RP = (2 * NT / TPR) < BM ? (2 * NT / TPR) : BM;
-  constexpr int HALF = RP;
-  constexpr int CLD = BN + 4;
-  float* cs = reinterpret_cast<float*>(smem);
+  gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
+}
+
+// M-streaming GEMM for large M x short K (K a multiple of BK, 16-byte aligned operands, no
+// split-K, batch 1, no bias-gradient column): a persistent grid walks the tiles (M fastest, so
+// consecutive blocks share the B tile through L2) and requests the next tile's first k-slice
+// before the current tile's epilogue, so operand loads stream underneath the output writes.
+template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC>
+__global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int tiles_m, long ntiles) {
+  constexpr int NT = 64 * NW;
+  constexpr int WAVES_N = NW / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int KSTEP = Mf<T>::KSTEP;
+  using GA = TileGeom<T, BM, BK, AK, NT>;
+  using GB = TileGeom<T, BN, BK, BKC, NT>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* const lds_base = reinterpret_cast<T*>(smem);
+#define LDS_A(i) (lds_base + (i) * GA::ELEMS)
+#define LDS_B(i) (lds_base + 2 * GA::ELEMS + (i) * GB::ELEMS)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+  const int nk = a.K / BK;
+  const T* A = (const T*)a.A;
+  const T* Bp = (const T*)a.B;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0xffffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, 0, 0xffffffff, 0x00020000);
+
+  long t = blockIdx.x;
+  if (t >= ntiles) return;
+  int bm = (int)(t % tiles_m) * BM, bn = (int)(t / tiles_m) * BN;
+  unsigned offa[GA::NVEC], offb[GB::NVEC];
+  fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
+  fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
+  uint4 ra[GA::NVEC], rb[GB::NVEC];
+  auto load = [&](int kt) {
+    const int k0 = kt * BK;
+    stage_load_fast<T, BM, BK, AK, NT>(ra, rsa, (int)((AK ? k0 : (long)k0 * a.lda) * sizeof(T)), offa);
+    stage_load_fast<T, BN, BK, BKC, NT>(rb, rsb, (int)((BKC ? k0 : (long)k0 * a.ldb) * sizeof(T)), offb);
+  };
+  auto store = [&](int buf) {
+    stage_store<T, BM, BK, AK, NT>(ra, LDS_A(buf));
+    stage_store<T, BN, BK, BKC, NT>(rb, LDS_B(buf));
+  };
+  float4_t acc[TM][TN];
+  auto compute = [&](const T* la, const T* lb) {
 #pragma unroll
-  for (int half = 0; half < BM / RP; ++half) {
-    __builtin_amdgcn_sched_barrier(0);  // keep each pass's loads in their pass (register pressure)
+    for (int ks = 0; ks < BK; ks += KSTEP) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t fa[TM], fb[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if ((wm * WM + i * 16) / RP != half) continue;
+        for (int i = 0; i < TM; ++i) fa[i] = frag_bf16<AK, GA::LD>((const bf16_t*)la, wm * WM + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = wn * WN + j * 16 + (lane & 15);
+        for (int j = 0; j < TN; ++j) fb[j] = frag_bf16<BKC, GB::LD>((const bf16_t*)lb, wn * WN + j * 16, ks, lane);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r - half * RP;
-          cs[row * CLD + col] = acc[i][j][r] * a.alpha;
-        }
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      } else {
+        float fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag_f32<AK, GA::LD>((const float*)la, wm * WM + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag_f32<BKC, GB::LD>((const float*)lb, wn * WN + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
     }
+  };
+
+  load(0);
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    store(0);
     __syncthreads();
-    constexpr int ITEMS = (HALF * TPR + NT - 1) / NT;
-    if (a.splits > 1) {  // fp32 partial tile -> workspace rows padded to ldw (16-byte stores)
-#pragma unroll
-      for (int it = 0; it < ITEMS; ++it) {
-        const int idx = threadIdx.x + it * NT;
-        const int row = idx / TPR, c8 = (idx % TPR) * 8;
-        const int m = bm + half * HALF + row, n = bn + c8;
-        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
-        float4* wp = reinterpret_cast<float4*>(a.ws + (((long)split * a.batch + b) * a.M + m) * a.ldw + n);
-        const float* cv = cs + row * CLD + c8;
-        wp[0] = make_float4(cv[0], cv[1], cv[2], cv[3]);
-        wp[1] = make_float4(cv[4], cv[5], cv[6], cv[7]);
-      }
-    } else {
-      EpiIn<T> in[ITEMS];
-      bool vec[ITEMS];
-#pragma unroll
-      for (int it = 0; it < ITEMS; ++it) {  // issue every vector's loads first
-        const int idx = threadIdx.x + it * NT;
-        const int row = idx / TPR, c8 = (idx % TPR) * 8;
-        const int m = bm + half * HALF + row, n = bn + c8;
-        vec[it] = idx < HALF * TPR && m < a.M && a.vec_ok && n + 8 <= a.N &&
-                  (a.act_col0 <= n || a.act_col0 >= n + 8);
-        if (vec[it]) epi_load<T>(a, b, m, n, in[it]);
-      }
-#pragma unroll
-      for (int it = 0; it < ITEMS; ++it) {
-        const int idx = threadIdx.x + it * NT;
-        const int row = idx / TPR, c8 = (idx % TPR) * 8;
-        const int m = bm + half * HALF + row, n = bn + c8;
-        if (idx >= HALF * TPR || m >= a.M || n >= a.Nw) continue;
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = cs[row * CLD + c8 + e];
-        if (vec[it]) {
-          epilogue8<T>(a, b, m, n, v, in[it]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (n + e < a.Nw) epilogue_store<T>(a, b, m, n + e, v[e]);
-        }
-      }
+    int cur = 0;
+    for (int kt = 0; kt + 1 < nk; ++kt) {
+      load(kt + 1);
+      compute(LDS_A(cur), LDS_B(cur));
+      store(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
     }
-    __syncthreads();
+    compute(LDS_A(cur), LDS_B(cur));
+    // next tile's first slice in flight during this tile's epilogue (a re-read of this tile's
+    // slice, L2-hot, when there is none: every load stays unconditional)
+    const long tn = t + gridDim.x;
+    const bool more = tn < ntiles;
+    const int bm_c = bm, bn_c = bn;
+    if (more) {
+      bm = (int)(tn % tiles_m) * BM;
+      bn = (int)(tn / tiles_m) * BN;
+    }
+    fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
+    fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
+    load(0);
+    __syncthreads();  // operand LDS reads done: the epilogue reuses it
+    gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm_c, bn_c, 0, 0);
+    if (!more) break;
+    t = tn;
   }
+#undef LDS_A
+#undef LDS_B
 }
 
 // Deterministic split-K combine: each block owns 256/G consecutive outputs and G lanes per output
@@ -610,8 +734,36 @@ int launch_cfg(GemmArgs& a, hipStream_t s) {
   return DFM_OK;
 }
 
+template <typename T, int BM, int BN, int NW, int WM_, int BK, bool AK, bool BKC>
+int launch_stream(GemmArgs& a, hipStream_t s) {
+  using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
+  using GB = TileGeom<T, BN, BK, BKC, 64 * NW>;
+  const size_t lds_op = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
+  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
+  const size_t lds_c = (size_t)RP * (BN + 4) * sizeof(float);
+  const size_t lds = lds_op > lds_c ? lds_op : lds_c;
+  auto kern = gemm_stream_kernel<T, BM, BN, NW, WM_, BK, AK, BKC>;
+  static int per_cu = -1;
+  if (per_cu < 0) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 64 * NW, lds) != hipSuccess || n < 1) n = 1;
+    per_cu = n;
+  }
+  const int tiles_m = cdiv(a.M, BM);
+  const long ntiles = (long)tiles_m * cdiv(a.Nw, BN);
+  const long grid = std::min(ntiles, (long)256 * per_cu);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, a, tiles_m, ntiles);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
 template <typename T, int BM, int BN, int NW, int WM_, int BK, int DEPTH>
 int launch_layout(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
+  if constexpr (DEPTH == 1 && BN <= 64 && sizeof(T) == 2) {
+    if (a.stream && ak && bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, true>(a, s);
+    if (a.stream && ak && !bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, false>(a, s);
+  }
   if (ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, true, DEPTH>(a, s);
   if (ak && !bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, false, DEPTH>(a, s);
   if (!ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, false, true, DEPTH>(a, s);
@@ -661,6 +813,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   constexpr int VEC = Mf<T>::VEC;
   GemmArgs a;
   a.A = A; a.B = B; a.C = C; a.ws = (float*)ws;
+  a.stream = 0;
   a.M = d->M; a.N = d->N; a.K = d->K; a.batch = d->batch > 0 ? d->batch : 1;
   a.Nw = d->N + (d->colsum ? 1 : 0);
   a.ldw = (a.Nw + 7) & ~7;
@@ -676,12 +829,27 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   pick_tile(d, BM, BN);
   a.splits = choose_splits(d, sizeof(T));
   if (a.splits > 1) DFM_CHECK_ARG(ws != nullptr, "dfm_gemm: split-K needs a workspace");
-  a.ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0);
-  a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0);
+  // fast (buffer-load) tiles need 16-byte aligned rows and one matrix within a 2 GiB descriptor
+  const double ext_a = ((double)(d->a_kcontig ? d->M : d->K) * d->lda) * sizeof(T);
+  const double ext_b = ((double)(d->b_kcontig ? d->N : d->K) * d->ldb) * sizeof(T);
+  a.ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0) &&
+          ext_a < 2147483647.0;
+  a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0) &&
+          ext_b < 2147483647.0;
   a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
              al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
   const bool ak = d->a_kcontig, bk = d->b_kcontig;
   const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
+  static const int stream_env = [] {  // DFM_GEMM_STREAM=0 disables the streaming kernel (A/B timing)
+    const char* e = getenv("DFM_GEMM_STREAM");
+    return e ? atoi(e) : 1;
+  }();
+  {  // large M x short K: persistent M-streaming kernel
+    const int BKsel = small_k ? (sizeof(T) == 2 ? 32 : 16) : (sizeof(T) == 2 ? 64 : 32);
+    const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
+    a.stream = stream_env != 0 && sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb && d->K % BKsel == 0 &&
+               d->K / BKsel <= 8 && tiles >= 1024;
+  }
   if (small_k) {
     constexpr int BKs = sizeof(T) == 2 ? 32 : 16;
     if (BN == 32) return launch_layout<T, 128, 32, 4, 4, BKs, 1>(a, ak, bk, s);

@@ -54,6 +54,31 @@ def test_gemm_layouts(dt, M, N, Kd):
     assert rel(db, dy.float().sum(0)) < TOL[dt]
 
 
+@pytest.mark.parametrize("M,N,Kd", [(140000, 64, 64), (131072 + 77, 256, 128), (140001, 160, 64),
+                                    (135000, 64, 512)])
+def test_gemm_stream_large_m(M, N, Kd):
+    """Large-M x short-K shapes take the persistent M-streaming kernel (bf16): forward with the
+    full fused epilogue and dgrad with the GELU-derivative multiplier, incl. ragged M / N tails."""
+    k = K()
+    dt = torch.bfloat16
+    x = torch.randn(M, Kd, device=DEV).to(dt)
+    w = (torch.randn(N, Kd, device=DEV) / Kd ** 0.5).to(dt)
+    b = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(dt)
+    ls = torch.rand(N, device=DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=dt)
+    y = k.linear(x, w, b, preact=pre, res=res, colscale=ls)
+    f = x.float() @ w.float().t() + b
+    assert rel(pre.float(), f) < TOL[dt]
+    assert rel(y.float(), res.float() + ls * f) < TOL[dt]
+    dy = torch.randn(M, N, device=DEV).to(dt)
+    h = torch.randn(M, Kd, device=DEV).to(dt)
+    dx = k.linear_dgrad(dy, w, gelu_grad_of=h)
+    hf = h.float()
+    gg = 0.5 * (1 + torch.erf(hf / math.sqrt(2))) + hf * torch.exp(-0.5 * hf * hf) / math.sqrt(2 * math.pi)
+    assert rel(dx.float(), (dy.float() @ w.float()) * gg) < TOL[dt]
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_splitk_and_strided(dt):
     k = K()
@@ -148,6 +173,34 @@ def test_dwconv(dt, ks, ident, B, H, W, C):
     dw, db = k.dwconv_bwd_weight(x.view(-1, C), dy.view(-1, C), (B, H, W), ks)
     assert rel(dw, wr.grad) < TOL[dt] * 2
     assert rel(db, br.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("ks", [3, 7])
+@pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 80), (1, 9, 70, 32), (3, 33, 5, 24)])
+def test_dwconv_strided_gelu_accumulate(dt, ks, B, H, W, C):
+    """Column-slice views (row stride > C), the fused GELU second output and accumulate=True."""
+    k = K()
+    xb = torch.randn(B * H * W, C + 16, device=DEV).to(dt)
+    x = xb[:, 8:8 + C]
+    w = torch.randn(C, 1, ks, ks, device=DEV) / ks
+    bias = torch.randn(C, device=DEV)
+    xr = x.float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    ref = F.conv2d(xr, w, bias, padding=ks // 2, groups=C) + xr
+    yb = torch.zeros(B * H * W, C + 8, device=DEV).to(dt)
+    gb = torch.zeros(B * H * W, C + 24, device=DEV).to(dt)
+    k.dwconv(x, (B, H, W), w, bias, ks, True, out=yb[:, :C], gelu_out=gb[:, 16:16 + C])
+    y = yb[:, :C].float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    assert rel(y, ref) < TOL[dt]
+    g = gb[:, 16:16 + C].float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    assert rel(g, F.gelu(y)) < TOL[dt]
+    dy = torch.randn(B * H * W, C, device=DEV).to(dt)
+    base = torch.randn(B * H * W, C, device=DEV).to(dt)
+    dx = base.clone()
+    k.dwconv_bwd_data(dy, (B, H, W), w, ks, False, dx=dx, accumulate=True)
+    dyr = dy.float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    refdx = F.conv_transpose2d(dyr, w, padding=ks // 2, groups=C) + base.float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    assert rel(dx.float().reshape(B, H, W, C).permute(0, 3, 1, 2), refdx) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)
