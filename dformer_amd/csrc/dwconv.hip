@@ -8,6 +8,7 @@
 // The weight gradient keeps per-thread tap accumulators across all tiles a block visits and writes
 // one partial per block; a fixed-order second pass sums them (deterministic, no float atomics).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -40,6 +41,16 @@ DFM_INLINE void stv(T* p, const float* v) {
 // group, sliding a (TWS+K-1)-vector window along the LDS row for each of the K kernel rows.
 // Global traffic is the tile plus its halo (read once, coalesced along channels); the identity
 // term comes from the staged tile centre for free.
+// XCD-aware block order. Blocks are dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+// one L2), so block b is given logical index remap(b): XCD k owns one contiguous run of the
+// logical order. Logical indices run channel-group fastest, then tile in raster order, so the
+// blocks that read the two halves of one 128-byte line, and the vertically adjacent tiles that
+// share K-1 halo rows, run on the same XCD close together in time (their re-reads hit its L2).
+DFM_INLINE long xcd_remap(long b, long n) {
+  const long per = n / 8, rem = n % 8, k = b % 8, i = b / 8;
+  return k * per + (k < rem ? k : rem) + i;
+}
+
 template <typename T, int K>
 struct DwTile;
 template <typename T> struct DwTile<T, 3> { static constexpr int TWS = 4, STRIPS = 8; };
@@ -59,10 +70,12 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
   uint4* xs = reinterpret_cast<uint4*>(dsm);                    // [IH][IW][NG]
   float* wl = reinterpret_cast<float*>(dsm + IH * IW * NG * 16);  // [K*K][CW]
 
-  const int tile = blockIdx.x;
+  const int ncg = (C / CPT + NG - 1) / NG;
+  const long l = xcd_remap(blockIdx.x, (long)gridDim.x);
+  const int tile = (int)(l / ncg);
   const int tw = tile % tiles_w, th = (tile / tiles_w) % tiles_h, b = tile / (tiles_w * tiles_h);
   const int h0 = th * TH, w0 = tw * TWT;
-  const int cbase = blockIdx.y * CW;
+  const int cbase = (int)(l % ncg) * CW;
   const long img = (long)b * H * W;
 
   for (int e = threadIdx.x; e < K * K * CW; e += 256) {
@@ -324,7 +337,7 @@ int dw_tile_launch(int B, int H, int W, int C, const void* x, long ldx, const fl
   constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
   const int tiles_h = (H + TH - 1) / TH, tiles_w = (W + TWT - 1) / TWT;
   const int G = C / CPT;
-  dim3 grid((unsigned)((long)B * tiles_h * tiles_w), cdiv(G, NG));
+  dim3 grid((unsigned)((long)B * tiles_h * tiles_w * cdiv(G, NG)));
   const size_t lds = (size_t)(TH + K - 1) * (TWT + K - 1) * NG * 16 + (size_t)K * K * NG * CPT * sizeof(float);
   hipLaunchKernelGGL((dw_tile_fwd_kernel<T, K, FLIP, NG>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
                      (const T*)x, ldx, w, bias, id, (T*)y, ldy, acc, (T*)gout, ldg);
@@ -341,7 +354,12 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
   const int G = C / DwCfg<T>::CPT;
   // channel groups per block: as many as the tile geometry allows without idling lanes
 #define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)
+  static const int ng3 = [] {  // DFM_DW_NG3=8: 64-channel (one 128-byte line) blocks for 3x3
+    const char* e = getenv("DFM_DW_NG3");
+    return e ? atoi(e) : 4;
+  }();
   if (k == 3) {
+    if (ng3 == 8 && G >= 8) GO(3, 8);
     if (G >= 4) GO(3, 4);
     if (G >= 2) GO(3, 2);
     GO(3, 1);

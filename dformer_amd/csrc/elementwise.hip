@@ -104,12 +104,65 @@ __global__ void ew2d_kernel(long rows, int C, const T* __restrict__ a, long lda,
   }
 }
 
+
+// 8-column vector form of ew2d_kernel (rows 16-byte aligned, C % 8 == 0)
+template <typename T, int OP>
+__global__ void ew2d_vec_kernel(long rows, int C, const T* __restrict__ a, long lda, const T* __restrict__ b, long ldb,
+                                const float* __restrict__ colscale, const float* __restrict__ rowscale, long rps,
+                                float alpha, T* __restrict__ d, long ldd, int accumulate) {
+  const int cv = C / 8;
+  const long n = rows * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cv;
+    const int c = (int)(i - r * cv) * 8;
+    float av[8], bv[8], v[8];
+    ld8<T>(a + r * lda + c, av);
+    if (b) ld8<T>(b + r * ldb + c, bv);
+    T* dp = d + r * ldd + c;
+    float o[8];
+    if (accumulate) ld8<T>(dp, o);
+    const float rs = (OP == 0 && rowscale) ? rowscale[r / rps] : 1.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (OP == 0) {
+        v[e] = alpha * av[e];
+        if (b) v[e] *= bv[e];
+        if (colscale) v[e] *= colscale[c + e];
+        v[e] *= rs;
+      } else if (OP == 1) {
+        v[e] = av[e] * gelu_grad_f(bv[e]);
+      } else {
+        v[e] = bv[e] > 0.f ? av[e] : 0.f;
+      }
+      if (accumulate) v[e] += o[e];
+    }
+    st8<T>(dp, v);
+  }
+}
+
+template <typename T>
+bool ew_al(const void* p, long ld) {
+  return p == nullptr || ((uintptr_t)p % 16 == 0 && ld % 8 == 0);
+}
+
 unsigned ew_grid(long n) { return (unsigned)min((long)8192, max(1L, (n + 255) / 256)); }
 
 template <int OP>
 int ew2d(int dtype, long rows, int C, const void* a, long lda, const void* b, long ldb, const float* cs,
          const float* rs, long rps, float alpha, void* d, long ldd, int acc, hipStream_t s) {
   if (rows * C == 0) return DFM_OK;
+  if (C % 8 == 0 && ew_al<float>(a, lda) && ew_al<float>(b, ldb) && ew_al<float>(d, ldd) &&
+      (dtype == DFM_BF16 || dtype == DFM_F32)) {
+    const unsigned gv = ew_grid(rows * C / 8);
+    if (dtype == DFM_BF16)
+      hipLaunchKernelGGL((ew2d_vec_kernel<bf16_t, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
+                         (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
+    else
+      hipLaunchKernelGGL((ew2d_vec_kernel<float, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const float*)a, lda,
+                         (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
   const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
     hipLaunchKernelGGL((ew2d_kernel<bf16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
@@ -176,6 +229,57 @@ __global__ void bn_bwd_apply_kernel(long rows, int C, const T* __restrict__ x, l
     T* dp = dx + r * lddx + c;
     if (accumulate) v += ldf(dp);
     stf(dp, v);
+  }
+}
+
+
+// 8-column vector forms of the BatchNorm apply kernels (rows 16-byte aligned, C % 8 == 0)
+template <typename T>
+__global__ void bn_apply_vec_kernel(long rows, int C, const T* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, const T* __restrict__ res, long ldres, int act,
+                                    T* __restrict__ y, long ldy) {
+  const int cv = C / 8;
+  const long n = rows * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cv;
+    const int c = (int)(i - r * cv) * 8;
+    float v[8], rv[8];
+    ld8<T>(x + r * ldx + c, v);
+    if (res) ld8<T>(res + r * ldres + c, rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = (v[e] - mean[c + e]) * rstd[c + e] * gamma[c + e] + beta[c + e];
+      if (res) v[e] += rv[e];
+      if (act == 2) v[e] = fmaxf(v[e], 0.f);
+    }
+    st8<T>(y + r * ldy + c, v);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_vec_kernel(long rows, int C, const T* __restrict__ x, long ldx, const T* __restrict__ dy,
+                                        long lddy, const float* __restrict__ mean, const float* __restrict__ rstd,
+                                        const float* __restrict__ gamma, const float* __restrict__ st, float inv_n,
+                                        T* __restrict__ dx, long lddx, int accumulate) {
+  const int cv = C / 8;
+  const long n = rows * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cv;
+    const int c = (int)(i - r * cv) * 8;
+    float xv[8], g[8], o[8];
+    ld8<T>(x + r * ldx + c, xv);
+    ld8<T>(dy + r * lddy + c, g);
+    T* dp = dx + r * lddx + c;
+    if (accumulate) ld8<T>(dp, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (xv[e] - mean[c + e]) * rstd[c + e];
+      float v = gamma[c + e] * rstd[c + e] * (g[e] - st[c + e] * inv_n - xh * st[C + c + e] * inv_n);
+      if (accumulate) v += o[e];
+      o[e] = v;
+    }
+    st8<T>(dp, o);
   }
 }
 
@@ -319,6 +423,17 @@ extern "C" int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx
                             const float* gamma, const float* beta, const void* res, long ldres, int act, void* y,
                             long ldy, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (C % 8 == 0 && ew_al<float>(x, ldx) && ew_al<float>(res, ldres) && ew_al<float>(y, ldy)) {
+    const unsigned gv = ew_grid(rows * C / 8);
+    if (dtype == DFM_BF16)
+      hipLaunchKernelGGL(bn_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean,
+                         rstd, gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
+    else
+      hipLaunchKernelGGL(bn_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean,
+                         rstd, gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
   const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean, rstd,
@@ -341,8 +456,19 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
                                 const float* mean, const float* rstd, const float* gamma, const float* stats2,
                                 double count, void* dx, long lddx, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  const unsigned g = ew_grid(rows * C);
   const float inv_n = (float)(1.0 / count);
+  if (C % 8 == 0 && ew_al<float>(x, ldx) && ew_al<float>(dy, lddy) && ew_al<float>(dx, lddx)) {
+    const unsigned gv = ew_grid(rows * C / 8);
+    if (dtype == DFM_BF16)
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
+                         (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx,
+                         (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
+  const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
                        (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);

@@ -5,9 +5,11 @@
 //   compile-time unrolled over MAXC classes), computes log-sum-exp and the CE term; block partials
 //   are summed in a fixed order.
 // Backward: a block owns a TY x TX tile of label pixels. Phase 1: every thread writes its pixel's
-//   (softmax - onehot) / count row into LDS. Phase 2: threads own (low-res cell, class) pairs of the
-//   patch the tile touches and gather the bilinear-weighted sum from LDS (separable tap weights).
+//   (softmax - onehot) / count row into LDS. Phase 2 (separable): each pixel row is reduced onto the
+//   patch's low-res columns (<= 2 taps per pixel), then the pixel rows onto its low-res rows.
 //   Phase 3: one global float atomic per (cell, class) per block (a cell is shared by <= ~10 blocks).
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -94,19 +96,14 @@ __global__ void zero_kernel(long n, float* __restrict__ p) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = 0.f;
 }
 
-DFM_INLINE float tap_w(int dst, int src_i, int in, int out) {
-  int i0, i1;
-  float l1;
-  src_idx(dst, in, out, i0, i1, l1);
-  return (i0 == src_i ? 1.f - l1 : 0.f) + (i1 == src_i ? l1 : 0.f);
-}
 
 template <typename T>
 __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, int ncls, const T* __restrict__ lg,
                                                            int H, int W, const long* __restrict__ label, int ignore,
                                                            const float* __restrict__ loss_out,
-                                                           const float* __restrict__ gscale, float* __restrict__ dlg) {
-  extern __shared__ __attribute__((aligned(16))) float gt[];  // [TY*TX][ncls+1]
+                                                           const float* __restrict__ gscale, float* __restrict__ dlg,
+                                                           int pcmax) {
+  extern __shared__ __attribute__((aligned(16))) float gt[];  // [TY*TX][ncls+1], then rx
   const int GLD = ncls + 1;
   const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY;
   int bid = blockIdx.x;
@@ -145,7 +142,8 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
     }
   }
   __syncthreads();
-  // phase 2: gather per (low-res cell, class) of the patch
+  // phase 2 (separable): (a) x-reduction of each pixel row onto the patch's low-res columns,
+  // (b) y-reduction onto its low-res rows; every pixel has <= 2 taps per axis.
   int a0, a1, b0, b1, t0;
   float tl;
   src_idx(y0, h, H, a0, t0, tl);
@@ -153,24 +151,57 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
   src_idx(x0, w, W, b0, t0, tl);
   src_idx(x0 + nx - 1, w, W, t0, b1, tl);
   const int pr = a1 - a0 + 1, pc = b1 - b0 + 1;
-  const float sx = (float)W / (float)w;
+  float* rx = gt + TY * TX * GLD;                      // [TY][pcmax][GLD]
+  __shared__ int xj0[TX], xj1[TX], yi0[TY], yi1[TY];   // taps relative to b0 / a0
+  __shared__ float xw0[TX], xw1[TX], yw0[TY], yw1[TY];
+  __shared__ int jlo[TX + 2], jhi[TX + 2];
+  if (threadIdx.x < nx) {
+    int i0, i1;
+    float l1;
+    src_idx(x0 + threadIdx.x, w, W, i0, i1, l1);
+    xj0[threadIdx.x] = i0 - b0; xj1[threadIdx.x] = i1 - b0;
+    xw0[threadIdx.x] = 1.f - l1; xw1[threadIdx.x] = l1;
+  }
+  if (threadIdx.x >= 64 && threadIdx.x < 64 + ny) {
+    const int py = threadIdx.x - 64;
+    int i0, i1;
+    float l1;
+    src_idx(y0 + py, h, H, i0, i1, l1);
+    yi0[py] = i0 - a0; yi1[py] = i1 - a0;
+    yw0[py] = 1.f - l1; yw1[py] = l1;
+  }
+  __syncthreads();
+  if (threadIdx.x < pc) {  // pixel-column range touching low-res column jj (taps are monotone in px)
+    const int jj = threadIdx.x;
+    int lo = nx, hi = -1;
+    for (int px = 0; px < nx; ++px)
+      if (xj0[px] == jj || xj1[px] == jj) {
+        lo = min(lo, px);
+        hi = px;
+      }
+    jlo[jj] = lo;
+    jhi[jj] = hi;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < ny * pc * ncls; e += 256) {
+    const int c = e % ncls, t = e / ncls, jj = t % pc, py = t / pc;
+    float r = 0.f;
+    const float* grow = gt + (py * TX) * GLD + c;
+    for (int px = jlo[jj]; px <= jhi[jj]; ++px) {
+      const float wx = (xj0[px] == jj ? xw0[px] : 0.f) + (xj1[px] == jj ? xw1[px] : 0.f);
+      r = fmaf(wx, grow[px * GLD], r);
+    }
+    rx[(py * pcmax + jj) * GLD + c] = r;
+  }
+  __syncthreads();
   for (int e = threadIdx.x; e < pr * pc * ncls; e += 256) {
-    const int c = e % ncls, cell = e / ncls;
-    const int i = a0 + cell / pc, j = b0 + cell % pc;
-    const int xlo = max(0, (int)floorf((j - 0.5f) * sx - 0.5f) - 1 - x0);
-    const int xhi = min(nx - 1, (int)ceilf((j + 1.5f) * sx - 0.5f) + 1 - x0);
+    const int c = e % ncls, t = e / ncls, jj = t % pc, ii = t / pc;
     float acc = 0.f;
     for (int py = 0; py < ny; ++py) {
-      const float wy = tap_w(y0 + py, i, h, H);
-      if (wy == 0.f) continue;
-      float r = 0.f;
-      for (int px = xlo; px <= xhi; ++px) {
-        const float wx = tap_w(x0 + px, j, w, W);
-        if (wx != 0.f) r += wx * gt[(py * TX + px) * GLD + c];
-      }
-      acc += wy * r;
+      const float wy = (yi0[py] == ii ? yw0[py] : 0.f) + (yi1[py] == ii ? yw1[py] : 0.f);
+      acc = fmaf(wy, rx[(py * pcmax + jj) * GLD + c], acc);
     }
-    if (acc != 0.f) atomicAdd(&dlg[(((long)b * h + i) * w + j) * ncls + c], acc);
+    if (acc != 0.f) atomicAdd(&dlg[(((long)b * h + a0 + ii) * w + b0 + jj) * ncls + c], acc);
   }
 }
 
@@ -209,21 +240,22 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
   hipLaunchKernelGGL(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
   DFM_LAUNCH_CHECK();
   const unsigned nblk = B * ((H + TY - 1) / TY) * ((W + TX - 1) / TX);
-  const size_t lds = (size_t)TY * TX * (ncls + 1) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
+  // low-res columns one TX-wide pixel tile can touch (+2 for the taps at both ends)
+  const int pcmax = std::min(TX + 2, (int)(((long)TX * w + W - 1) / W) + 3);
+  const size_t lds = ((size_t)TY * TX + (size_t)TY * pcmax) * (ncls + 1) * sizeof(float);
+  if (lds > 64 * 1024) {  // only small upsampling ratios need more than the default
     (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+                              (int)lds);
     (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
+                              (int)lds);
+    (void)hipGetLastError();  // a refused attribute must not read as this launch's error
   }
   if (dtype == DFM_BF16)
     hipLaunchKernelGGL(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
-                       H, W, label, ignore, loss_out, gscale, dlogits);
+                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
   else
     hipLaunchKernelGGL(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,
-                       H, W, label, ignore, loss_out, gscale, dlogits);
+                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -152,6 +152,32 @@ def test_layernorm(dt, C):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("C", [32, 128, 512, 1024])
+def test_layernorm_views_accumulate(dt, C):
+    """Column-slice views (row stride > C), the fused residual-gradient add and accumulate=True."""
+    k = K()
+    rows = 777
+    xb = (torch.randn(rows, C + 16, device=DEV) * 2 + 0.5).to(dt)
+    x = xb[:, 8:8 + C]
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    yb = torch.zeros(rows, C + 8, device=DEV).to(dt)
+    _, mean, rstd = k.layernorm(x, g, b, 1e-6, out=yb[:, 8:])
+    xr = x.float().requires_grad_()
+    ref = F.layer_norm(xr, (C,), g, b, 1e-6)
+    assert rel(yb[:, 8:].float(), ref) < TOL[dt]
+    dy = torch.randn(rows, C, device=DEV).to(dt)
+    dres = torch.randn(rows, C, device=DEV).to(dt)
+    base = torch.randn(rows, C + 8, device=DEV).to(dt)
+    dx = base.clone()
+    ref.backward(dy.float())
+    k.layernorm_bwd(x, dy, g, mean, rstd, dx=dx[:, :C], accumulate=True, dres=dres)
+    want = xr.grad + dres.float() + base[:, :C].float()
+    assert rel(dx[:, :C].float(), want) < TOL[dt] * 2
+    assert torch.equal(dx[:, C:], base[:, C:])
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("ks,ident", [(7, False), (3, True)])
 @pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16)])
 def test_dwconv(dt, ks, ident, B, H, W, C):
@@ -275,8 +301,18 @@ def test_colsum_and_elementwise(dt):
     pr = pre.float().requires_grad_()
     F.gelu(pr).backward(x.float())
     assert rel(g.float(), pr.grad) < TOL[dt]
-    y = k.scale_mul(x, mul=m, colscale=torch.rand(72, device=DEV))
-    assert y.shape == x.shape
+    cs = torch.rand(72, device=DEV)
+    y = k.scale_mul(x, mul=m, colscale=cs)
+    assert rel(y.float(), x.float() * m.float() * cs) < TOL[dt]
+    # strided views + accumulate (vector path) and an odd width (scalar path)
+    acc = torch.randn(5000, 80, device=DEV).to(dt)
+    want = acc[:, 8:].float() + x.float() * m.float() * cs * rs.repeat_interleave(1250)[:, None]
+    k.scale_mul(x, mul=m, colscale=cs, rowscale=rs, rows_per_scale=1250, out=acc[:, 8:], accumulate=True)
+    assert rel(acc[:, 8:].float(), want) < TOL[dt]
+    xo, po = x[:, :71], pre.detach()[:, :71]
+    pr2 = po.detach().float().clone().requires_grad_()
+    F.gelu(pr2).backward(xo.float())
+    assert rel(k.gelu_bwd(xo, po).float(), pr2.grad) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)
