@@ -46,7 +46,9 @@ struct GemmArgs {
   int vec_ok;      // output-side rows 16-byte aligned (vector epilogue)
   int mul_gelu_grad;
   int stream;      // host: take the M-streaming persistent kernel
+  int tiles_n;     // output column tiles (grid.x enumerates tiles_m * tiles_n)
 };
+
 
 template <typename T> struct Mf;
 template <> struct Mf<bf16_t> {
@@ -424,7 +426,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-  const int bm = blockIdx.x * BM, bn = blockIdx.y * BN;
+  const int tiles_m = (a.M + BM - 1) / BM;  // grid.x enumerates M tiles fastest
+  const int bm = (blockIdx.x % tiles_m) * BM, bn = (blockIdx.x / tiles_m) * BN;
   const int b = blockIdx.z / a.splits, split = blockIdx.z % a.splits;
 
   const int kper = ((a.K + a.splits - 1) / a.splits + BK - 1) / BK * BK;
@@ -714,7 +717,8 @@ int launch_cfg(GemmArgs& a, hipStream_t s) {
   constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;  // epilogue rows per pass
   const size_t lds_c = (size_t)RP * (BN + 4) * sizeof(float);
   const size_t lds = lds_op > lds_c ? lds_op : lds_c;
-  dim3 grid(cdiv(a.M, BM), cdiv(a.Nw, BN), a.batch * a.splits);
+  a.tiles_n = cdiv(a.Nw, BN);
+  dim3 grid(cdiv(a.M, BM) * a.tiles_n, 1, a.batch * a.splits);
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>,

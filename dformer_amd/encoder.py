@@ -129,6 +129,7 @@ class Block(nn.Module):
             self.mlp_e2 = MLP(dim // 2, int(mlp_ratio))
         self.drop_depth = drop_depth
         self.drop_path_masks = None  # tests may inject the 4 per-sample keep masks (mmcv call order)
+        self._row_scales = None  # [4, B] DropPath scales drawn for the whole backbone by DFormer.forward
 
     def forward(self, x, x_e):
         B, H, W, C = x.shape
@@ -138,6 +139,9 @@ class Block(nn.Module):
         if self.drop_path_masks is not None and self.training and self.drop_prob > 0:
             keep = 1.0 - self.drop_prob
             rs = [m.to(device=x.device, dtype=torch.float32) / keep for m in self.drop_path_masks]
+        elif self._row_scales is not None:
+            rs = list(self._row_scales.unbind(0))
+            self._row_scales = None
         else:
             rs = [_drop_path_scale(B, self.drop_prob, self.training, x.device) for _ in range(4)]
         ls1e = self.layer_scale_1_e if not self.drop_depth else None
@@ -204,6 +208,19 @@ class DFormer(nn.Module):
         invalidate_weights()
         return r
 
+    def _draw_drop_path(self, B, dev):
+        """mmcv DropPath scales floor(keep + U[0,1)) / keep for all four DropPath calls of every
+        Block, drawn by one RNG launch for the whole backbone instead of four per Block."""
+        blocks = [b for st in self.stages for b in st]
+        if not self.training or all(b.drop_prob == 0.0 for b in blocks):
+            return
+        keep = getattr(self, "_keep", None)
+        if keep is None or keep.device != dev:
+            keep = self._keep = torch.tensor([1.0 - b.drop_prob for b in blocks], device=dev).view(-1, 1, 1)
+        rs = (keep + torch.rand(len(blocks), 4, B, device=dev)).floor_().div_(keep)
+        for b, r in zip(blocks, rs.unbind(0)):
+            b._row_scales = r if b.drop_prob > 0 else None
+
     def _downsample(self, i, x, e):
         dt = self.compute_dtype
         with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
@@ -222,6 +239,7 @@ class DFormer(nn.Module):
         dt = self.compute_dtype
         x = x.to(dt).contiguous(memory_format=torch.channels_last)
         x_e = x_e.to(dt).contiguous(memory_format=torch.channels_last)
+        self._draw_drop_path(x.shape[0], x.device)
         outs = []
         for i in range(4):
             x, x_e = self._downsample(i, x, x_e)
