@@ -122,6 +122,174 @@ __global__ void bilinear_bwd_kernel(int B, int Hi, int Wi, int Ho, int Wo, int C
   }
 }
 
+
+// ------------------------------------------------------------------ 8-channel vector forms
+// (C % 8 == 0, 16-byte aligned rows). Each lane moves 8 channels per 16-byte access.
+inline bool vec_ok(int C, const void* p, long ld) {
+  return C % 8 == 0 && ld % 8 == 0 && (uintptr_t)p % 16 == 0;
+}
+
+// pool: one block per (image, cell); CV = C/8 lanes per pixel, 256/CV pixels of the bin in
+// flight, partial sums meet in LDS in a fixed order.
+template <typename T>
+__global__ __launch_bounds__(256) void pool7_fwd_vec_kernel(int B, int H, int W, int C, const T* __restrict__ x,
+                                                            long ldx, T* __restrict__ y, long ldy) {
+  extern __shared__ float pred[];  // [PG][C]
+  const int cell = blockIdx.x % 49, b = blockIdx.x / 49;
+  const int CV = C / 8, PG = 256 / CV;
+  const int cv = threadIdx.x % CV, pg = threadIdx.x / CV;
+  const int i = cell / 7, j = cell % 7;
+  const int h0 = bin_lo(i, H), h1 = bin_hi(i, H), w0 = bin_lo(j, W), w1 = bin_hi(j, W);
+  const int nw = w1 - w0, npix = (h1 - h0) * nw;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pg < PG) {
+    for (int q = pg; q < npix; q += PG) {
+      const int h = h0 + q / nw, w = w0 + q % nw;
+      float v[8];
+      ld8<T>(x + ((long)(b * H + h) * W + w) * ldx + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pred[pg * C + cv * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  const float inv = 1.f / (float)npix;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float t = 0.f;
+    for (int g = 0; g < PG; ++g) t += pred[g * C + c];
+    stf(y + ((long)b * 49 + cell) * ldy + c, t * inv);
+  }
+}
+
+// pool backward: one lane per (pixel, 8 channels), gathering the overlapping bins it lies in.
+template <typename T>
+__global__ void pool7_bwd_vec_kernel(int B, int H, int W, int C, const T* __restrict__ dy, long lddy,
+                                     T* __restrict__ dx, long lddx, int accumulate) {
+  const int CV = C / 8;
+  const long n = (long)B * H * W * CV;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % CV) * 8;
+    const long pix = e / CV;
+    const int w = pix % W, h = (pix / W) % H, b = pix / ((long)W * H);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // for n >= 7 a row lies in bins ic-1..ic+1 only; smaller maps repeat rows over more bins
+    const int ic = (h * 7) / H, jc = (w * 7) / W;
+    const int ia = H >= 7 ? max(0, ic - 1) : 0, ib = H >= 7 ? min(6, ic + 1) : 6;
+    const int ja = W >= 7 ? max(0, jc - 1) : 0, jb = W >= 7 ? min(6, jc + 1) : 6;
+    for (int i = ia; i <= ib; ++i) {
+      const int ha = bin_lo(i, H), hb = bin_hi(i, H);
+      if (h < ha || h >= hb) continue;
+      for (int j = ja; j <= jb; ++j) {
+        const int wa = bin_lo(j, W), wb = bin_hi(j, W);
+        if (w < wa || w >= wb) continue;
+        const float inv = 1.f / (float)((hb - ha) * (wb - wa));
+        float v[8];
+        ld8<T>(dy + ((long)b * 49 + i * 7 + j) * lddy + c, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += v[q] * inv;
+      }
+    }
+    T* p = dx + pix * lddx + c;
+    if (accumulate) {
+      float o[8];
+      ld8<T>(p, o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += o[q];
+    }
+    st8<T>(p, s);
+  }
+}
+
+template <typename T>
+__global__ void bilinear_fwd_vec_kernel(int B, int Hi, int Wi, int Ho, int Wo, int C, const T* __restrict__ x,
+                                        long ldx, T* __restrict__ y, long ldy, int accumulate) {
+  const int CV = C / 8;
+  const long n = (long)B * Ho * Wo * CV;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % CV) * 8;
+    const long pix = e / CV;
+    const int wo = pix % Wo, ho = (pix / Wo) % Ho, b = pix / ((long)Wo * Ho);
+    int h0, h1, w0, w1;
+    float lh, lw;
+    src_index(ho, Hi, Ho, h0, h1, lh);
+    src_index(wo, Wi, Wo, w0, w1, lw);
+    const T* xb = x + (long)b * Hi * Wi * ldx + c;
+    float v00[8], v01[8], v10[8], v11[8], o[8];
+    ld8<T>(xb + ((long)h0 * Wi + w0) * ldx, v00);
+    ld8<T>(xb + ((long)h0 * Wi + w1) * ldx, v01);
+    ld8<T>(xb + ((long)h1 * Wi + w0) * ldx, v10);
+    ld8<T>(xb + ((long)h1 * Wi + w1) * ldx, v11);
+    T* p = y + pix * ldy + c;
+    if (accumulate) ld8<T>(p, o);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float v = (1.f - lh) * ((1.f - lw) * v00[q] + lw * v01[q]) + lh * ((1.f - lw) * v10[q] + lw * v11[q]);
+      o[q] = accumulate ? o[q] + v : v;
+    }
+    st8<T>(p, o);
+  }
+}
+
+// bilinear backward (a gather): one block per input cell (b, hi, wi); the output rows / columns
+// that read the cell and their tap weights go to LDS once, then CV lanes per output pixel walk the
+// window with 16-byte loads and the partial sums meet in LDS in a fixed order.
+constexpr int BL_MAXT = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void bilinear_bwd_vec_kernel(int B, int Hi, int Wi, int Ho, int Wo, int C,
+                                                               const T* __restrict__ dy, long lddy,
+                                                               T* __restrict__ dx, long lddx, int accumulate) {
+  extern __shared__ float bred[];  // [PG][C]
+  __shared__ int rows[BL_MAXT], cols[BL_MAXT];
+  __shared__ float rw[BL_MAXT], cw[BL_MAXT];
+  __shared__ int nr, nc;
+  const int wi = blockIdx.x % Wi, hi = (blockIdx.x / Wi) % Hi, b = blockIdx.x / (Wi * Hi);
+  if (threadIdx.x == 0) {
+    const float sh = (float)Ho / (float)Hi, sw = (float)Wo / (float)Wi;
+    const int ho0 = max(0, (int)floorf((hi - 0.5f) * sh - 0.5f) - 1);
+    const int ho1 = min(Ho - 1, (int)ceilf((hi + 1.5f) * sh - 0.5f) + 1);
+    const int wo0 = max(0, (int)floorf((wi - 0.5f) * sw - 0.5f) - 1);
+    const int wo1 = min(Wo - 1, (int)ceilf((wi + 1.5f) * sw - 0.5f) + 1);
+    int k = 0;
+    for (int ho = ho0; ho <= ho1 && k < BL_MAXT; ++ho) {
+      const float t = tap_weight(ho, hi, Hi, Ho);
+      if (t != 0.f) { rows[k] = ho; rw[k] = t; ++k; }
+    }
+    nr = k;
+    k = 0;
+    for (int wo = wo0; wo <= wo1 && k < BL_MAXT; ++wo) {
+      const float t = tap_weight(wo, wi, Wi, Wo);
+      if (t != 0.f) { cols[k] = wo; cw[k] = t; ++k; }
+    }
+    nc = k;
+  }
+  __syncthreads();
+  const int CV = C / 8, PG = 256 / CV;
+  const int cv = threadIdx.x % CV, pg = threadIdx.x / CV;
+  const int npix = nr * nc;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pg < PG) {
+    for (int q = pg; q < npix; q += PG) {
+      const int r = q / nc, k = q % nc;
+      const float wgt = rw[r] * cw[k];
+      float v[8];
+      ld8<T>(dy + ((long)(b * Ho + rows[r]) * Wo + cols[k]) * lddy + cv * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(wgt, v[e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bred[pg * C + cv * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  const long pix = (long)(b * Hi + hi) * Wi + wi;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float t = 0.f;
+    for (int g = 0; g < PG; ++g) t += bred[g * C + c];
+    T* p = dx + pix * lddx + c;
+    stf(p, accumulate ? t + ldf(p) : t);
+  }
+}
+
 // ------------------------------------------------------------------ pooled attention
 constexpr int NQ = 49;
 constexpr int NC = 64;  // keys per chunk
@@ -340,6 +508,23 @@ int dispatch(int dtype, F8 f8, F32 f32) {
 extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, const void* x, long ldx, void* y,
                                       long ldy, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (C <= 2048 && vec_ok(C, x, ldx)) {
+    const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
+    return dispatch(
+        dtype,
+        [&] {
+          hipLaunchKernelGGL(pool7_fwd_vec_kernel<bf16_t>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
+                             (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        },
+        [&] {
+          hipLaunchKernelGGL(pool7_fwd_vec_kernel<float>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
+                             (const float*)x, ldx, (float*)y, ldy);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        });
+  }
   dim3 grid(B * 49, cdiv(C, 256));
   return dispatch(
       dtype,
@@ -358,6 +543,23 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, const void* dy, long lddy, void* dx,
                                       long lddx, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (vec_ok(C, dy, lddy) && vec_ok(C, dx, lddx)) {
+    const unsigned gv = grid_for((long)B * H * W * (C / 8));
+    return dispatch(
+        dtype,
+        [&] {
+          hipLaunchKernelGGL(pool7_bwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy,
+                             lddy, (bf16_t*)dx, lddx, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        },
+        [&] {
+          hipLaunchKernelGGL(pool7_bwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const float*)dy,
+                             lddy, (float*)dx, lddx, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        });
+  }
   const unsigned g = grid_for((long)B * H * W * C);
   return dispatch(
       dtype,
@@ -376,6 +578,23 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* x, long ldx,
                                 void* y, long ldy, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (vec_ok(C, x, ldx) && vec_ok(C, y, ldy)) {
+    const unsigned gv = grid_for((long)B * Ho * Wo * (C / 8));
+    return dispatch(
+        dtype,
+        [&] {
+          hipLaunchKernelGGL(bilinear_fwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
+                             (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        },
+        [&] {
+          hipLaunchKernelGGL(bilinear_fwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
+                             (const float*)x, ldx, (float*)y, ldy, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        });
+  }
   const unsigned g = grid_for((long)B * Ho * Wo * C);
   return dispatch(
       dtype,
@@ -394,6 +613,25 @@ extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
 extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* dy, long lddy,
                                 void* dx, long lddx, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
+  // taps per axis: ~2 * out/in + 3 must fit the block's LDS lists
+  const bool taps_fit = 2 * (Ho / Hi) + 6 <= BL_MAXT && 2 * (Wo / Wi) + 6 <= BL_MAXT && Ho >= Hi && Wo >= Wi;
+  if (C <= 2048 && taps_fit && vec_ok(C, dy, lddy) && (uintptr_t)dx % 4 == 0) {
+    const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
+    return dispatch(
+        dtype,
+        [&] {
+          hipLaunchKernelGGL(bilinear_bwd_vec_kernel<bf16_t>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
+                             C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        },
+        [&] {
+          hipLaunchKernelGGL(bilinear_bwd_vec_kernel<float>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
+                             C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
+          DFM_LAUNCH_CHECK();
+          return DFM_OK;
+        });
+  }
   const unsigned g = grid_for((long)B * Hi * Wi * C);
   return dispatch(
       dtype,
