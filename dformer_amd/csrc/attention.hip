@@ -5,6 +5,8 @@
 // The attention is split over key chunks (flash-style partial max / sum / output + a combine
 // pass), so K and V are read exactly once per head; the backward recomputes P from the saved
 // log-sum-exp and writes dK/dV per chunk directly, dQ through per-chunk partials.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -125,9 +127,16 @@ __global__ void bilinear_bwd_kernel(int B, int Hi, int Wi, int Ho, int Wo, int C
 
 // ------------------------------------------------------------------ 8-channel vector forms
 // (C % 8 == 0, 16-byte aligned rows). Each lane moves 8 channels per 16-byte access.
-inline bool vec_ok(int C, const void* p, long ld) {
-  return C % 8 == 0 && ld % 8 == 0 && (uintptr_t)p % 16 == 0;
+// DFM_SCALAR_RESIZE bitmask (A/B checks): 1 bilinear fwd, 2 bilinear bwd, 4 pool fwd, 8 pool bwd
+// take the scalar kernels
+inline int scalar_resize_mask() {
+  static const int m = [] {
+    const char* e = getenv("DFM_SCALAR_RESIZE");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
 }
+inline bool vec_ok(int C, const void* p, long ld) { return C % 8 == 0 && ld % 8 == 0 && (uintptr_t)p % 16 == 0; }
 
 // pool: one block per (image, cell); CV = C/8 lanes per pixel, 256/CV pixels of the bin in
 // flight, partial sums meet in LDS in a fixed order.
@@ -494,6 +503,349 @@ __global__ void attn_dq_reduce_kernel(AttnArgs a) {
   }
 }
 
+
+// ------------------------------------------------------------------ MFMA pooled attention (bf16)
+// One wave owns a chunk of `kpw` keys of one (image, head) and walks it in 32-key blocks with
+// v_mfma_f32_16x16x32_bf16 (fp32 accumulate); the 49 queries are padded to 64. Fragment lanes:
+// A (m = lane&15, k = 8*(lane>>4)+e), B (n = lane&15, k = 8*(lane>>4)+e), C (n = lane&15,
+// m = 4*(lane>>4)+r). Loading the A operand's rows in the permuted order
+// row(i) = 8*(i>>2) + 4t + (i&3) for the two 16-row tiles t of a 32-row block makes the C tiles
+// of the pair hold, per lane, rows 8*(lane>>4)+e in natural order: exactly a B (or A) fragment
+// of the next product, so P and dS never leave registers except where a transpose is needed
+// (K^T and dS^T for dQ, V^T for O: staged in LDS and read with ds_read_b64_tr_b16).
+// Softmax row statistics are reduced with lane shuffles (xor 16, 32) across the 4 lane groups.
+DFM_INLINE bf16x8_t ldfrag16(const bf16_t* p, bool ok) {
+  if (!ok) return bf16x8_t{};
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+DFM_INLINE bf16x8_t pack_bf16x8(const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(w[0], w[1], w[2], w[3]));
+}
+// fragment (r = r0 + (lane&15), k = k0 + 8*(lane>>4) + e) of an LDS image stored [k][r] (r contiguous)
+DFM_INLINE bf16x8_t frag_tr(const bf16_t* lds, int LD, int r0, int k0, int lane) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+  typedef __attribute__((address_space(3))) short4_t lds_s4;
+  const bf16_t* a0 = lds + (k0 + 8 * g + q) * LD + r0 + 4 * p;
+  const bf16_t* a1 = a0 + 4 * LD;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a1));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  short8_t sv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, sv);
+}
+DFM_INLINE void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#define MFMA16(A, B, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16((A), (B), (C), 0, 0, 0)
+
+// Forward: S^T = K Q^T (keys as rows), online softmax per query, O^T += V^T P^T.
+// Partials per wave (chunk): unnormalised O [49][DH], running max m and sum l (scaled units).
+template <int DH>
+__global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw, int groups) {
+  constexpr int KD = (DH + 31) / 32, ND = DH / 16, LDV = DH + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t sV[4][32 * LDV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int bh = blockIdx.x / groups, chunk = (blockIdx.x % groups) * 4 + w;
+  if (chunk >= a.nchunk) return;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const int n0 = chunk * kpw, n1 = min(a.N, n0 + kpw);
+  const bf16_t* Q = (const bf16_t*)a.q + (long)b * NQ * a.ldq + h * DH;
+  const bf16_t* K = (const bf16_t*)a.k + (long)b * a.N * a.ldkv + h * DH;
+  const bf16_t* V = (const bf16_t*)a.v + (long)b * a.N * a.ldkv + h * DH;
+  bf16_t* sv = sV[w];
+  bf16x8_t qf[4][KD];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < KD; ++ks) {
+      const int q = 16 * nt + j, d0 = 32 * ks + 8 * g;
+      qf[nt][ks] = ldfrag16(Q + (long)q * a.ldq + d0, q < NQ && d0 < DH);
+    }
+  float mrun[4], lrun[4];
+  float4_t o[ND][4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    mrun[nt] = -INFINITY;
+    lrun[nt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) o[dt][nt] = float4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int kb = n0; kb < n1; kb += 32) {
+    // V block -> LDS [key][d] (zero rows past the chunk)
+    constexpr int VCH = DH / 8;
+#pragma unroll
+    for (int it = 0; it < (32 * VCH + 63) / 64; ++it) {
+      const int idx = lane + 64 * it;
+      if (idx < 32 * VCH) {
+        const int key = idx / VCH, ch = idx % VCH;
+        const uint4 u = kb + key < n1 ? *reinterpret_cast<const uint4*>(V + (long)(kb + key) * a.ldkv + ch * 8)
+                                      : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(sv + key * LDV + ch * 8) = u;
+      }
+    }
+    bf16x8_t kf[2][KD];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KD; ++ks) {
+        const int key = kb + 8 * (j >> 2) + 4 * t + (j & 3), d0 = 32 * ks + 8 * g;
+        kf[t][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+      }
+    float4_t st[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        float4_t acc = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KD; ++ks) acc = MFMA16(kf[t][ks], qf[nt][ks], acc);
+        st[t][nt] = acc;
+      }
+    bf16x8_t pf[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float sv8[8];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int key = kb + 8 * g + e;
+        const float x = key < n1 ? st[e >> 2][nt][e & 3] * a.scale : -INFINITY;
+        sv8[e] = x;
+        mx = fmaxf(mx, x);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrun[nt], mx);
+      const float alpha = __expf(mrun[nt] - mnew);
+      float ps = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sv8[e] = __expf(sv8[e] - mnew);
+        ps += sv8[e];
+      }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      lrun[nt] = lrun[nt] * alpha + ps;
+      mrun[nt] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) o[dt][nt] *= alpha;
+      pf[nt] = pack_bf16x8(sv8);
+    }
+    lds_wave_sync();
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const bf16x8_t vf = frag_tr(sv, LDV, 16 * dt, 0, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) o[dt][nt] = MFMA16(vf, pf[nt], o[dt][nt]);
+    }
+    lds_wave_sync();  // the next block's V stage overwrites sv
+  }
+  float* pm = a.ws + (long)a.B * a.heads * a.nchunk * NQ * DH;
+  float* pl = pm + (long)a.B * a.heads * a.nchunk * NQ;
+  const long base = ((long)bh * a.nchunk + chunk) * NQ;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int q = 16 * nt + j;
+    if (q >= NQ) continue;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+      *reinterpret_cast<float4*>(a.ws + (base + q) * DH + 16 * dt + 4 * g) =
+          make_float4(o[dt][nt][0], o[dt][nt][1], o[dt][nt][2], o[dt][nt][3]);
+    if (g == 0) {
+      pm[base + q] = mrun[nt];
+      pl[base + q] = lrun[nt];
+    }
+  }
+}
+
+// Backward per wave chunk: S' = Q K^T and dP' = dO V^T with keys as columns (lane = key), then
+// P' = exp(S' scale - lse), dS' = P' (dP' - D); dV^T += dO^T P', dK^T += Q^T dS' (scale), both
+// complete per 32-key block and stored directly; dQ^T += K^T dS'^T through LDS (partial per chunk).
+template <int DH>
+__global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw, int groups) {
+  constexpr int KD = (DH + 31) / 32, ND = DH / 16, LDD = DH + 8, LDQ = 64 + 8;
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[64 * LDD], sO[64 * LDD];
+  __shared__ __attribute__((aligned(16))) bf16_t sK[4][32 * LDD], sS[4][32 * LDQ];
+  __shared__ float sL[64], sD[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int bh = blockIdx.x / groups, chunk = (blockIdx.x % groups) * 4 + w;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const bf16_t* Q = (const bf16_t*)a.q + (long)b * NQ * a.ldq + h * DH;
+  const bf16_t* GO = (const bf16_t*)a.dout + (long)b * NQ * a.lddo + h * DH;
+  const bf16_t* Op = (const bf16_t*)a.o + (long)b * NQ * a.ldo + h * DH;
+  constexpr int VCH = DH / 8;
+  for (int idx = threadIdx.x; idx < 64 * VCH; idx += 256) {  // Q, dO -> LDS [q][d], rows >= 49 zero
+    const int q = idx / VCH, ch = idx % VCH;
+    uint4 uq = make_uint4(0, 0, 0, 0), uo = make_uint4(0, 0, 0, 0);
+    if (q < NQ) {
+      uq = *reinterpret_cast<const uint4*>(Q + (long)q * a.ldq + ch * 8);
+      uo = *reinterpret_cast<const uint4*>(GO + (long)q * a.lddo + ch * 8);
+    }
+    *reinterpret_cast<uint4*>(sQ + q * LDD + ch * 8) = uq;
+    *reinterpret_cast<uint4*>(sO + q * LDD + ch * 8) = uo;
+  }
+  if (threadIdx.x < 64) {  // lse and D = rowsum(dO * O)
+    const int q = threadIdx.x;
+    float dsum = 0.f, l = 0.f;
+    if (q < NQ) {
+      for (int d = 0; d < DH; d += 8) {
+        float x[8], y[8];
+        ld8<bf16_t>(GO + (long)q * a.lddo + d, x);
+        ld8<bf16_t>(Op + (long)q * a.ldo + d, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum += x[e] * y[e];
+      }
+      l = a.lse[(long)bh * NQ + q];
+    }
+    sL[q] = l;
+    sD[q] = dsum;
+  }
+  __syncthreads();
+  if (chunk >= a.nchunk) return;
+  const int n0 = chunk * kpw, n1 = min(a.N, n0 + kpw);
+  const bf16_t* K = (const bf16_t*)a.k + (long)b * a.N * a.ldkv + h * DH;
+  const bf16_t* V = (const bf16_t*)a.v + (long)b * a.N * a.ldkv + h * DH;
+  bf16_t* dK = (bf16_t*)a.dk + (long)b * a.N * a.lddkv + h * DH;
+  bf16_t* dV = (bf16_t*)a.dv + (long)b * a.N * a.lddkv + h * DH;
+  bf16_t* sk = sK[w];
+  bf16_t* ss = sS[w];
+  // per-wave constant fragments
+  bf16x8_t qa[2][2][KD], oa[2][2][KD];  // A (m = q permuted, k = d)
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KD; ++ks) {
+        const int q = 32 * qb + 8 * (j >> 2) + 4 * t + (j & 3), d0 = 32 * ks + 8 * g;
+        qa[qb][t][ks] = ldfrag16(sQ + q * LDD + d0, d0 < DH);
+        oa[qb][t][ks] = ldfrag16(sO + q * LDD + d0, d0 < DH);
+      }
+  bf16x8_t qt[ND][2], ot[ND][2];  // A (m = d, k = q): Q^T, dO^T
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      qt[dt][qb] = frag_tr(sQ, LDD, 16 * dt, 32 * qb, lane);
+      ot[dt][qb] = frag_tr(sO, LDD, 16 * dt, 32 * qb, lane);
+    }
+  float Lq[2][8], Dq[2][8];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      Lq[qb][e] = sL[32 * qb + 8 * g + e];
+      Dq[qb][e] = sD[32 * qb + 8 * g + e];
+    }
+  float4_t dq[ND][4];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) dq[dt][nt] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = n0; kb < n1; kb += 32) {
+#pragma unroll
+    for (int it = 0; it < (32 * VCH + 63) / 64; ++it) {  // K block -> LDS [key][d]
+      const int idx = lane + 64 * it;
+      if (idx < 32 * VCH) {
+        const int key = idx / VCH, ch = idx % VCH;
+        const uint4 u = kb + key < n1 ? *reinterpret_cast<const uint4*>(K + (long)(kb + key) * a.ldkv + ch * 8)
+                                      : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(sk + key * LDD + ch * 8) = u;
+      }
+    }
+    bf16x8_t kf[2][KD], vf[2][KD];  // B (k = d, n = key)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < KD; ++ks) {
+        const int key = kb + 16 * kt + j, d0 = 32 * ks + 8 * g;
+        kf[kt][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+        vf[kt][ks] = ldfrag16(V + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+      }
+    bf16x8_t pb[2][2], dsb[2][2];  // [kt][qb]: B (k = q 32qb + 8g + e, n = key 16kt + j)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bool kvalid = kb + 16 * kt + j < n1;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float4_t sp[2], dp[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          float4_t s4 = float4_t{0.f, 0.f, 0.f, 0.f}, d4 = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KD; ++ks) {
+            s4 = MFMA16(qa[qb][t][ks], kf[kt][ks], s4);
+            d4 = MFMA16(oa[qb][t][ks], vf[kt][ks], d4);
+          }
+          sp[t] = s4;
+          dp[t] = d4;
+        }
+        float p8[8], ds8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int q = 32 * qb + 8 * g + e;
+          const float p = (kvalid && q < NQ) ? __expf(sp[e >> 2][e & 3] * a.scale - Lq[qb][e]) : 0.f;
+          p8[e] = p;
+          ds8[e] = p * (dp[e >> 2][e & 3] - Dq[qb][e]);
+        }
+        pb[kt][qb] = pack_bf16x8(p8);
+        dsb[kt][qb] = pack_bf16x8(ds8);
+        // dS' row (key) -> LDS [key][q] for the dS^T operand of dQ
+        *reinterpret_cast<bf16x8_t*>(ss + (16 * kt + j) * LDQ + 32 * qb + 8 * g) = dsb[kt][qb];
+      }
+    }
+    // dV^T, dK^T tiles of this key block (contraction over the 64 queries = 2 k-steps)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int key = kb + 16 * kt + j;
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        float4_t v4 = float4_t{0.f, 0.f, 0.f, 0.f}, k4 = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          v4 = MFMA16(ot[dt][qb], pb[kt][qb], v4);
+          k4 = MFMA16(qt[dt][qb], dsb[kt][qb], k4);
+        }
+        if (key < n1) {
+          const int d = 16 * dt + 4 * g;
+          uint2 uv, uk;
+          uv.x = (uint32_t)f2bf(v4[0]) | ((uint32_t)f2bf(v4[1]) << 16);
+          uv.y = (uint32_t)f2bf(v4[2]) | ((uint32_t)f2bf(v4[3]) << 16);
+          uk.x = (uint32_t)f2bf(k4[0] * a.scale) | ((uint32_t)f2bf(k4[1] * a.scale) << 16);
+          uk.y = (uint32_t)f2bf(k4[2] * a.scale) | ((uint32_t)f2bf(k4[3] * a.scale) << 16);
+          *reinterpret_cast<uint2*>(dV + (long)key * a.lddkv + d) = uv;
+          *reinterpret_cast<uint2*>(dK + (long)key * a.lddkv + d) = uk;
+        }
+      }
+    }
+    lds_wave_sync();
+    // dQ^T[d][q] += sum_key K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt) {
+      const bf16x8_t ka = frag_tr(sk, LDD, 16 * dt, 0, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) dq[dt][nt] = MFMA16(ka, frag_tr(ss, LDQ, 16 * nt, 0, lane), dq[dt][nt]);
+    }
+    lds_wave_sync();
+  }
+  const long base = ((long)bh * a.nchunk + chunk) * NQ;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int q = 16 * nt + j;
+    if (q >= NQ) continue;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+      *reinterpret_cast<float4*>(a.ws + (base + q) * DH + 16 * dt + 4 * g) =
+          make_float4(dq[dt][nt][0] * a.scale, dq[dt][nt][1] * a.scale, dq[dt][nt][2] * a.scale,
+                      dq[dt][nt][3] * a.scale);
+  }
+}
+#undef MFMA16
+
 unsigned grid_for(long n) { return (unsigned)min((long)8192, max(1L, (n + 255) / 256)); }
 
 template <typename F8, typename F32>
@@ -508,7 +860,7 @@ int dispatch(int dtype, F8 f8, F32 f32) {
 extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, const void* x, long ldx, void* y,
                                       long ldy, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (C <= 2048 && vec_ok(C, x, ldx)) {
+  if (!(scalar_resize_mask() & 4) && C <= 2048 && vec_ok(C, x, ldx)) {
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,
@@ -543,7 +895,7 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, const void* dy, long lddy, void* dx,
                                       long lddx, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (vec_ok(C, dy, lddy) && vec_ok(C, dx, lddx)) {
+  if (!(scalar_resize_mask() & 8) && vec_ok(C, dy, lddy) && vec_ok(C, dx, lddx)) {
     const unsigned gv = grid_for((long)B * H * W * (C / 8));
     return dispatch(
         dtype,
@@ -578,7 +930,7 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* x, long ldx,
                                 void* y, long ldy, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (vec_ok(C, x, ldx) && vec_ok(C, y, ldy)) {
+  if (!(scalar_resize_mask() & 1) && vec_ok(C, x, ldx) && vec_ok(C, y, ldy)) {
     const unsigned gv = grid_for((long)B * Ho * Wo * (C / 8));
     return dispatch(
         dtype,
@@ -615,7 +967,7 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   hipStream_t s = (hipStream_t)stream;
   // taps per axis: ~2 * out/in + 3 must fit the block's LDS lists
   const bool taps_fit = 2 * (Ho / Hi) + 6 <= BL_MAXT && 2 * (Wo / Wi) + 6 <= BL_MAXT && Ho >= Hi && Wo >= Wi;
-  if (C <= 2048 && taps_fit && vec_ok(C, dy, lddy) && (uintptr_t)dx % 4 == 0) {
+  if (!(scalar_resize_mask() & 2) && C <= 2048 && taps_fit && vec_ok(C, dy, lddy) && (uintptr_t)dx % 4 == 0) {
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,
@@ -649,6 +1001,29 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
 
 static int nchunks(int N) { return (N + NC - 1) / NC; }
 
+// bf16 MFMA path: head dim a multiple of 16 (<= 48), 16-byte aligned rows
+static bool attn_mfma_ok(int dtype, int dh, const void* const* ptrs, const long* lds, int n) {
+  if (dtype != DFM_BF16 || !(dh == 16 || dh == 32 || dh == 48)) return false;
+  for (int i = 0; i < n; ++i)
+    if ((uintptr_t)ptrs[i] % 16 != 0 || lds[i] % 8 != 0) return false;
+  return true;
+}
+static int attn_kpw(int N) { return N >= 2048 ? 128 : 64; }  // keys per wave (a multiple of 32 and of NC)
+
+template <int DH>
+static void attn_mfma_launch(AttnArgs& a, bool bwd, hipStream_t s) {
+  const int kpw = attn_kpw(a.N);
+  const int groups = (a.nchunk + 3) / 4;
+  const dim3 grid((unsigned)(a.B * a.heads * groups));
+  if (bwd) hipLaunchKernelGGL(attn_bwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
+  else hipLaunchKernelGGL(attn_fwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
+}
+static void attn_mfma(AttnArgs& a, bool bwd, hipStream_t s) {
+  if (a.dh == 16) attn_mfma_launch<16>(a, bwd, s);
+  else if (a.dh == 32) attn_mfma_launch<32>(a, bwd, s);
+  else attn_mfma_launch<48>(a, bwd, s);
+}
+
 extern "C" size_t dfm_pooled_attn_workspace(int B, int heads, int N, int dh) {
   const long nchk = nchunks(N);
   return (size_t)B * heads * nchk * NQ * (dh + 2) * sizeof(float);
@@ -663,6 +1038,18 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
   a.B = B; a.heads = heads; a.N = N; a.dh = dh; a.nchunk = nchunks(N);
   a.q = q; a.ldq = ldq; a.k = k; a.v = v; a.ldkv = ldkv; a.scale = scale; a.o = o; a.ldo = ldo; a.lse = lse;
   a.ws = (float*)workspace;
+  {
+    const void* ptrs[] = {q, k, v, o};
+    const long lds_[] = {ldq, ldkv, ldkv, ldo};
+    if (attn_mfma_ok(dtype, dh, ptrs, lds_, 4)) {
+      a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
+      attn_mfma(a, false, s);
+      DFM_LAUNCH_CHECK();
+      hipLaunchKernelGGL(attn_fwd_combine_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      DFM_LAUNCH_CHECK();
+      return DFM_OK;
+    }
+  }
   const int DP = dh + 1;
   const size_t lds = (size_t)(NQ * DP + 2 * NC * DP + NQ * (NC + 1)) * sizeof(float);
   const unsigned nblk = B * heads * a.nchunk;
@@ -697,6 +1084,18 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
   a.q = q; a.ldq = ldq; a.k = k; a.v = v; a.ldkv = ldkv; a.scale = scale; a.o = const_cast<void*>(o); a.ldo = ldo; a.lse = (float*)lse;
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddkv = lddkv;
   a.ws = (float*)workspace;
+  {
+    const void* ptrs[] = {q, k, v, o, dout, dq, dk, dv};
+    const long lds_[] = {ldq, ldkv, ldkv, ldo, lddo, ldq, lddkv, lddkv};
+    if (attn_mfma_ok(dtype, dh, ptrs, lds_, 8)) {
+      a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
+      attn_mfma(a, true, s);
+      DFM_LAUNCH_CHECK();
+      hipLaunchKernelGGL(attn_dq_reduce_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      DFM_LAUNCH_CHECK();
+      return DFM_OK;
+    }
+  }
   const int DP = dh + 1;
   const size_t lds = (size_t)(2 * NQ * DP + 2 * NC * DP + NQ * (NC + 1) + 2 * NQ) * sizeof(float);
   const unsigned nblk = B * heads * a.nchunk;

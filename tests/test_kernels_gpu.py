@@ -263,7 +263,28 @@ def test_bilinear(dt, hi, ho):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("B,heads,N,dh", [(2, 2, 300, 32), (1, 4, 1200, 32), (2, 1, 37, 16), (1, 2, 150, 48),
+@pytest.mark.parametrize("hi,ho,C", [((12, 16), (24, 32), 64), ((6, 8), (24, 32), 128), ((7, 7), (60, 80), 64),
+                                     ((30, 40), (60, 80), 512)])
+def test_bilinear_strided(dt, hi, ho, C):
+    """Column-slice views on both sides (the decoders' resize+concat and its backward)."""
+    k = K()
+    B = 2
+    xb = torch.randn(B * hi[0] * hi[1], C + 24, device=DEV).to(dt)
+    x = xb[:, 16:16 + C]
+    yb = torch.zeros(B * ho[0] * ho[1], C + 40, device=DEV).to(dt)
+    k.bilinear(x, hi, ho, B, out=yb[:, 32:32 + C])
+    xr = x.float().reshape(B, *hi, C).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    ref = F.interpolate(xr, ho, mode="bilinear", align_corners=False)
+    assert rel(yb[:, 32:32 + C].float().view(B, *ho, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    dyb = torch.randn(B * ho[0] * ho[1], C + 8, device=DEV).to(dt)
+    dy = dyb[:, 8:]
+    ref.backward(dy.float().reshape(B, *ho, C).permute(0, 3, 1, 2))
+    dx = k.bilinear_bwd(dy, hi, ho, B)
+    assert rel(dx.float().view(B, *hi, C).permute(0, 3, 1, 2), xr.grad) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,heads,N,dh",[(2, 2, 300, 32), (1, 4, 1200, 32), (2, 1, 37, 16), (1, 2, 150, 48),
                                          (2, 4, 99, 36)])
 def test_pooled_attention(dt, B, heads, N, dh):
     k = K()
