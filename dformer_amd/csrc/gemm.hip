@@ -54,8 +54,8 @@ template <typename T> struct Mf;
 template <> struct Mf<bf16_t> {
   static constexpr int VEC = 8;    // elements per 16-byte vector
   static constexpr int KSTEP = 32; // k per MFMA
-  static constexpr int PADK = 8;   // k-contiguous row pad (elements)
-  static constexpr int PADR = 8;   // row-contiguous row pad (elements)
+  static constexpr int PADK = 16;  // k-contiguous row pad: rows 160 B apart, conflict-free ds_read_b128 fragments
+  static constexpr int PADR = 0;   // row-contiguous rows: no pad, 16-byte chunks XOR-swizzled (tr_swz)
 };
 template <> struct Mf<float> {
   static constexpr int VEC = 4;
@@ -198,6 +198,17 @@ DFM_INLINE void patch_ones(uint4* regs, int r0, int ones_r) {
   }
 }
 
+// XOR swizzle of the 16-byte chunks of row k of a row-contiguous bf16 LDS tile (R elements per
+// row, no pad): the 8 rows one ds_read_b64_tr_b16 lane group reads (k0 + 8g + q, g < 2, q < 4)
+// land on 16 distinct 4-bank slots instead of 2-way conflicting, and the 8 consecutive lanes of a
+// ds_write_b128 still hit distinct banks.
+template <int R>
+DFM_INLINE int tr_swz(int k) {
+  if constexpr (R >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else if constexpr (R == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  else return 2 * ((k >> 3) & 1);
+}
+
 template <typename T, int R, int BK, bool KC, int NT>
 DFM_INLINE void stage_store(const uint4* regs, T* lds) {
   using G = TileGeom<T, R, BK, KC, NT>;
@@ -211,7 +222,10 @@ DFM_INLINE void stage_store(const uint4* regs, T* lds) {
       *reinterpret_cast<uint4*>(lds + r * G::LD + kc) = regs[i];
     } else {
       const int k = v / (R / VEC), rc = (v % (R / VEC)) * VEC;
-      *reinterpret_cast<uint4*>(lds + k * G::LD + rc) = regs[i];
+      if constexpr (sizeof(T) == 2)
+        *reinterpret_cast<uint4*>(lds + k * G::LD + (((rc >> 3) ^ tr_swz<R>(k)) << 3)) = regs[i];
+      else
+        *reinterpret_cast<uint4*>(lds + k * G::LD + rc) = regs[i];
     }
   }
 }
@@ -225,8 +239,9 @@ DFM_INLINE bf16x8_t frag_bf16(const bf16_t* lds, int r0, int k0, int lane) {
   } else {
     const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
     typedef __attribute__((address_space(3))) short4_t lds_s4;
-    const bf16_t* a0 = lds + (k0 + 8 * g + q) * LD + r0 + 4 * p;
-    const bf16_t* a1 = a0 + 4 * LD;
+    const int k = k0 + 8 * g + q, r = r0 + 4 * p;  // LD == R (PADR = 0): swizzled 16-byte chunks
+    const bf16_t* a0 = lds + k * LD + ((((r >> 3) ^ tr_swz<LD>(k)) << 3) | (r & 7));
+    const bf16_t* a1 = lds + (k + 4) * LD + ((((r >> 3) ^ tr_swz<LD>(k + 4)) << 3) | (r & 7));
     short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0));
     short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a1));
     typedef __attribute__((ext_vector_type(8))) short short8_t;
