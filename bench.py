@@ -79,7 +79,7 @@ def roofline_of(probe):
             traffic = rec.get("traffic_bytes_per_launch")
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": f"gemm_kernel bf16 ConvFFN fc2 stage0 (M={M},K={Kd},N={N}), fused bias+residual epilogue",
+            "kernel": f"gemm_stream_kernel bf16 ConvFFN fc2 stage0 (M={M},K={Kd},N={N}), fused bias+residual epilogue",
             "launches": len(probe.events), "avg_us": round(us, 2), "bytes_per_launch": nbytes,
             "tflops": round(flops / (us * 1e-6) / 1e12, 1)}
 

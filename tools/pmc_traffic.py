@@ -16,10 +16,10 @@ def per_launch(d, counter):
     for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "gemm_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if "gemm_" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     if not vals:
-        raise SystemExit(f"no {counter} rows for gemm_kernel under {d}")
+        raise SystemExit(f"no {counter} rows for a gemm kernel under {d}")
     return statistics.median(vals), len(vals)
 
 
@@ -31,7 +31,7 @@ def main():
     fetch = 2 * fetch_kib * 1024
     write = write_kib * 1024
     algo = 2 * (M * Kd + N * Kd + 3 * M * N)
-    rec = {"key": [M, N, Kd, 1, 1], "kernel": "gemm_kernel bf16 fc2 stage0 (fused bias+residual epilogue)",
+    rec = {"key": [M, N, Kd, 1, 1], "kernel": "gemm_stream_kernel bf16 fc2 stage0 (persistent M-streaming, fused bias+residual epilogue)",
            "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib, "launches": [nf, nw],
            "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
            "traffic_bytes_per_launch": fetch + write, "algorithmic_bytes_per_launch": algo,
