@@ -324,6 +324,194 @@ __global__ __launch_bounds__(256) void dw_tile_wgrad_kernel(int B, int H, int W,
   }
 }
 
+// ---------------------------------------------------------------- row-streaming 3x3 weight gradient
+// (8-byte lane vectors: 4 bf16 / 2 fp32 channels per lane keep the register window + 10 tap
+// accumulators at ~130 VGPRs, 3 waves per SIMD; a wave still reads 512 contiguous bytes per load)
+// The tiled kernel above reduces one LDS tile per block visit; on the small-spatial, wide-channel
+// stages (30x40 / 15x20 with 1024-2048 hidden channels) a block sees a single tile and the
+// staging, the strip-major LDS reads (bank conflicts) and the per-block reduction dominate. Here a
+// lane owns one 16-byte channel vector and a TW-column strip and walks down a chunk of RC rows,
+// keeping the three input rows its taps touch in registers (one new input row and one dy row per
+// output row, loaded one row ahead so the next loads are in flight during the FMAs). A wave's
+// lanes cover consecutive channel vectors of one pixel (a contiguous 1 KB line at C=512), so every
+// load is coalesced and each element of x and dy is fetched once from HBM (the two halo columns
+// and halo rows between neighbouring strips / chunks come from L2). The 9 taps + bias of all the
+// units a block visits stay in registers; one LDS reduction per block writes the block's partial
+// [blockIdx.x][C][10]; partial_sum_kernel sums them in fixed order (deterministic).
+constexpr int W3_TW = 4;
+
+struct W3Geom {
+  int LPU, UPW, slices, nstrips, nchunks, RC;
+  long units, nsb;
+};
+
+__host__ __device__ inline long w3_units(int B, int nstrips, int nchunks) { return (long)B * nstrips * nchunks; }
+
+template <typename T> struct W3Cfg { static constexpr int EPL = 8 / sizeof(T); };
+
+template <typename T>
+W3Geom w3_geom(int B, int H, int W, int C) {
+  constexpr int CPT = W3Cfg<T>::EPL;
+  W3Geom g;
+  const int G = C / CPT;
+  g.LPU = std::min(64, G);
+  g.UPW = 64 / g.LPU;
+  g.slices = (G + g.LPU - 1) / g.LPU;
+  g.nstrips = (W + W3_TW - 1) / W3_TW;
+  // ~3072 waves in flight (12 per CU at this kernel's register budget): split the rows into chunks
+  // of at least 4 until the units fill them
+  const long target_waves = 3072;
+  long want = (target_waves * g.UPW + (long)B * g.nstrips * g.slices - 1) / ((long)B * g.nstrips * g.slices);
+  want = std::max(1L, std::min(want, (long)(H + 3) / 4));
+  g.RC = (int)((H + want - 1) / want);
+  g.nchunks = (H + g.RC - 1) / g.RC;
+  g.units = w3_units(B, g.nstrips, g.nchunks);
+  const long waves = (g.units + g.UPW - 1) / g.UPW;
+  g.nsb = std::max(1L, (waves + 3) / 4);
+  return g;
+}
+
+template <typename T>
+DFM_INLINE uint2 w3_ld(const T* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint2*>(p) : make_uint2(0, 0);
+}
+
+template <typename T>
+DFM_INLINE void w3_unpack(uint2 q, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  } else {
+    v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dw3_stream_wgrad_kernel(int B, int H, int W, int C, int RC, int nstrips,
+                                                               int nchunks, int LPU, int UPW,
+                                                               const T* __restrict__ x, long ldx,
+                                                               const T* __restrict__ dy, long lddy,
+                                                               float* __restrict__ part) {
+  constexpr int CPT = W3Cfg<T>::EPL, TW = W3_TW, NX = TW + 2, NV = 10 * CPT, VCH = 20;
+  __shared__ float red[4][VCH][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lg = lane % LPU, usub = lane / LPU;
+  const int G = C / CPT, cg = blockIdx.y * LPU + lg;
+  const bool valid = usub < UPW && cg < G;
+  const int c0 = cg * CPT;
+  const long units = w3_units(B, nstrips, nchunks);
+
+  float acc[10][CPT];
+#pragma unroll
+  for (int a = 0; a < 10; ++a)
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) acc[a][e] = 0.f;
+
+  const long stride = (long)gridDim.x * 4 * UPW;
+  for (long u = ((long)blockIdx.x * 4 + wave) * UPW + usub; valid && u < units; u += stride) {
+    const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
+    const long b = u / ((long)nstrips * nchunks);
+    const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
+    const long img = b * H * W;
+    auto load_x = [&](int h, uint2* r) {
+      const bool hok = h >= 0 && h < H;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        const int w = w0 - 1 + q;
+        r[q] = w3_ld<T>(x + (img + (long)h * W + w) * ldx + c0, hok && w >= 0 && w < W);
+      }
+    };
+    auto load_dy = [&](int h, uint2* r) {
+      const bool hok = h < h1;
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int w = w0 + t;
+        r[t] = w3_ld<T>(dy + (img + (long)h * W + w) * lddy + c0, hok && w < W);
+      }
+    };
+    uint2 x0[NX], x1[NX], x2[NX], dc[TW];
+    load_x(h0 - 1, x0);
+    load_x(h0, x1);
+    load_x(h0 + 1, x2);
+    load_dy(h0, dc);
+    for (int h = h0; h < h1; ++h) {
+      uint2 xn[NX], dn[TW];
+      load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
+      load_dy(h + 1, dn);
+      float gv[TW][CPT];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        w3_unpack<T>(dc[t], gv[t]);
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) acc[9][e] += gv[t][e];
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const uint2* xr = a == 0 ? x0 : (a == 1 ? x1 : x2);
+#pragma unroll
+        for (int q = 0; q < NX; ++q) {
+          float xv[CPT];
+          w3_unpack<T>(xr[q], xv);
+          // input column q feeds output column t with tap j = q - t
+#pragma unroll
+          for (int t = 0; t < TW; ++t) {
+            const int j = q - t;
+            if (j < 0 || j >= 3) continue;
+#pragma unroll
+            for (int e = 0; e < CPT; ++e) acc[a * 3 + j][e] = fmaf(gv[t][e], xv[e], acc[a * 3 + j][e]);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        x0[q] = x1[q];
+        x1[q] = x2[q];
+        x2[q] = xn[q];
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t) dc[t] = dn[t];
+    }
+  }
+
+  // block reduction over the 4 waves and the UPW units of a wave that share a channel vector
+  const long pbase = (long)blockIdx.x * C * 10;
+#pragma unroll
+  for (int vc = 0; vc < NV; vc += VCH) {
+    if (vc) __syncthreads();
+#pragma unroll
+    for (int v = 0; v < VCH; ++v)
+      if (vc + v < NV) red[wave][v][lane] = acc[(vc + v) / CPT][(vc + v) % CPT];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < VCH * LPU; idx += 256) {
+      const int v = idx / LPU, l = idx % LPU, V = vc + v;
+      const int c = (blockIdx.y * LPU + l) * CPT + V % CPT;
+      if (V >= NV || c >= C) continue;
+      float sum = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int us = 0; us < UPW; ++us) sum += red[w][v][us * LPU + l];
+      const int tap = V / CPT;  // 0..8 = kernel row * 3 + col, 9 = bias
+      part[pbase + (long)c * 10 + tap] = sum;
+    }
+  }
+}
+
+template <typename T>
+long w3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
+               hipStream_t s) {
+  const W3Geom g = w3_geom<T>(B, H, W, C);
+  hipLaunchKernelGGL(dw3_stream_wgrad_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H,
+                     W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, part);
+  return g.nsb;
+}
+
+static bool w3_enabled() {  // DFM_DW_WG3=0 selects the LDS-tiled 3x3 weight gradient (A/B)
+  static const bool on = [] {
+    const char* e = getenv("DFM_DW_WG3");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 template <typename T>
 bool dw_aligned(int C, const void* p, long ld) {
   constexpr int CPT = DwCfg<T>::CPT;
@@ -464,7 +652,9 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
 
 extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k) {
   long nsb = 1;
-  if (k == 3) nsb = std::max(wgrad_nsb_any<float, 3>(B, H, W, C), wgrad_nsb_any<bf16_t, 3>(B, H, W, C));
+  if (k == 3)
+    nsb = std::max({wgrad_nsb_any<float, 3>(B, H, W, C), wgrad_nsb_any<bf16_t, 3>(B, H, W, C),
+                    w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb});
   else if (k == 7) nsb = std::max(wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C));
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);
 }
@@ -481,11 +671,13 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
     nsb = k == 7 ? wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                 : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+          : w3_enabled() ? w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                         : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
     nsb = k == 7 ? wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                 : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+          : w3_enabled() ? w3_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                         : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else {
     dfm_set_error("dfm_dwconv_bwd_weight: bad dtype");
     return DFM_ERR_DTYPE;
