@@ -504,6 +504,138 @@ long w3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* 
   return g.nsb;
 }
 
+// ---------------------------------------------------------------- row-streaming 7x7 weight gradient
+// Same lane/strip/chunk walk as the 3x3 kernel, but the 49 taps x 4 channels would not fit in
+// registers, so each block owns one kernel row i (7 taps + the bias from i == 0) and streams the
+// input row h+i-3 next to dy row h. The seven blocks of one spatial block are consecutive in the
+// XCD-remapped order, so they run together on one XCD and their x / dy re-reads hit its L2.
+template <typename T>
+W3Geom w7_geom(int B, int H, int W, int C) {
+  constexpr int CPT = W3Cfg<T>::EPL;
+  W3Geom g;
+  const int G = C / CPT;
+  g.LPU = std::min(64, G);
+  g.UPW = 64 / g.LPU;
+  g.slices = (G + g.LPU - 1) / g.LPU;
+  g.nstrips = (W + W3_TW - 1) / W3_TW;
+  const long target_waves = 4096 / 7;  // per kernel row: ~16 waves per CU over the 7 rows
+  long want = (target_waves * g.UPW + (long)B * g.nstrips * g.slices - 1) / ((long)B * g.nstrips * g.slices);
+  want = std::max(1L, std::min(want, (long)(H + 3) / 4));
+  g.RC = (int)((H + want - 1) / want);
+  g.nchunks = (H + g.RC - 1) / g.RC;
+  g.units = w3_units(B, g.nstrips, g.nchunks);
+  const long waves = (g.units + g.UPW - 1) / g.UPW;
+  g.nsb = std::max(1L, (waves + 3) / 4);
+  return g;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dw7_stream_wgrad_kernel(int B, int H, int W, int C, int RC, int nstrips,
+                                                               int nchunks, int LPU, int UPW, int nsb,
+                                                               const T* __restrict__ x, long ldx,
+                                                               const T* __restrict__ dy, long lddy,
+                                                               float* __restrict__ part) {
+  constexpr int CPT = W3Cfg<T>::EPL, TW = W3_TW, K = 7, NX = TW + K - 1, NV = (K + 1) * CPT;
+  __shared__ float red[4][NV][64];
+  const long l = xcd_remap(blockIdx.x, (long)gridDim.x);
+  const int sb = (int)(l / K), i = (int)(l % K);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lg = lane % LPU, usub = lane / LPU;
+  const int G = C / CPT, cg = blockIdx.y * LPU + lg;
+  const bool valid = usub < UPW && cg < G;
+  const int c0 = cg * CPT;
+  const long units = w3_units(B, nstrips, nchunks);
+
+  float acc[K + 1][CPT];
+#pragma unroll
+  for (int a = 0; a <= K; ++a)
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) acc[a][e] = 0.f;
+
+  const long stride = (long)nsb * 4 * UPW;
+  for (long u = ((long)sb * 4 + wave) * UPW + usub; valid && u < units; u += stride) {
+    const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
+    const long b = u / ((long)nstrips * nchunks);
+    const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
+    const long img = b * H * W;
+    auto load = [&](int h, uint2* xr, uint2* dr) {  // x row h+i-3 and dy row h (zeros past the chunk)
+      const int hx = h + i - K / 2;
+      const bool hok = h < h1 && hx >= 0 && hx < H;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        const int w = w0 - K / 2 + q;
+        xr[q] = w3_ld<T>(x + (img + (long)hx * W + w) * ldx + c0, hok && w >= 0 && w < W);
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int w = w0 + t;
+        dr[t] = w3_ld<T>(dy + (img + (long)h * W + w) * lddy + c0, h < h1 && w < W);
+      }
+    };
+    uint2 xc[NX], dc[TW];
+    load(h0, xc, dc);
+    for (int h = h0; h < h1; ++h) {
+      uint2 xn[NX], dn[TW];
+      load(h + 1, xn, dn);
+      float gv[TW][CPT];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        w3_unpack<T>(dc[t], gv[t]);
+#pragma unroll
+        for (int e = 0; e < CPT; ++e) acc[K][e] += gv[t][e];
+      }
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        float xv[CPT];
+        w3_unpack<T>(xc[q], xv);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          const int j = q - t;
+          if (j < 0 || j >= K) continue;
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) acc[j][e] = fmaf(gv[t][e], xv[e], acc[j][e]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NX; ++q) xc[q] = xn[q];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) dc[t] = dn[t];
+    }
+  }
+
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[wave][v][lane] = acc[v / CPT][v % CPT];
+  __syncthreads();
+  const long pbase = (long)sb * C * (K * K + 1);
+  for (int idx = threadIdx.x; idx < NV * LPU; idx += 256) {
+    const int v = idx / LPU, lq = idx % LPU, tap = v / CPT;
+    const int c = (blockIdx.y * LPU + lq) * CPT + v % CPT;
+    if (c >= C || (tap == K && i != 0)) continue;
+    float sum = 0.f;
+    for (int w = 0; w < 4; ++w)
+      for (int us = 0; us < UPW; ++us) sum += red[w][v][us * LPU + lq];
+    part[pbase + (long)c * (K * K + 1) + (tap < K ? i * K + tap : K * K)] = sum;
+  }
+}
+
+template <typename T>
+long w7_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
+               hipStream_t s) {
+  const W3Geom g = w7_geom<T>(B, H, W, C);
+  hipLaunchKernelGGL(dw7_stream_wgrad_kernel<T>, dim3((unsigned)(g.nsb * 7), (unsigned)g.slices), dim3(256), 0, s,
+                     B, H, W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (int)g.nsb, (const T*)x, ldx,
+                     (const T*)dy, lddy, part);
+  return g.nsb;
+}
+
+static bool w7_enabled() {  // DFM_DW_WG7=0 selects the LDS-tiled 7x7 weight gradient (A/B)
+  static const bool on = [] {
+    const char* e = getenv("DFM_DW_WG7");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static bool w3_enabled() {  // DFM_DW_WG3=0 selects the LDS-tiled 3x3 weight gradient (A/B)
   static const bool on = [] {
     const char* e = getenv("DFM_DW_WG3");
@@ -655,7 +787,9 @@ extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, in
   if (k == 3)
     nsb = std::max({wgrad_nsb_any<float, 3>(B, H, W, C), wgrad_nsb_any<bf16_t, 3>(B, H, W, C),
                     w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb});
-  else if (k == 7) nsb = std::max(wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C));
+  else if (k == 7)
+    nsb = std::max({wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C),
+                    w7_geom<float>(B, H, W, C).nsb, w7_geom<bf16_t>(B, H, W, C).nsb});
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);
 }
 
@@ -670,12 +804,14 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   long nsb;
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
+    nsb = k == 7 ? (w7_enabled() ? w7_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                 : wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s)
+    nsb = k == 7 ? (w7_enabled() ? w7_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                 : wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else {
