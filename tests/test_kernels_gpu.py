@@ -179,7 +179,7 @@ def test_layernorm_views_accumulate(dt, C):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("ks,ident", [(7, False), (3, True)])
-@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16), (1, 33, 41, 40)])
 def test_dwconv(dt, ks, ident, B, H, W, C):
     k = K()
     x = torch.randn(B, H, W, C, device=DEV).to(dt)
@@ -203,7 +203,7 @@ def test_dwconv(dt, ks, ident, B, H, W, C):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("ks", [3, 7])
-@pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 80), (1, 9, 70, 32), (3, 33, 5, 24)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 80), (1, 9, 70, 32), (3, 33, 5, 24), (2, 37, 29, 24)])
 def test_dwconv_strided_gelu_accumulate(dt, ks, B, H, W, C):
     """Column-slice views (row stride > C), the fused GELU second output and accumulate=True."""
     k = K()
