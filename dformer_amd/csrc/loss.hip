@@ -28,7 +28,8 @@ DFM_INLINE void src_idx(int dst, int in, int out, int& i0, int& i1, float& l1) {
 
 // z[c] for c < ncls (others -inf); returns the logit of class `lab` through a predicated select
 template <typename T>
-DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float (&z)[MAXC]) {
+DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float (&z)[MAXC],
+                       bool vec) {
   int h0, h1, w0, w1;
   float lh, lw;
   src_idx(y, h, H, h0, h1, lh);
@@ -38,6 +39,26 @@ DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x,
   const T* p10 = lg + (((long)b * h + h1) * w + w0) * ncls;
   const T* p11 = lg + (((long)b * h + h1) * w + w1) * ncls;
   const float a00 = (1.f - lh) * (1.f - lw), a01 = (1.f - lh) * lw, a10 = lh * (1.f - lw), a11 = lh * lw;
+  if constexpr (sizeof(T) == 2) {
+    if (vec) {  // 16-byte rows of 8 classes: 4 vector loads per 8 classes instead of 32 scalar ones
+#pragma unroll
+      for (int v = 0; v < MAXC / 8; ++v) {
+        if (v * 8 < ncls) {
+          float f00[8], f01[8], f10[8], f11[8];
+          ld8<T>(p00 + v * 8, f00);
+          ld8<T>(p01 + v * 8, f01);
+          ld8<T>(p10 + v * 8, f10);
+          ld8<T>(p11 + v * 8, f11);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) z[v * 8 + e] = a00 * f00[e] + a01 * f01[e] + a10 * f10[e] + a11 * f11[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) z[v * 8 + e] = -INFINITY;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
     z[c] = c < ncls ? a00 * ldf(p00 + c) + a01 * ldf(p01 + c) + a10 * ldf(p10 + c) + a11 * ldf(p11 + c) : -INFINITY;
@@ -48,12 +69,13 @@ __global__ __launch_bounds__(256) void seg_loss_fwd_kernel(int B, int h, int w, 
                                                            int H, int W, const long* __restrict__ label, int ignore,
                                                            float* __restrict__ lse_out, float* __restrict__ part) {
   const long n = (long)B * H * W;
+  const bool vec = ncls % 8 == 0 && ((uintptr_t)lg & 15) == 0;
   float s = 0.f, cnt = 0.f;
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < n; p += (long)gridDim.x * blockDim.x) {
     const int x = p % W, y = (p / W) % H, b = p / ((long)W * H);
     const long lab = label[p];
     float z[MAXC];
-    interp(lg, b, h, w, ncls, y, x, H, W, z);
+    interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
     float m = -INFINITY, zl = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -113,6 +135,7 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
   const int y0 = ty * TY, x0 = tx * TX;
   const int ny = min(TY, H - y0), nx = min(TX, W - x0);
   const float inv = (gscale ? gscale[0] : 1.f) / fmaxf(loss_out[1], 1.f);
+  const bool vec = ncls % 8 == 0 && ((uintptr_t)lg & 15) == 0;
   // phase 1: per-pixel d loss / d upsampled logits
   {
     const int py = threadIdx.x / TX, px = threadIdx.x % TX;
@@ -123,7 +146,7 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
     const bool valid = lab != ignore && lab >= 0 && lab < ncls;
     if (valid) {
       float z[MAXC];
-      interp(lg, b, h, w, ncls, y, x, H, W, z);
+      interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
       float m = -INFINITY;
 #pragma unroll
       for (int c = 0; c < MAXC; ++c) m = fmaxf(m, z[c]);

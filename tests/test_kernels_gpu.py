@@ -383,7 +383,7 @@ def test_nmf_update_softmax():
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (1, 17, 23, 67, 92, 37), (2, 8, 12, 64, 96, 40)])
+@pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (1, 17, 23, 67, 92, 37), (2, 8, 12, 64, 96, 40), (1, 30, 40, 37, 50, 19), (1, 13, 11, 100, 90, 16)])
 def test_seg_loss(dt, B, h, w, H, W, ncls):
     k = K()
     lg = torch.randn(B, h, w, ncls, device=DEV).to(dt)
