@@ -179,7 +179,10 @@ def test_layernorm_views_accumulate(dt, C):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("ks,ident", [(7, False), (3, True)])
-@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16), (1, 33, 41, 40)])
+# (1, 9, 10, 520) / (1, 33, 34, 520): channel vectors not a multiple of the 64-lane slice of the
+# row-streaming kernels (partial last slice), the latter also on the streaming 3x3 forward's planes
+@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16), (1, 33, 41, 40),
+                                     (1, 9, 10, 520), (1, 33, 34, 520)])
 def test_dwconv(dt, ks, ident, B, H, W, C):
     k = K()
     x = torch.randn(B, H, W, C, device=DEV).to(dt)
