@@ -52,6 +52,77 @@ __global__ __launch_bounds__(256) void colred_kernel(long rows, int C, const T* 
   }
 }
 
+// Narrow-row variant (C/V lanes per row, V = one 16-byte vector of channels per lane, 256/(C/V)
+// rows per pass): the scalar kernel above idles most of its 64 column lanes and issues 2-byte
+// loads when C is 16..64 (the stem BatchNorms: 1.2M rows x 16/32 channels). Same partial layout.
+template <typename T>
+DFM_INLINE void ldvec(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    ld8<T>(p, v);
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const T* __restrict__ x, long ldx,
+                                                         const T* __restrict__ y, long ldy,
+                                                         const float* __restrict__ p0, const float* __restrict__ p1,
+                                                         long rps, float* __restrict__ part, int nblk) {
+  constexpr int NOUT = MODE == 0 ? 1 : 2, V = 16 / sizeof(T);
+  __shared__ float red[NOUT][256][V + 1];
+  const int G = C / V, RL = 256 / G;
+  const int g = threadIdx.x % G, rl = threadIdx.x / G, c0 = g * V;
+  const long per = (rows + nblk - 1) / nblk;
+  const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
+  float s0[V], s1[V], mu[V], rs[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    s0[e] = 0.f;
+    s1[e] = 0.f;
+    mu[e] = MODE == 2 ? p0[c0 + e] : 0.f;
+    rs[e] = MODE == 2 ? p1[c0 + e] : 0.f;
+  }
+  for (long r = r0 + rl; r < r1; r += RL) {
+    float xv[V];
+    ldvec<T>(x + r * ldx + c0, xv);
+    if (MODE == 0) {
+      float yv[V];
+      if (y) ldvec<T>(y + r * ldy + c0, yv);
+      const float sc = p1 ? p1[r / rps] : 1.f;
+#pragma unroll
+      for (int e = 0; e < V; ++e) s0[e] += (y ? xv[e] * yv[e] : xv[e]) * sc;
+    } else if (MODE == 1) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s0[e] += xv[e];
+        s1[e] += xv[e] * xv[e];
+      }
+    } else {
+      float gv[V];
+      ldvec<T>(y + r * ldy + c0, gv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s0[e] += gv[e];
+        s1[e] += gv[e] * (xv[e] - mu[e]) * rs[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    red[0][threadIdx.x][e] = s0[e];
+    if (NOUT == 2) red[NOUT - 1][threadIdx.x][e] = s1[e];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < NOUT * C; idx += 256) {
+    const int k = idx / C, c = idx % C, gg = c / V, e = c % V;
+    float v = 0.f;
+    for (int q = 0; q < RL; ++q) v += red[k][q * G + gg][e];
+    part[((long)blockIdx.x * NOUT + k) * C + c] = v;
+  }
+}
+
 __global__ void colred_sum_kernel(int nblk, int n, const float* __restrict__ part, float* __restrict__ out,
                                   int accumulate) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -68,8 +139,16 @@ int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, c
            long rps, float* out, int accumulate, void* ws, hipStream_t s) {
   constexpr int NOUT = MODE == 0 ? 1 : 2;
   const int nblk = red_blocks(rows);
-  hipLaunchKernelGGL((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x, ldx,
-                     (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
+  constexpr int V = 16 / sizeof(T);
+  const int G = C / V;
+  const bool vec = C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
+                   (!y || (ldy % V == 0 && ((uintptr_t)y & 15) == 0));
+  if (vec)
+    hipLaunchKernelGGL((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
+                       (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
+  else
+    hipLaunchKernelGGL((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x,
+                       ldx, (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
   DFM_LAUNCH_CHECK();
   hipLaunchKernelGGL(partial_sum_kernel<0>, dim3(cdiv((long)NOUT * C, 64)), dim3(1024), 0, s, nblk, (long)NOUT * C,
                      (const float*)ws, out, (float*)nullptr, 0L, accumulate);

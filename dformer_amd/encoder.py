@@ -4,13 +4,16 @@ keys (Originofamonia/DFormer models/encoders/DFormer.py), computed by HIP kernel
 Layout: inside a stage the activations are NHWC rows in the compute dtype; the reference's
 Block.forward(x [B,H,W,C], x_e [B,H,W,C/2]) -> (x, x_e) surface is kept. nn.Linear / nn.Conv2d
 children are parameter containers only (their forward is never called on the hot path).
-The stems / stage downsampling (BN + conv3x3 s2, DFormer.py:194-228) run as channels-last
-PyTorch convolutions in round 1 (SURVEY.md §8f item 2 lists them as the next native target).
+The stems / stage downsampling (BN + conv3x3 s2, DFormer.py:194-228) run their 3x3 stride-2
+convolutions as channels-last PyTorch convolutions (SURVEY.md §8f item 2 lists them as the next
+native target); their BatchNorms run on the library's NHWC BN kernels (BNRowsFn).
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import kernels as K
+from .decoders import _allreduce, _world
 from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, invalidate_weights
 
 _EMPTY = {}
@@ -158,6 +161,51 @@ def _bn(c, syncbn):
     return nn.SyncBatchNorm(c) if syncbn else nn.BatchNorm2d(c)
 
 
+class BNRowsFn(torch.autograd.Function):
+    """BatchNorm2d / SyncBatchNorm (DFormer.py:219-228 stems and downsample layers) on a
+    channels-last NCHW tensor, computed as [B*H*W, C] rows by the library's BN kernels: batch
+    statistics + running-stat update in training (all-reduced for SyncBN), running stats in eval."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, bn, sync):
+        B, C, H, W = x.shape
+        xr = x.permute(0, 2, 3, 1).contiguous().view(-1, C)
+        rows = xr.shape[0]
+        if bn.training:
+            st = _allreduce(K.bn_stats(xr), sync)
+            count = rows * _world(sync)
+            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
+                                       bn.running_mean, bn.running_var)
+            bn.num_batches_tracked.add_(1)
+        else:
+            mean = bn.running_mean
+            rstd = torch.rsqrt(bn.running_var + bn.eps)
+            count = rows
+        y = K.bn_apply(xr, mean, rstd, gamma, beta)
+        ctx.save_for_backward(xr, mean, rstd, gamma)
+        ctx.sync, ctx.count, ctx.shape = sync, count, (B, C, H, W)
+        return y.view(B, H, W, C).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, mean, rstd, gamma = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        dyr = dy.permute(0, 2, 3, 1).contiguous().view(-1, C)
+        st2 = _allreduce(K.bn_bwd_stats(xr, dyr, mean, rstd), ctx.sync)
+        dx = K.bn_bwd_apply(xr, dyr, mean, rstd, gamma, st2, ctx.count)
+        return dx.view(B, H, W, C).permute(0, 3, 1, 2), st2[1].clone(), st2[0].clone(), None, None
+
+
+def _run_downsample(seq, x):
+    """nn.Sequential of the reference's downsample layer; its BatchNorms on BNRowsFn."""
+    for m in seq:
+        if isinstance(m, nn.modules.batchnorm._BatchNorm) and x.is_cuda:
+            x = BNRowsFn.apply(x, m.weight, m.bias, m, isinstance(m, nn.SyncBatchNorm))
+        else:
+            x = m(x)
+    return x
+
+
 class DFormer(nn.Module):
     """DFormer backbone (DFormer.py:184-305). forward(x, x_e) -> (outs[4] NCHW views, None) like the
     reference; outs are channels-last buffers in the compute dtype."""
@@ -224,8 +272,8 @@ class DFormer(nn.Module):
     def _downsample(self, i, x, e):
         dt = self.compute_dtype
         with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
-            x = self.downsample_layers[i](x)
-            e = self.downsample_layers_e[i](e)
+            x = _run_downsample(self.downsample_layers[i], x)
+            e = _run_downsample(self.downsample_layers_e[i], e)
         return x, e
 
     def forward(self, x, x_e):
