@@ -106,11 +106,19 @@ __global__ __launch_bounds__(256) void seg_loss_fwd_kernel(int B, int h, int w, 
   }
 }
 
+// one wave: lane l sums partials l, l+64, ... (both outputs), then a fixed-order wave reduction
+// (a single-thread serial sum over the 1024 partials cost ~80 us of dependent loads)
 __global__ void seg_loss_sum_kernel(int nblk, const float* __restrict__ part, float* __restrict__ out) {
-  if (threadIdx.x < 2) {
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[b * 2 + threadIdx.x];
-    out[threadIdx.x] = s;
+  float s0 = 0.f, s1 = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 64) {
+    s0 += part[b * 2];
+    s1 += part[b * 2 + 1];
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  if (threadIdx.x == 0) {
+    out[0] = s0;
+    out[1] = s1;
   }
 }
 
