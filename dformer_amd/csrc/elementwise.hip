@@ -1,6 +1,8 @@
 // Bandwidth-bound helpers: column reductions (bias / layer-scale grads, BatchNorm statistics),
 // activation backward, residual chain rule, dtype casts, NMF multiplicative updates and AdamW.
 // All reductions are two-stage with fixed order (deterministic, no float atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -141,7 +143,14 @@ int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, c
   const int nblk = red_blocks(rows);
   constexpr int V = 16 / sizeof(T);
   const int G = C / V;
-  const bool vec = C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
+  // DFM_COLRED_VEC=1 selects the vectorized narrow-row reduction. Off by default: its different fp32
+  // summation order shifts the one-pass BN variance (E[x²] - E[x]², cancellation-prone) enough to
+  // move the fp32 end-to-end input-gradient golden past its 1e-3 gate; needs shifted BN sums first.
+  static const bool vec_on = [] {
+    const char* e = getenv("DFM_COLRED_VEC");
+    return e && atoi(e) == 1;
+  }();
+  const bool vec = vec_on && C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
                    (!y || (ldy % V == 0 && ((uintptr_t)y & 15) == 0));
   if (vec)
     hipLaunchKernelGGL((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
