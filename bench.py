@@ -2,27 +2,72 @@
 """DFormer-Base + ham decoder, 480x640, bs=16 per GPU, bf16 training-step throughput (images/s).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL over xGMI)
+  (N > 1: one rank per GPU over RCCL/xGMI. Launched by torch.distributed.run it uses the
+  WORLD_SIZE/RANK/LOCAL_RANK it finds; started directly with --gpus N > 1 it re-launches itself
+  under torch.distributed.run as a child process before touching the GPU.)
 
 One step = forward + fused CE loss + backward (bucketed RCCL all-reduce overlapped) + fused AdamW,
-on synthetic inputs resident in HBM (BASELINE.json config 3 / 4). Rank 0 prints one JSON line with
-the whole-job images/s, the roofline of the dominant kernel and the CPU-oracle baseline.
+on synthetic inputs resident in HBM (BASELINE.json config 3 / 4). Rank 0 prints one JSON line:
+whole-job images/s over the K timed steps (barrier + synchronize on both sides, max over ranks),
+per-step median / p10 / p90, the roofline of the dominant kernel and of the whole step, and the
+CPU-oracle baseline.
+
+Measurement:
+  * census step (untimed, after warm-up): the library's launch tracer times every kernel it
+    launches with HIP events on the launching stream, and kernels.ACCOUNT charges every entry
+    point's algorithmic FLOPs / HBM bytes to the kernel it launched -> per-kernel table
+    (launches, F_k, B_k, ideal = sum max(F/P, B/BW), measured). The dominant kernel is the one with
+    the largest measured time; the table is written with --table-out.
+  * timed steps: only the dominant kernel's launches carry HIP events; its average duration over
+    the timed region gives roofline.achieved = algorithmic bytes (or FLOPs) per launch / duration.
+  * roofline.step: sum_k max(F_k/P, B_k/BW) over the census / ms_per_step; and SURVEY §8d's
+    fused-model bound for DFormer-B bs16 (4.33 TFLOP at the bf16 MFMA peak) / ms_per_step.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 METRIC = "images/s training-step, DFormer-B 480×640 bs=16/GPU, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-MFMA_BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}  # dense bf16 MFMA; f32-input MFMA (= vector rate)
+# SURVEY §8d: DFormer-B fwd 90.3 GFLOP/img, training step ~3x -> 4.33 TFLOP per bs-16 step
+SURVEY_TFLOP_PER_IMG = 4.33 / 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--arch", default="DFormer-Base")
+    ap.add_argument("--decoder", default="ham")
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-census", action="store_true")
+    ap.add_argument("--table-out", default=None, help="write the per-kernel F/B/time table (JSON) here")
+    return ap.parse_args()
+
+
+def relaunch_distributed(args):
+    """--gpus N > 1 without a torch.distributed.run environment: start N ranks as a child
+    torch.distributed.run (nothing has touched the GPU in this process) and exit with its code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 class Cfg(dict):
@@ -36,6 +81,7 @@ def make_cfg(arch="DFormer-Base", decoder="ham", ncls=40):
 
 
 def synthetic_batch(B, H, W, ncls, device, seed):
+    import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     mean = torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)
@@ -47,85 +93,118 @@ def synthetic_batch(B, H, W, ncls, device, seed):
     return rgb, dep, lab
 
 
-def dominant_probe(model, batch, height, width):
-    """The dominant kernel whose roofline is reported: the ConvFFN fc2 GEMM of stage 0
-    (DFormer.py:55; M = batch*(H/4)*(W/4) pixels, K = 8*C hidden, N = C = 64 for Base), fused
-    bias + layer-scale residual epilogue that also writes the pre-residual branch output. Its
-    launches inside the timed steps are bracketed by HIP events on their own stream."""
+def census(step_fn):
+    """One untimed step with every library kernel timed and every entry point's algorithmic
+    FLOPs / bytes charged to the first kernel it launched. Returns {kernel: row}."""
+    import torch
     from dformer_amd import kernels as K
-    enc = model.encoder_backbone
-    C = enc.dims[0]
-    M = batch * (height // 4) * (width // 4)
-    return K.LaunchProbe(M, C, C * enc.mlp_ratios[0], True, True)
+    torch.cuda.synchronize()
+    K.ACCOUNT = []
+    K.trace(3)
+    step_fn()
+    torch.cuda.synchronize()
+    timed = K.trace_read()
+    K.trace(0)
+    acct, K.ACCOUNT = K.ACCOUNT, None
+    table = {}
+    for name, ms in timed:
+        r = table.setdefault(name, dict(launches=0, measured_ms=0.0, flops=0.0, bytes=0.0, ideal_ms=0.0, peak=None))
+        r["launches"] += 1
+        r["measured_ms"] += ms
+    for funcs, flops, nbytes, peak in acct:
+        if not funcs:
+            continue
+        name = K.kernel_name(funcs[0])
+        r = table.setdefault(name, dict(launches=0, measured_ms=0.0, flops=0.0, bytes=0.0, ideal_ms=0.0, peak=None))
+        r["flops"] += flops
+        r["bytes"] += nbytes
+        r["peak"] = peak
+        r["ideal_ms"] += max(flops / (MFMA_PEAK_TFS[peak] * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    return table
 
 
-def roofline_of(probe):
-    """Algorithmic bytes per launch: read hidden A (M*K) + W (N*K) + residual (M*N), write the
-    output and the saved branch output (2*M*N); bf16 = 2 B. HBM traffic per launch comes from
-    the rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE x2 on gfx950 + WRITE_SIZE)."""
-    M, N, Kd = probe.key[:3]
-    us = probe.mean_us()
-    if us is None:
-        return None
-    nbytes = 2 * (M * Kd + N * Kd + 3 * M * N)
-    flops = 2 * M * N * Kd
-    ach = nbytes / (us * 1e-6) / 1e9
+def dominant_roofline(table, name, durations_ms):
+    r = table[name]
+    n_c = max(r["launches"], 1)
+    fl, by = r["flops"] / n_c, r["bytes"] / n_c
+    avg_s = sum(durations_ms) / len(durations_ms) * 1e-3
+    peak = MFMA_PEAK_TFS[r["peak"] or "bf16"]
+    t_mfma, t_hbm = fl / (peak * 1e12), by / (HBM_PEAK_GBS * 1e9)
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_dominant_pmc.json")
+    pmc = os.path.join(HERE, "profiles", "r02_dominant_pmc.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
             rec = json.load(f)
-        if tuple(rec.get("key", ())) == probe.key:
+        if rec.get("kernel") == name:
             traffic = rec.get("traffic_bytes_per_launch")
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": f"gemm_stream_kernel bf16 ConvFFN fc2 stage0 (M={M},K={Kd},N={N}), fused bias+residual epilogue",
-            "launches": len(probe.events), "avg_us": round(us, 2), "bytes_per_launch": nbytes,
-            "tflops": round(flops / (us * 1e-6) / 1e12, 1)}
+    if t_mfma >= t_hbm:
+        ach = fl / avg_s / 1e12
+        out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
+    else:
+        ach = by / avg_s / 1e9
+        out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(ach / HBM_PEAK_GBS, 4)}
+    out.update(traffic=traffic, kernel=name, launches=len(durations_ms), avg_us=round(avg_s * 1e6, 2),
+               bytes_per_launch=round(by), flops_per_launch=round(fl),
+               census_share=round(r["measured_ms"] / max(sum(t["measured_ms"] for t in table.values()), 1e-9), 4))
+    return out
 
 
-def cpu_baseline(model_sd, seconds=20.0):
-    """The CPU oracle (oracle/dformer_ref.py, parity-pinned to the reference goldens) timed on
-    this host: DFormer-B + ham fwd+bwd, fp32, bs=2 at 480x640 (SURVEY §8d CPU baseline)."""
+def cpu_baseline(model_sd, seconds):
+    """The CPU oracle (oracle/dformer_ref.py, parity-pinned to the reference goldens) timed on this
+    host's cores, fp32: DFormer-B + ham fwd+bwd bs=2 at 480x640 (the GPU metric's workload), plus
+    BASELINE config 1 (DFormer-Tiny forward, bs=2, 480x640) as a second leg."""
+    import torch
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import dformer_ref as R
+    import gen
     ncores = len(os.sched_getaffinity(0))
     threads = max(1, min(ncores, int(os.environ.get("OMP_NUM_THREADS", ncores))))
     torch.set_num_threads(threads)
-    p = {k: v.detach().float().cpu().clone().requires_grad_(v.is_floating_point() and "running" not in k)
-         for k, v in model_sd.items() if not k.endswith("num_batches_tracked")}
     B, H, W = 2, 480, 640
     rgb, dep, lab = synthetic_batch(B, H, W, 40, "cpu", 0)
-    g = torch.Generator().manual_seed(1)
-    bases = torch.rand(B, 512, 64, generator=g)
-    bases = bases / bases.norm(dim=1, keepdim=True)
-    n, t_total = 0, 0.0
-    while t_total < seconds and n < 20:
-        t0 = time.perf_counter()
+    bases = torch.from_numpy(gen.nmf_bases(B, 512, 64)).float()
+
+    def timeit(fn, budget, max_iter):
+        fn()  # warm-up
+        n, t = 0, 0.0
+        while t < budget and n < max_iter:
+            t0 = time.perf_counter()
+            fn()
+            t += time.perf_counter() - t0
+            n += 1
+        return B * n / t, n
+
+    p = {k: v.detach().float().cpu().clone().requires_grad_(v.is_floating_point() and "running" not in k)
+         for k, v in model_sd.items() if not k.endswith("num_batches_tracked")}
+
+    def base_step():
         _, _, loss = R.segmentor_forward(p, "DFormer-Base", "ham", rgb, dep, bases, True, lab)
         loss.backward()
-        dt = time.perf_counter() - t0
-        if n > 0 or seconds < 1:  # first iteration is warm-up
-            t_total += dt
-        n += 1
-    timed = max(1, n - 1)
-    return {"value": round(B * timed / max(t_total, 1e-9), 3), "unit": "images/s", "cores": threads,
-            "kind": "port", "sample": f"oracle DFormer-B+ham fwd+bwd fp32 bs=2 480x640, {timed} timed iters"}
+
+    v_base, n_base = timeit(base_step, seconds, 20)
+    shapes = R.segmentor_shapes("DFormer-Tiny", "ham", 40)
+    pt = {k: torch.from_numpy(v).float() for k, v in gen.state_dict_values(shapes.items()).items()}
+
+    def tiny_fwd():
+        with torch.no_grad():
+            R.segmentor_forward(pt, "DFormer-Tiny", "ham", rgb, dep, bases, False, None)
+
+    v_tiny, n_tiny = timeit(tiny_fwd, seconds * 0.5, 60)
+    return {"value": round(v_base, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle DFormer-B+ham fwd+bwd fp32 bs=2 480x640, {n_base} timed iters",
+            "config1": {"value": round(v_tiny, 3), "unit": "images/s",
+                        "sample": f"oracle DFormer-Tiny+ham forward fp32 bs=2 480x640 (BASELINE config 1), "
+                                  f"{n_tiny} timed iters"}}
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--arch", default="DFormer-Base")
-    ap.add_argument("--decoder", default="ham")
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    args = ap.parse_args()
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args))
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -135,6 +214,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    from dformer_amd import kernels as K
     from dformer_amd.segmentor import EncoderDecoder
     from dformer_amd.train import FusedAdamW, train_step
 
@@ -154,41 +234,85 @@ def main():
     opt = FusedAdamW(model, lr=cfg.lr, weight_decay=cfg.weight_decay, world=world, compute_dtype=torch.bfloat16)
     rgb, dep, lab = synthetic_batch(args.batch, args.height, args.width, cfg.num_classes, dev, 8964 + rank)
 
+    def step():
+        return train_step(model, opt, rgb, dep, lab)
+
     for _ in range(args.warmup):
-        train_step(model, opt, rgb, dep, lab)
+        step()
+    table, dom = None, None
+    if not args.no_census:
+        table = census(step)
+        dom = max(table, key=lambda n: table[n]["measured_ms"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    from dformer_amd import kernels as K
-    probe = dominant_probe(model, args.batch, args.height, args.width) if rank == 0 else None
-    K.GEMM_PROBE = probe
+    if dom is not None:
+        K.trace(2, dom)
+    s = torch.cuda.current_stream()
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record(s)
     loss = None
-    for _ in range(args.steps):
-        loss = train_step(model, opt, rgb, dep, lab)
+    for i in range(args.steps):
+        loss = step()
+        marks[i + 1].record(s)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    K.GEMM_PROBE = None
+    dom_ms = None
+    if dom is not None:
+        dom_ms = [ms for _, ms in K.trace_read()]
+        K.trace(0)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = elapsed.item()
+    per_step = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
+    q = statistics.quantiles(per_step, n=10) if len(per_step) >= 2 else [per_step[0]] * 9
     images = world * args.batch * args.steps
     value = images / elapsed
+    ms_step = elapsed / args.steps * 1e3
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights)",
         "config": {"workload": f"{args.arch}+{args.decoder} train step fwd+bwd+AdamW",
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                    "image": [args.height, args.width], "parallelism": f"dp{world}"},
+        "step_ms_gpu": {"median": round(statistics.median(per_step), 3), "p10": round(q[0], 3),
+                        "p90": round(q[-1], 3)},
         "loss": round(float(loss.item()), 4) if loss is not None else None,
     }
     if rank == 0:
-        result["roofline"] = roofline_of(probe)
+        if table is not None and dom_ms:
+            roof = dominant_roofline(table, dom, dom_ms)
+            ideal = sum(r["ideal_ms"] for r in table.values())
+            traced = sum(r["measured_ms"] for r in table.values())
+            survey_ms = None
+            if (args.arch, args.decoder, args.height, args.width) == ("DFormer-Base", "ham", 480, 640):
+                survey_ms = SURVEY_TFLOP_PER_IMG * args.batch / MFMA_PEAK_TFS["bf16"] * 1e3
+            top = sorted(table.items(), key=lambda kv: -kv[1]["measured_ms"])[:5]
+            roof["step"] = {
+                "ideal_ms": round(ideal, 3), "frac": round(ideal / ms_step, 4),
+                "survey_bound_ms": round(survey_ms, 3) if survey_ms else None,
+                "survey_frac": round(survey_ms / ms_step, 4) if survey_ms else None,
+                "census_traced_ms": round(traced, 3), "census_untraced_ms": round(per_step[len(per_step) // 2] - traced, 3),
+                "census_launches": sum(r["launches"] for r in table.values()),
+                "top": [{"kernel": n[:120], "ms": round(r["measured_ms"], 3), "ideal_ms": round(r["ideal_ms"], 3),
+                         "launches": r["launches"]} for n, r in top]}
+            result["roofline"] = roof
+            if args.table_out:
+                os.makedirs(os.path.dirname(os.path.abspath(args.table_out)), exist_ok=True)
+                with open(args.table_out, "w") as f:
+                    json.dump({"config": result["config"], "ms_per_step": result["ms_per_step"],
+                               "peaks": {"hbm_GBs": HBM_PEAK_GBS, "mfma_TFs": MFMA_PEAK_TFS},
+                               "kernels": {n: {k: (round(v, 6) if isinstance(v, float) else v) for k, v in r.items()}
+                                           for n, r in sorted(table.items(), key=lambda kv: -kv[1]["measured_ms"])}},
+                              f, indent=1)
+        else:
+            result["roofline"] = None
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(sd_cpu, args.cpu_seconds)
         print(json.dumps(result), flush=True)

@@ -81,6 +81,10 @@ _SIGS = {
     "dfm_seg_loss_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P]),
     "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P]),
     "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, P]),
+    "dfm_trace_set": (c_int, [c_int, ctypes.c_char_p]),
+    "dfm_trace_take": (c_int, [ctypes.POINTER(c_void_p), c_int]),
+    "dfm_trace_read": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_float), c_int]),
+    "dfm_kernel_name": (ctypes.c_char_p, [c_void_p]),
 }
 
 

@@ -17,7 +17,7 @@ from collections import OrderedDict
 
 import torch
 
-from .functional import invalidate_weights
+from .functional import has_grad_slot, invalidate_weights
 
 
 def _read(src):
@@ -37,12 +37,20 @@ def load_pretrained_backbone(backbone, src, freeze=True):
     sd = _strip(sd, "backbone.")
     if next(iter(sd), "").startswith("module."):
         sd = _strip(sd, "module.")
-    res = backbone.load_state_dict(sd, strict=False)
     if freeze:
         keys = set(sd)
-        for name, p in backbone.named_parameters():
-            if any(name == k or name.startswith(k + ".") for k in keys):
-                p.requires_grad = False
+        to_freeze = [(name, p) for name, p in backbone.named_parameters()
+                     if any(name == k or name.startswith(k + ".") for k in keys)]
+        live = [name for name, p in to_freeze if has_grad_slot(p)]
+        if live:
+            # the reference freezes inside the model constructor, before any optimizer exists; a live
+            # FusedAdamW would keep writing and applying gradients of these parameters
+            raise RuntimeError(f"load_pretrained_backbone(freeze=True) after FusedAdamW was built: {live[:3]}... "
+                               "are in its flat groups; load (and freeze) first, then build the optimizer")
+    res = backbone.load_state_dict(sd, strict=False)
+    if freeze:
+        for _, p in to_freeze:
+            p.requires_grad = False
     invalidate_weights()
     return res.missing_keys, res.unexpected_keys
 

@@ -865,13 +865,13 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
     return dispatch(
         dtype,
         [&] {
-          hipLaunchKernelGGL(pool7_fwd_vec_kernel<bf16_t>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
+          DFM_LAUNCH(pool7_fwd_vec_kernel<bf16_t>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
                              (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
         [&] {
-          hipLaunchKernelGGL(pool7_fwd_vec_kernel<float>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
+          DFM_LAUNCH(pool7_fwd_vec_kernel<float>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
                              (const float*)x, ldx, (float*)y, ldy);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
@@ -881,12 +881,12 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(pool7_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, H, W, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
+        DFM_LAUNCH(pool7_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, H, W, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(pool7_fwd_kernel<float>, grid, dim3(256), 0, s, B, H, W, C, (const float*)x, ldx, (float*)y, ldy);
+        DFM_LAUNCH(pool7_fwd_kernel<float>, grid, dim3(256), 0, s, B, H, W, C, (const float*)x, ldx, (float*)y, ldy);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });
@@ -900,13 +900,13 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
     return dispatch(
         dtype,
         [&] {
-          hipLaunchKernelGGL(pool7_bwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy,
+          DFM_LAUNCH(pool7_bwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy,
                              lddy, (bf16_t*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
         [&] {
-          hipLaunchKernelGGL(pool7_bwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const float*)dy,
+          DFM_LAUNCH(pool7_bwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const float*)dy,
                              lddy, (float*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
@@ -916,12 +916,12 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(pool7_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+        DFM_LAUNCH(pool7_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(pool7_bwd_kernel<float>, dim3(g), dim3(256), 0, s, B, H, W, C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
+        DFM_LAUNCH(pool7_bwd_kernel<float>, dim3(g), dim3(256), 0, s, B, H, W, C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });
@@ -935,13 +935,13 @@ extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
     return dispatch(
         dtype,
         [&] {
-          hipLaunchKernelGGL(bilinear_fwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
+          DFM_LAUNCH(bilinear_fwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
                              (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
         [&] {
-          hipLaunchKernelGGL(bilinear_fwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
+          DFM_LAUNCH(bilinear_fwd_vec_kernel<float>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
                              (const float*)x, ldx, (float*)y, ldy, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
@@ -951,12 +951,12 @@ extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(bilinear_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
+        DFM_LAUNCH(bilinear_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(bilinear_fwd_kernel<float>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const float*)x, ldx, (float*)y, ldy, accumulate);
+        DFM_LAUNCH(bilinear_fwd_kernel<float>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const float*)x, ldx, (float*)y, ldy, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });
@@ -972,13 +972,13 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
     return dispatch(
         dtype,
         [&] {
-          hipLaunchKernelGGL(bilinear_bwd_vec_kernel<bf16_t>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
+          DFM_LAUNCH(bilinear_bwd_vec_kernel<bf16_t>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
                              C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
         [&] {
-          hipLaunchKernelGGL(bilinear_bwd_vec_kernel<float>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
+          DFM_LAUNCH(bilinear_bwd_vec_kernel<float>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
                              C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
@@ -988,12 +988,12 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(bilinear_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+        DFM_LAUNCH(bilinear_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(bilinear_bwd_kernel<float>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
+        DFM_LAUNCH(bilinear_bwd_kernel<float>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const float*)dy, lddy, (float*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });
@@ -1015,8 +1015,8 @@ static void attn_mfma_launch(AttnArgs& a, bool bwd, hipStream_t s) {
   const int kpw = attn_kpw(a.N);
   const int groups = (a.nchunk + 3) / 4;
   const dim3 grid((unsigned)(a.B * a.heads * groups));
-  if (bwd) hipLaunchKernelGGL(attn_bwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
-  else hipLaunchKernelGGL(attn_fwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
+  if (bwd) DFM_LAUNCH(attn_bwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
+  else DFM_LAUNCH(attn_fwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
 }
 static void attn_mfma(AttnArgs& a, bool bwd, hipStream_t s) {
   if (a.dh == 16) attn_mfma_launch<16>(a, bwd, s);
@@ -1045,7 +1045,7 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
       attn_mfma(a, false, s);
       DFM_LAUNCH_CHECK();
-      hipLaunchKernelGGL(attn_fwd_combine_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
@@ -1057,16 +1057,16 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(attn_fwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
+        DFM_LAUNCH(attn_fwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_fwd_combine_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(attn_fwd_chunk_kernel<float>, dim3(nblk), dim3(256), lds, s, a);
+        DFM_LAUNCH(attn_fwd_chunk_kernel<float>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_fwd_combine_kernel<float>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_fwd_combine_kernel<float>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });
@@ -1091,7 +1091,7 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
       attn_mfma(a, true, s);
       DFM_LAUNCH_CHECK();
-      hipLaunchKernelGGL(attn_dq_reduce_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
@@ -1103,16 +1103,16 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
   return dispatch(
       dtype,
       [&] {
-        hipLaunchKernelGGL(attn_bwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
+        DFM_LAUNCH(attn_bwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_dq_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
       [&] {
-        hipLaunchKernelGGL(attn_bwd_chunk_kernel<float>, dim3(nblk), dim3(256), lds, s, a);
+        DFM_LAUNCH(attn_bwd_chunk_kernel<float>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        hipLaunchKernelGGL(attn_dq_reduce_kernel<float>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_dq_reduce_kernel<float>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       });

@@ -165,6 +165,19 @@ __global__ __launch_bounds__(1024) void partial_sum_kernel(int nblk, long n, con
   }
 }
 
+// ---- every kernel launch goes through DFM_LAUNCH: the launch tracer (runtime.cpp) can record
+// which kernels an entry point enqueued and time chosen kernels with HIP events on their stream.
+extern int dfm_trace_flags;
+void dfm_trace_pre(const void* func, hipStream_t s);
+void dfm_trace_post(const void* func, hipStream_t s);
+#define DFM_LAUNCH(kern, grid, block, lds, stream, ...)                       \
+  do {                                                                       \
+    const int _dfm_tr = dfm_trace_flags;                                     \
+    if (_dfm_tr) dfm_trace_pre((const void*)(kern), (hipStream_t)(stream));  \
+    hipLaunchKernelGGL(kern, grid, block, lds, stream, __VA_ARGS__);         \
+    if (_dfm_tr) dfm_trace_post((const void*)(kern), (hipStream_t)(stream)); \
+  } while (0)
+
 // ---- host-side error plumbing (thread-local last error string)
 void dfm_set_error(const char* fmt, ...);
 #define DFM_CHECK_ARG(cond, ...)          \

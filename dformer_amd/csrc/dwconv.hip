@@ -498,7 +498,7 @@ template <typename T>
 long w3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
                hipStream_t s) {
   const W3Geom g = w3_geom<T>(B, H, W, C);
-  hipLaunchKernelGGL(dw3_stream_wgrad_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H,
+  DFM_LAUNCH(dw3_stream_wgrad_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H,
                      W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, part);
   return g.nsb;
 }
@@ -621,7 +621,7 @@ template <typename T>
 long w7_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
                hipStream_t s) {
   const W3Geom g = w7_geom<T>(B, H, W, C);
-  hipLaunchKernelGGL(dw7_stream_wgrad_kernel<T>, dim3((unsigned)(g.nsb * 7), (unsigned)g.slices), dim3(256), 0, s,
+  DFM_LAUNCH(dw7_stream_wgrad_kernel<T>, dim3((unsigned)(g.nsb * 7), (unsigned)g.slices), dim3(256), 0, s,
                      B, H, W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (int)g.nsb, (const T*)x, ldx,
                      (const T*)dy, lddy, part);
   return g.nsb;
@@ -776,7 +776,7 @@ template <typename T, bool FLIP>
 int f3_launch(int B, int H, int W, int C, const void* x, long ldx, const float* w, const float* bias, int id,
               void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
   const W3Geom g = f3_geom<T>(B, H, W, C);
-  hipLaunchKernelGGL((dw3_stream_fwd_kernel<T, FLIP>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B,
+  DFM_LAUNCH((dw3_stream_fwd_kernel<T, FLIP>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B,
                      H, W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, w, bias, id, (T*)y, ldy,
                      acc, (T*)gout, ldg);
   DFM_LAUNCH_CHECK();
@@ -814,7 +814,7 @@ int dw_tile_launch(int B, int H, int W, int C, const void* x, long ldx, const fl
   const int G = C / CPT;
   dim3 grid((unsigned)((long)B * tiles_h * tiles_w * cdiv(G, NG)));
   const size_t lds = (size_t)(TH + K - 1) * (TWT + K - 1) * NG * 16 + (size_t)K * K * NG * CPT * sizeof(float);
-  hipLaunchKernelGGL((dw_tile_fwd_kernel<T, K, FLIP, NG>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
+  DFM_LAUNCH((dw_tile_fwd_kernel<T, K, FLIP, NG>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
                      (const T*)x, ldx, w, bias, id, (T*)y, ldy, acc, (T*)gout, ldg);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -900,7 +900,7 @@ long wgrad_launch(int B, int H, int W, int C, const void* x, long ldx, const voi
   wgrad_geom<T, K, NG>(B, H, W, C, tiles_h, tiles_w, grid);
   const size_t lds_tile = ((size_t)(TH + KI - 1) * (TWT + K - 1) * NG + (size_t)TH * TWT * NG) * 16;
   const size_t lds_red = (size_t)4 * (KI * K + 1) * NG * CPT * sizeof(float);
-  hipLaunchKernelGGL((dw_tile_wgrad_kernel<T, K, NG>), grid, dim3(256), std::max(lds_tile, lds_red), s, B, H, W, C,
+  DFM_LAUNCH((dw_tile_wgrad_kernel<T, K, NG>), grid, dim3(256), std::max(lds_tile, lds_red), s, B, H, W, C,
                      tiles_h, tiles_w, (const T*)x, ldx, (const T*)dy, lddy, part);
   return grid.x;
 }
@@ -978,7 +978,7 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, (int)nsb,
+  DFM_LAUNCH(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, (int)nsb,
                      (long)C * (k * k + 1), (const float*)part, dw, db, (long)(k * k + 1), 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

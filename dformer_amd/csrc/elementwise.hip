@@ -14,9 +14,9 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void colred_kernel(long rows, int C, const T* __restrict__ x, long ldx,
                                                      const T* __restrict__ y, long ldy, const float* __restrict__ p0,
                                                      const float* __restrict__ p1, long rps, float* __restrict__ part,
-                                                     int nblk) {
+                                                     int nblk, float* __restrict__ aux) {
   // MODE 0: sum x * (y?) * rowscale(p1?)           -> 1 output
-  // MODE 1: BN stats: sum x, sum x^2               -> 2 outputs
+  // MODE 1: BN stats, shifted by K = x[row 0]: sum (x-K), sum (x-K)^2 -> 2 outputs (+ K into aux)
   // MODE 2: BN bwd:  sum y, sum y * (x - p0[c]) * p1[c]   -> 2 outputs (y = dy, p0 mean, p1 rstd)
   constexpr int NOUT = MODE == 0 ? 1 : 2;
   const int cl = threadIdx.x % COLS, rl = threadIdx.x / COLS;  // 4 row lanes
@@ -24,9 +24,11 @@ __global__ __launch_bounds__(256) void colred_kernel(long rows, int C, const T* 
   const long per = (rows + nblk - 1) / nblk;
   const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
   float s0 = 0.f, s1 = 0.f;
+  const float k0 = (MODE == 1 && c < C) ? ldf(x + c) : 0.f;
+  if (MODE == 1 && blockIdx.x == 0 && rl == 0 && c < C) aux[c] = k0;
   if (c < C) {
     for (long r = r0 + rl; r < r1; r += 4) {
-      const float xv = ldf(x + r * ldx + c);
+      const float xv = ldf(x + r * ldx + c) - k0;
       if (MODE == 0) {
         float v = xv;
         if (y) v *= ldf(y + r * ldy + c);
@@ -71,24 +73,35 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const T* __restrict__ x, long ldx,
                                                          const T* __restrict__ y, long ldy,
                                                          const float* __restrict__ p0, const float* __restrict__ p1,
-                                                         long rps, float* __restrict__ part, int nblk) {
+                                                         long rps, float* __restrict__ part, int nblk,
+                                                         float* __restrict__ aux) {
   constexpr int NOUT = MODE == 0 ? 1 : 2, V = 16 / sizeof(T);
   __shared__ float red[NOUT][256][V + 1];
   const int G = C / V, RL = 256 / G;
   const int g = threadIdx.x % G, rl = threadIdx.x / G, c0 = g * V;
   const long per = (rows + nblk - 1) / nblk;
   const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
-  float s0[V], s1[V], mu[V], rs[V];
+  float s0[V], s1[V], mu[V], rs[V], k0[V];
+  if (MODE == 1) ldvec<T>(x + c0, k0);  // BN stats shift: row 0
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     s0[e] = 0.f;
     s1[e] = 0.f;
     mu[e] = MODE == 2 ? p0[c0 + e] : 0.f;
     rs[e] = MODE == 2 ? p1[c0 + e] : 0.f;
+    if (MODE != 1) k0[e] = 0.f;
+  }
+  if (MODE == 1 && blockIdx.x == 0 && rl == 0) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) aux[c0 + e] = k0[e];
   }
   for (long r = r0 + rl; r < r1; r += RL) {
     float xv[V];
     ldvec<T>(x + r * ldx + c0, xv);
+    if (MODE == 1) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) xv[e] -= k0[e];
+    }
     if (MODE == 0) {
       float yv[V];
       if (y) ldvec<T>(y + r * ldy + c0, yv);
@@ -138,28 +151,28 @@ int red_blocks(long rows) { return (int)min((long)RED_BLOCKS, max(1L, (rows + 25
 
 template <typename T, int MODE>
 int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, const float* p0, const float* p1,
-           long rps, float* out, int accumulate, void* ws, hipStream_t s) {
+           long rps, float* out, int accumulate, void* ws, hipStream_t s, float* aux = nullptr) {
   constexpr int NOUT = MODE == 0 ? 1 : 2;
   const int nblk = red_blocks(rows);
   constexpr int V = 16 / sizeof(T);
   const int G = C / V;
-  // DFM_COLRED_VEC=1 selects the vectorized narrow-row reduction. Off by default: its different fp32
-  // summation order shifts the one-pass BN variance (E[x²] - E[x]², cancellation-prone) enough to
-  // move the fp32 end-to-end input-gradient golden past its 1e-3 gate; needs shifted BN sums first.
+  // The vectorized narrow-row reduction is the default (DFM_COLRED_VEC=0 selects the scalar kernel
+  // for A/B timing). BN statistics are sums shifted by the first row, so the variance no longer
+  // cancels (E[x²] - E[x]² moved the fp32 input-gradient golden past 1e-3 in round 1).
   static const bool vec_on = [] {
     const char* e = getenv("DFM_COLRED_VEC");
-    return e && atoi(e) == 1;
+    return !e || atoi(e) != 0;
   }();
   const bool vec = vec_on && C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
                    (!y || (ldy % V == 0 && ((uintptr_t)y & 15) == 0));
   if (vec)
-    hipLaunchKernelGGL((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
-                       (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
+    DFM_LAUNCH((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
+                       (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
   else
-    hipLaunchKernelGGL((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x,
-                       ldx, (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk);
+    DFM_LAUNCH((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x,
+                       ldx, (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<0>, dim3(cdiv((long)NOUT * C, 64)), dim3(1024), 0, s, nblk, (long)NOUT * C,
+  DFM_LAUNCH(partial_sum_kernel<0>, dim3(cdiv((long)NOUT * C, 64)), dim3(1024), 0, s, nblk, (long)NOUT * C,
                      (const float*)ws, out, (float*)nullptr, 0L, accumulate);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -243,20 +256,20 @@ int ew2d(int dtype, long rows, int C, const void* a, long lda, const void* b, lo
       (dtype == DFM_BF16 || dtype == DFM_F32)) {
     const unsigned gv = ew_grid(rows * C / 8);
     if (dtype == DFM_BF16)
-      hipLaunchKernelGGL((ew2d_vec_kernel<bf16_t, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
+      DFM_LAUNCH((ew2d_vec_kernel<bf16_t, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
                          (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
     else
-      hipLaunchKernelGGL((ew2d_vec_kernel<float, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const float*)a, lda,
+      DFM_LAUNCH((ew2d_vec_kernel<float, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const float*)a, lda,
                          (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
     DFM_LAUNCH_CHECK();
     return DFM_OK;
   }
   const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL((ew2d_kernel<bf16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
+    DFM_LAUNCH((ew2d_kernel<bf16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
                        (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
   else if (dtype == DFM_F32)
-    hipLaunchKernelGGL((ew2d_kernel<float, OP>), dim3(g), dim3(256), 0, s, rows, C, (const float*)a, lda,
+    DFM_LAUNCH((ew2d_kernel<float, OP>), dim3(g), dim3(256), 0, s, rows, C, (const float*)a, lda,
                        (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
   else {
     dfm_set_error("elementwise: bad dtype");
@@ -278,8 +291,10 @@ __global__ void bn_finalize_kernel(int C, const float* __restrict__ st, double c
                                    float* __restrict__ rv) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  const double mu = st[c] / count;
-  double var = st[C + c] / count - mu * mu;
+  // st = (sum (x-K), sum (x-K)^2, K): mean = K + d, var = E[(x-K)^2] - d^2 with d = E[x-K] small
+  const double d = st[c] / count;
+  const double mu = st[2 * C + c] + d;
+  double var = st[C + c] / count - d * d;
   if (var < 0) var = 0;
   mean[c] = (float)mu;
   rstd[c] = (float)(1.0 / sqrt(var + eps));
@@ -457,10 +472,10 @@ extern "C" int dfm_cast(int din, int dout, long n, const void* x, void* y, dfm_s
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return DFM_OK;
   const unsigned g = ew_grid(n);
-  if (din == DFM_F32 && dout == DFM_BF16) hipLaunchKernelGGL((cast_kernel<float, bf16_t>), dim3(g), dim3(256), 0, s, n, (const float*)x, (bf16_t*)y);
-  else if (din == DFM_BF16 && dout == DFM_F32) hipLaunchKernelGGL((cast_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (float*)y);
-  else if (din == DFM_F32 && dout == DFM_F32) hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, n, (const float*)x, (float*)y);
-  else if (din == DFM_BF16 && dout == DFM_BF16) hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (bf16_t*)y);
+  if (din == DFM_F32 && dout == DFM_BF16) DFM_LAUNCH((cast_kernel<float, bf16_t>), dim3(g), dim3(256), 0, s, n, (const float*)x, (bf16_t*)y);
+  else if (din == DFM_BF16 && dout == DFM_F32) DFM_LAUNCH((cast_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (float*)y);
+  else if (din == DFM_F32 && dout == DFM_F32) DFM_LAUNCH((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, n, (const float*)x, (float*)y);
+  else if (din == DFM_BF16 && dout == DFM_BF16) DFM_LAUNCH((cast_kernel<bf16_t, bf16_t>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (bf16_t*)y);
   else {
     dfm_set_error("dfm_cast: bad dtype");
     return DFM_ERR_DTYPE;
@@ -493,15 +508,18 @@ extern "C" int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx
                             dfm_stream_t stream) {
   DFM_CHECK_ARG(x && stats && ws, "dfm_bn_stats: null argument");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == DFM_BF16) return colred<bf16_t, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s);
-  if (dtype == DFM_F32) return colred<float, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s);
+  DFM_CHECK_ARG(rows > 0, "dfm_bn_stats: no rows");
+  if (dtype == DFM_BF16)
+    return colred<bf16_t, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s, stats + 2 * C);
+  if (dtype == DFM_F32)
+    return colred<float, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s, stats + 2 * C);
   dfm_set_error("dfm_bn_stats: bad dtype");
   return DFM_ERR_DTYPE;
 }
 
 extern "C" int dfm_bn_finalize(int C, const float* stats, double count, float eps, float momentum, float* mean,
                                float* rstd, float* rm, float* rv, dfm_stream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, stats, count, eps,
+  DFM_LAUNCH(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, stats, count, eps,
                      momentum, mean, rstd, rm, rv);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -514,20 +532,20 @@ extern "C" int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx
   if (C % 8 == 0 && ew_al<float>(x, ldx) && ew_al<float>(res, ldres) && ew_al<float>(y, ldy)) {
     const unsigned gv = ew_grid(rows * C / 8);
     if (dtype == DFM_BF16)
-      hipLaunchKernelGGL(bn_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean,
+      DFM_LAUNCH(bn_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean,
                          rstd, gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
     else
-      hipLaunchKernelGGL(bn_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean,
+      DFM_LAUNCH(bn_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean,
                          rstd, gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
     DFM_LAUNCH_CHECK();
     return DFM_OK;
   }
   const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean, rstd,
+    DFM_LAUNCH(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean, rstd,
                        gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean, rstd,
+    DFM_LAUNCH(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean, rstd,
                        gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -548,20 +566,20 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
   if (C % 8 == 0 && ew_al<float>(x, ldx) && ew_al<float>(dy, lddy) && ew_al<float>(dx, lddx)) {
     const unsigned gv = ew_grid(rows * C / 8);
     if (dtype == DFM_BF16)
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
+      DFM_LAUNCH(bn_bwd_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
                          (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
     else
-      hipLaunchKernelGGL(bn_bwd_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx,
+      DFM_LAUNCH(bn_bwd_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx,
                          (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
     DFM_LAUNCH_CHECK();
     return DFM_OK;
   }
   const unsigned g = ew_grid(rows * C);
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
+    DFM_LAUNCH(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
                        (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx,
+    DFM_LAUNCH(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx,
                        (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -569,7 +587,7 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
 
 extern "C" int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
                               dfm_stream_t stream) {
-  hipLaunchKernelGGL(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out);
+  DFM_LAUNCH(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
@@ -577,21 +595,21 @@ extern "C" int dfm_nmf_update(long n, const float* a, const float* num, const fl
 extern "C" int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                                   const float* out, float eps, float* ga, int acc, float* gnum, float* gden,
                                   dfm_stream_t stream) {
-  hipLaunchKernelGGL(nmf_update_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den, out,
+  DFM_LAUNCH(nmf_update_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den, out,
                      eps, ga, acc, gnum, gden);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
 extern "C" int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream) {
-  hipLaunchKernelGGL(softmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, x, y);
+  DFM_LAUNCH(softmax_rows_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, x, y);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
 extern "C" int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int acc,
                                     dfm_stream_t stream) {
-  hipLaunchKernelGGL(softmax_rows_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, y, dy, dx,
+  DFM_LAUNCH(softmax_rows_bwd_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, rows, R, y, dy, dx,
                      acc);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -603,7 +621,7 @@ extern "C" int dfm_adamw(long n, float* p, const float* g, float* m, float* v, f
   if (n == 0) return DFM_OK;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
-  hipLaunchKernelGGL(adamw_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1, beta2,
+  DFM_LAUNCH(adamw_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1, beta2,
                      eps, wd, bc1, sqrtf(bc2), gscale, (bf16_t*)bf16_copy);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -672,17 +690,17 @@ extern "C" int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, l
   hipStream_t s = (hipStream_t)stream;
   const int nblk = (int)min((long)RES_BLOCKS, max(1L, rows / 64));
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(residual_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, rows, C, (const bf16_t*)dout, lddout,
+    DFM_LAUNCH(residual_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, rows, C, (const bf16_t*)dout, lddout,
                        (const bf16_t*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (bf16_t*)df, lddf, (float*)ws);
   else if (dtype == DFM_F32)
-    hipLaunchKernelGGL(residual_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, rows, C, (const float*)dout, lddout,
+    DFM_LAUNCH(residual_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, rows, C, (const float*)dout, lddout,
                        (const float*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (float*)df, lddf, (float*)ws);
   else {
     dfm_set_error("dfm_residual_bwd: bad dtype");
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<0>, dim3(cdiv(C, 64)), dim3(1024), 0, s, nblk, (long)C, (const float*)ws, dscale,
+  DFM_LAUNCH(partial_sum_kernel<0>, dim3(cdiv(C, 64)), dim3(1024), 0, s, nblk, (long)C, (const float*)ws, dscale,
                      (float*)nullptr, 0L, 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

@@ -740,14 +740,14 @@ int launch_cfg(GemmArgs& a, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>), grid, dim3(64 * NW), lds, s, a);
+  DFM_LAUNCH((gemm_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>), grid, dim3(64 * NW), lds, s, a);
   DFM_LAUNCH_CHECK();
   if (a.splits > 1) {
     const long total = (long)a.batch * a.M * a.ldw;
     if (a.splits >= 8)
-      hipLaunchKernelGGL((splitk_reduce_kernel<T, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
+      DFM_LAUNCH((splitk_reduce_kernel<T, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((splitk_reduce_kernel<T, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
+      DFM_LAUNCH((splitk_reduce_kernel<T, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
     DFM_LAUNCH_CHECK();
   }
   return DFM_OK;
@@ -772,7 +772,7 @@ int launch_stream(GemmArgs& a, hipStream_t s) {
   const int tiles_m = cdiv(a.M, BM);
   const long ntiles = (long)tiles_m * cdiv(a.Nw, BN);
   const long grid = std::min(ntiles, (long)256 * per_cu);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, a, tiles_m, ntiles);
+  DFM_LAUNCH(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, a, tiles_m, ntiles);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

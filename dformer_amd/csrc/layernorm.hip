@@ -355,7 +355,7 @@ int ln_fwd(long rows, int C, const void* x, long ldx, const float* gamma, const 
     const unsigned vgrid = cdiv(rows, 256 / VG);
 #define GOV(GG, NN)                                                                                          \
   if (VG == GG && VNV == NN) {                                                                                \
-    hipLaunchKernelGGL((ln_fwd_vec_kernel<T, GG, NN>), dim3(vgrid), dim3(256), 0, s, rows, C, (const T*)x, ldx, \
+    DFM_LAUNCH((ln_fwd_vec_kernel<T, GG, NN>), dim3(vgrid), dim3(256), 0, s, rows, C, (const T*)x, ldx, \
                        gamma, beta, eps, (T*)y, ldy, mean, rstd);                                             \
     DFM_LAUNCH_CHECK();                                                                                      \
     return DFM_OK;                                                                                           \
@@ -366,7 +366,7 @@ int ln_fwd(long rows, int C, const void* x, long ldx, const float* gamma, const 
   const int G = pick_g(C);
   const unsigned grid = cdiv(rows, 256 / G);
 #define GO(GG)                                                                                            \
-  hipLaunchKernelGGL((ln_fwd_kernel<T, GG>), dim3(grid), dim3(256), 0, s, rows, C, (const T*)x, ldx, gamma, \
+  DFM_LAUNCH((ln_fwd_kernel<T, GG>), dim3(grid), dim3(256), 0, s, rows, C, (const T*)x, ldx, gamma, \
                      beta, eps, (T*)y, ldy, mean, rstd)
   switch (G) {
     case 8: GO(8); break;
@@ -392,7 +392,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
     bool launched = false;
 #define GOV(GG, NN)                                                                                            \
   if (!launched && VG == GG && VNV == NN) {                                                                     \
-    hipLaunchKernelGGL((ln_bwd_vec_kernel<T, GG, NN>), dim3(vgrid), dim3(256), 0, s, rows, C, (const T*)x, ldx,   \
+    DFM_LAUNCH((ln_bwd_vec_kernel<T, GG, NN>), dim3(vgrid), dim3(256), 0, s, rows, C, (const T*)x, ldx,   \
                        (const T*)dy, lddy, gamma, mean, rstd, (const T*)dres, lddres, (T*)dx, lddx, acc, part); \
     launched = true;                                                                                           \
   }
@@ -400,7 +400,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
 #undef GOV
     if (launched) {
       DFM_LAUNCH_CHECK();
-      hipLaunchKernelGGL(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)vgrid, 2L * C,
+      DFM_LAUNCH(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)vgrid, 2L * C,
                          (const float*)part, dg, db, (long)C, 0);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
@@ -409,7 +409,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
   const int G = pick_g(C);
   const unsigned grid = min((unsigned)LN_BWD_BLOCKS, cdiv(rows, 256 / G));
 #define GO(GG)                                                                                             \
-  hipLaunchKernelGGL((ln_bwd_kernel<T, GG>), dim3(grid), dim3(256), 0, s, rows, C, (const T*)x, ldx,         \
+  DFM_LAUNCH((ln_bwd_kernel<T, GG>), dim3(grid), dim3(256), 0, s, rows, C, (const T*)x, ldx,         \
                      (const T*)dy, lddy, gamma, mean, rstd, (const T*)dres, lddres, (T*)dx, lddx, acc, part)
   switch (G) {
     case 8: GO(8); break;
@@ -419,7 +419,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
   }
 #undef GO
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)grid, 2L * C,
+  DFM_LAUNCH(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)grid, 2L * C,
                      (const float*)part, dg, db, (long)C, 0);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

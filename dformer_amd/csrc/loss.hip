@@ -249,13 +249,13 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
   const long n = (long)B * H * W;
   const int nblk = (int)min((long)LOSS_BLOCKS, (n + 255) / 256);
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H,
+    DFM_LAUNCH(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H,
                        W, label, ignore, lse, (float*)workspace);
   else
-    hipLaunchKernelGGL(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H,
+    DFM_LAUNCH(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H,
                        W, label, ignore, lse, (float*)workspace);
   DFM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(seg_loss_sum_kernel, dim3(1), dim3(64), 0, s, nblk, (const float*)workspace, loss_out);
+  DFM_LAUNCH(seg_loss_sum_kernel, dim3(1), dim3(64), 0, s, nblk, (const float*)workspace, loss_out);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
@@ -268,7 +268,7 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
                 "dfm_seg_loss_bwd: bad argument (needs ncls <= 64 and an upsampling resize)");
   hipStream_t s = (hipStream_t)stream;
   const long nl = (long)B * h * w * ncls;
-  hipLaunchKernelGGL(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
+  DFM_LAUNCH(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
   DFM_LAUNCH_CHECK();
   const unsigned nblk = B * ((H + TY - 1) / TY) * ((W + TX - 1) / TX);
   // low-res columns one TX-wide pixel tile can touch (+2 for the taps at both ends)
@@ -282,10 +282,10 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
     (void)hipGetLastError();  // a refused attribute must not read as this launch's error
   }
   if (dtype == DFM_BF16)
-    hipLaunchKernelGGL(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
+    DFM_LAUNCH(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
                        H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
   else
-    hipLaunchKernelGGL(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,
+    DFM_LAUNCH(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,
                        H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
   DFM_LAUNCH_CHECK();
   return DFM_OK;

@@ -28,6 +28,46 @@ def _world(sync):
     return 1
 
 
+def merge_bn_stats(parts, counts):
+    """Chan-merge per-shard shifted BN statistics into one (0, M2, mean) triple.
+
+    parts: [S, 3, C] float32 = (sum (x-K_s), sum (x-K_s)^2, K_s) per shard; counts: [S] rows.
+    Returns [3, C] whose finalize gives the statistics of the union of the shards (what
+    SyncBatchNorm's all_gather of (mean, invstd, count) computes, torch/nn/modules/_functions.py)."""
+    n = counts.to(torch.float64).view(-1, 1)
+    s1, s2, k = parts[:, 0].double(), parts[:, 1].double(), parts[:, 2].double()
+    d = s1 / n
+    mean_s = k + d
+    m2_s = s2 - s1 * d
+    N = n.sum()
+    mean = (n * mean_s).sum(0) / N
+    m2 = (m2_s + n * (mean_s - mean) ** 2).sum(0)
+    return torch.stack([torch.zeros_like(mean), m2, mean]).float()
+
+
+def bn_batch_stats(x, bn, sync):
+    """Train-mode BatchNorm / SyncBatchNorm statistics of NHWC rows x: (mean, rstd, count), with the
+    running statistics updated like torch (momentum, unbiased variance). With SyncBN over a
+    multi-rank group the per-rank shifted sums are all-gathered and Chan-merged."""
+    st = K.bn_stats(x)
+    rows = x.shape[0]
+    world = _world(sync)
+    count = rows
+    if world > 1:
+        gathered = [torch.empty_like(st) for _ in range(world)]
+        dist.all_gather(gathered, st)
+        cnt = torch.tensor([float(rows)], device=x.device)
+        counts = [torch.empty_like(cnt) for _ in range(world)]
+        dist.all_gather(counts, cnt)
+        counts = torch.cat(counts)
+        st = merge_bn_stats(torch.stack(gathered), counts)
+        count = int(counts.sum().item())
+    mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1, bn.running_mean,
+                               bn.running_var)
+    bn.num_batches_tracked.add_(1)
+    return mean, rstd, count
+
+
 # ============================================================================ building blocks
 class ConvBNActFn(torch.autograd.Function):
     """y = act(BN(x @ W^T) [+ res])  — mmcv ConvModule(1x1 conv, BN, ReLU) (ham_head.py:204-220)."""
@@ -39,11 +79,7 @@ class ConvBNActFn(torch.autograd.Function):
         y0 = K.linear(x, Wc)
         rows = x.shape[0]
         if bn.training:
-            st = _allreduce(K.bn_stats(y0), sync)
-            count = rows * _world(sync)
-            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
-                                       bn.running_mean, bn.running_var)
-            bn.num_batches_tracked.add_(1)
+            mean, rstd, count = bn_batch_stats(y0, bn, sync)
         else:
             mean = bn.running_mean
             rstd = torch.rsqrt(bn.running_var + bn.eps)
@@ -442,11 +478,7 @@ class FuseBNReLUFn(torch.autograd.Function):
         y0 = K.linear(cat, Wc, b)
         rows = cat.shape[0]
         if bn.training:
-            st = _allreduce(K.bn_stats(y0), sync)
-            count = rows * _world(sync)
-            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
-                                       bn.running_mean, bn.running_var)
-            bn.num_batches_tracked.add_(1)
+            mean, rstd, count = bn_batch_stats(y0, bn, sync)
         else:
             mean, rstd, count = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps), rows
         y = K.bn_apply(y0, mean, rstd, gamma, beta, act=2)

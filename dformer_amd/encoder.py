@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .decoders import _allreduce, _world
+from .decoders import _allreduce, bn_batch_stats
 from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, invalidate_weights
 
 _EMPTY = {}
@@ -175,11 +175,7 @@ class BNRowsFn(torch.autograd.Function):
         xr = x.permute(0, 2, 3, 1).contiguous().view(-1, C)
         rows = xr.shape[0]
         if bn.training:
-            st = _allreduce(K.bn_stats(xr), sync)
-            count = rows * _world(sync)
-            mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
-                                       bn.running_mean, bn.running_var)
-            bn.num_batches_tracked.add_(1)
+            mean, rstd, count = bn_batch_stats(xr, bn, sync)
         else:
             mean = bn.running_mean
             rstd = torch.rsqrt(bn.running_var + bn.eps)
@@ -199,11 +195,10 @@ class BNRowsFn(torch.autograd.Function):
         return dx.view(B, H, W, C).permute(0, 3, 1, 2), st2[1].clone(), st2[0].clone(), None, None
 
 
-# DFM_NATIVE_STEM_BN=1 runs the stem / downsample BatchNorms on BNRowsFn (≈0.5 ms/step faster than
-# MIOpen at DFormer-B bs16). Off by default: the library's BN statistics are one-pass fp32 sums
-# (var = E[x²] - E[x]²), and on the stem activations that cancellation moves the fp32 end-to-end
-# input-gradient golden (e2e_tiny_small) to 3.6e-3 against its 1e-3 gate; MIOpen's BN passes it.
-_NATIVE_STEM_BN = os.environ.get("DFM_NATIVE_STEM_BN", "0") == "1"
+# The stem / downsample BatchNorms run on BNRowsFn (the library's BN kernels, statistics as sums
+# shifted by the first row so the variance does not cancel); DFM_NATIVE_STEM_BN=0 selects torch's
+# BatchNorm (MIOpen) for A/B timing.
+_NATIVE_STEM_BN = os.environ.get("DFM_NATIVE_STEM_BN", "1") == "1"
 
 
 def _run_downsample(seq, x):

@@ -9,6 +9,8 @@ Reference semantics (file:line in Originofamonia/DFormer):
   ConvFFNFn     MLP.forward + Block residual/layer-scale/DropPath   DFormer.py:48-67, 173-179
   AttentionFn   Attention.forward + Block residuals                 DFormer.py:70-145, 168-179
 """
+import weakref
+
 import torch
 
 from . import kernels as K
@@ -52,19 +54,32 @@ _GSLOT = {}
 
 def register_grad_slot(p, flat, offset):
     """Weight gradients of `p` are written straight into flat[offset:offset+numel] (the optimizer's
-    flat gradient buffer); autograd then adopts that view as p.grad without a copy."""
-    _GSLOT[id(p)] = (flat, offset, tuple(p.shape))
+    flat gradient buffer); autograd then adopts that view as p.grad without a copy. The entry holds
+    a weak reference so a recycled id() of a dead parameter never aliases a live slot."""
+    _GSLOT[id(p)] = (flat, offset, tuple(p.shape), weakref.ref(p))
 
 
 def clear_grad_slots():
     _GSLOT.clear()
 
 
-def gslot(p):
+def _slot(p):
     s = _GSLOT.get(id(p))
+    if s is None or s[3]() is not p:
+        return None
+    return s
+
+
+def has_grad_slot(p):
+    """True while `p` belongs to a live FusedAdamW flat group (its gradients go to a flat slot)."""
+    return _slot(p) is not None
+
+
+def gslot(p):
+    s = _slot(p)
     if s is None:
         return None
-    flat, off, shape = s
+    flat, off, shape, _ = s
     n = 1
     for d in shape:
         n *= d

@@ -4,6 +4,8 @@ All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose la
 (the row stride is passed through as `ld`, so column slices of wider buffers work in place).
 Activations are float32 or bfloat16; statistics / params / param-grads are float32.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -15,22 +17,47 @@ _ws_cache = {}
 GEMM_TRACE = None
 
 
-class LaunchProbe:
-    """Brackets every GEMM launch of one shape/layout with HIP events on the launching stream
-    (bench.py's live roofline measurement of the dominant kernel inside the timed steps)."""
-
-    def __init__(self, M, N, K, a_kcontig, b_kcontig):
-        self.key = (M, N, K, int(a_kcontig), int(b_kcontig))
-        self.events = []
-
-    def mean_us(self):
-        if not self.events:
-            return None
-        self.events[-1][1].synchronize()
-        return sum(a.elapsed_time(b) for a, b in self.events) * 1e3 / len(self.events)
+# ---------------------------------------------------------------- accounting (bench.py)
+# When ACCOUNT is a list, every wrapper appends (kernel funcs launched, algorithmic FLOPs, algorithmic
+# HBM bytes, MFMA peak class) after its C call: the FLOPs/bytes an ideal kernel for that op must do
+# (inputs read once, outputs written once; workspaces and split-K partials are not algorithmic).
+# The library's launch tracer says which kernels the call enqueued; the first one is charged.
+ACCOUNT = None
+_FUNCS = (ctypes.c_void_p * 64)()
 
 
-GEMM_PROBE = None
+def trace(flags, probe=None):
+    """Launch tracer of the library: flags 0 off, 1 record launched kernels, 2 time (HIP events) the
+    kernel named `probe` (demangled, as rocprofv3 prints it; None = every kernel), 3 both."""
+    check(lib.dfm_trace_set(flags, probe.encode() if probe else None), "dfm_trace_set")
+
+
+def trace_read():
+    """[(kernel name, ms)] of the timed launches since the last read (synchronises on the last one)."""
+    cap = 1 << 16
+    funcs = (ctypes.c_void_p * cap)()
+    ms = (ctypes.c_float * cap)()
+    n = lib.dfm_trace_read(funcs, ms, cap)
+    return [(kernel_name(funcs[i]), float(ms[i])) for i in range(min(n, cap))]
+
+
+_NAMES = {}
+
+
+def kernel_name(func):
+    nm = _NAMES.get(func)
+    if nm is None:
+        nm = _NAMES[func] = lib.dfm_kernel_name(func).decode()
+    return nm
+
+
+def _acct(flops, nbytes, peak="bf16"):
+    n = lib.dfm_trace_take(_FUNCS, 64)
+    ACCOUNT.append((tuple(_FUNCS[i] for i in range(min(n, 64))), float(flops), float(nbytes), peak))
+
+
+def _es(t):
+    return t.element_size()
 
 
 def _ws(nbytes, dev):
@@ -72,16 +99,14 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
                           {"dtype": dt, "beta": d.beta, "out_f32": out.dtype == torch.float32})
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
-    probe = GEMM_PROBE
-    if probe is not None and probe.key == (M, N, K, int(a_kcontig), int(b_kcontig)):
-        s = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), s.cuda_stream), "dfm_gemm")
-        e1.record(s)
-        probe.events.append((e0, e1))
-        return out
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
+    if ACCOUNT is not None:
+        es, nb = _es(a), max(batch, 1)
+        byt = es * (M * K * nb + N * K * (nb if stride_b else 1))
+        byt += M * N * nb * (out.element_size() * (2 if beta != 0.0 else 1))
+        byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None))
+        byt += 4 * N * (bias is not None) + 4 * M * (colsum is not None)
+        _acct(2.0 * M * N * K * nb, byt, "bf16" if a.dtype != torch.float32 else "f32")
     return out
 
 
@@ -152,6 +177,8 @@ def layernorm(x, gamma, beta, eps=1e-6, out=None):
     rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
     check(lib.dfm_layernorm_fwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(gamma), ptr(beta), eps, ptr(out),
                                 ld(out), ptr(mean), ptr(rstd), stream()), "dfm_layernorm_fwd")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * 2 + 8 * rows)
     return out, mean, rstd
 
 
@@ -167,6 +194,8 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dres=None
     check(lib.dfm_layernorm_bwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(gamma), ptr(mean),
                                 ptr(rstd), ptr(dres), ld(dres) if dres is not None else 0, ptr(dx), ld(dx),
                                 int(accumulate), ptr(dg), ptr(db), ptr(ws), stream()), "dfm_layernorm_bwd")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * (3 + (dres is not None) + bool(accumulate)) + 8 * rows)
     return dx, dg, db
 
 
@@ -180,6 +209,8 @@ def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
     check(lib.dfm_residual_bwd(dtype_code(dout), rows, C, ptr(dout), ld(dout), ptr(f), ld(f), ptr(colscale),
                                ptr(rowscale), rows_per_scale, ptr(df), ld(df), ptr(dls), ptr(ws), stream()),
           "dfm_residual_bwd")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(dout) * 3)
     return df, dls
 
 
@@ -193,6 +224,8 @@ def dwconv(x, shape, w, bias, k, add_identity=False, out=None, gelu_out=None):
     check(lib.dfm_dwconv_fwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(w), ptr(bias), int(add_identity),
                              ptr(out), ld(out), ptr(gelu_out), ld(gelu_out) if gelu_out is not None else 0,
                              stream()), "dfm_dwconv_fwd")
+    if ACCOUNT is not None:
+        _acct(2 * k * k * C * x.shape[0], x.shape[0] * C * _es(x) * (2 + (gelu_out is not None)))
     return out
 
 
@@ -204,6 +237,8 @@ def dwconv_bwd_data(dy, shape, w, k, add_identity=False, dx=None, accumulate=Fal
         accumulate = False
     check(lib.dfm_dwconv_bwd_data(dtype_code(dy), B, H, W, C, k, ptr(dy), ld(dy), ptr(w), int(add_identity),
                                   ptr(dx), ld(dx), int(accumulate), stream()), "dfm_dwconv_bwd_data")
+    if ACCOUNT is not None:
+        _acct(2 * k * k * C * dy.shape[0], dy.shape[0] * C * _es(dy) * (2 + bool(accumulate)))
     return dx
 
 
@@ -217,6 +252,8 @@ def dwconv_bwd_weight(x, dy, shape, k, dw=None, db=None):
     ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
     check(lib.dfm_dwconv_bwd_weight(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(dw), ptr(db),
                                     ptr(ws), stream()), "dfm_dwconv_bwd_weight")
+    if ACCOUNT is not None:
+        _acct(2 * k * k * C * x.shape[0], x.shape[0] * C * _es(x) * 2)
     return dw, db
 
 
@@ -229,6 +266,8 @@ def colsum(x, mul=None, rowscale=None, rows_per_scale=1, out=None, accumulate=Fa
     ws = _ws(lib.dfm_colsum_workspace(rows, C), x.device)
     check(lib.dfm_colsum(dtype_code(x), rows, C, ptr(x), ld(x), ptr(mul), ld(mul) if mul is not None else 0,
                          ptr(rowscale), rows_per_scale, ptr(out), int(accumulate), ptr(ws), stream()), "dfm_colsum")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * (1 + (mul is not None)))
     return out
 
 
@@ -237,6 +276,8 @@ def cast(x, dtype, out=None):
         out = torch.empty(x.shape, device=x.device, dtype=dtype)
     assert x.is_contiguous() and out.is_contiguous()
     check(lib.dfm_cast(dtype_code(x), dtype_code(out), x.numel(), ptr(x), ptr(out), stream()), "dfm_cast")
+    if ACCOUNT is not None:
+        _acct(0, x.numel() * (_es(x) + _es(out)))
     return out
 
 
@@ -247,6 +288,8 @@ def gelu_bwd(dy, pre, out=None, accumulate=False):
         accumulate = False
     check(lib.dfm_gelu_bwd(dtype_code(dy), rows, C, ptr(dy), ld(dy), ptr(pre), ld(pre), ptr(out), ld(out),
                            int(accumulate), stream()), "dfm_gelu_bwd")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(dy) * (3 + bool(accumulate)))
     return out
 
 
@@ -256,6 +299,8 @@ def relu_bwd(dy, y, out=None):
         out = torch.empty(rows, C, device=dy.device, dtype=dy.dtype)
     check(lib.dfm_relu_bwd(dtype_code(dy), rows, C, ptr(dy), ld(dy), ptr(y), ld(y), ptr(out), ld(out), stream()),
           "dfm_relu_bwd")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(dy) * 3)
     return out
 
 
@@ -267,6 +312,8 @@ def scale_mul(src, mul=None, colscale=None, rowscale=None, rows_per_scale=1, alp
     check(lib.dfm_scale_mul(dtype_code(src), rows, C, ptr(src), ld(src), ptr(mul), ld(mul) if mul is not None else 0,
                             ptr(colscale), ptr(rowscale), rows_per_scale, alpha, ptr(out), ld(out), int(accumulate),
                             stream()), "dfm_scale_mul")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(src) * (2 + (mul is not None) + bool(accumulate)))
     return out
 
 
@@ -278,6 +325,8 @@ def pool7(x, shape, out=None):
         out = torch.empty(B * 49, C, device=x.device, dtype=x.dtype)
     check(lib.dfm_adaptive_pool7_fwd(dtype_code(x), B, H, W, C, ptr(x), ld(x), ptr(out), ld(out), stream()),
           "dfm_adaptive_pool7_fwd")
+    if ACCOUNT is not None:
+        _acct(0, (B * H * W + B * 49) * C * _es(x))
     return out
 
 
@@ -289,6 +338,8 @@ def pool7_bwd(dy, shape, dx=None, accumulate=False):
         accumulate = False
     check(lib.dfm_adaptive_pool7_bwd(dtype_code(dy), B, H, W, C, ptr(dy), ld(dy), ptr(dx), ld(dx), int(accumulate),
                                      stream()), "dfm_adaptive_pool7_bwd")
+    if ACCOUNT is not None:
+        _acct(0, (B * H * W * (1 + bool(accumulate)) + B * 49) * C * _es(dy))
     return dx
 
 
@@ -300,6 +351,8 @@ def bilinear(x, in_hw, out_hw, B, out=None, accumulate=False):
         accumulate = False
     check(lib.dfm_bilinear_fwd(dtype_code(x), B, Hi, Wi, Ho, Wo, C, ptr(x), ld(x), ptr(out), ld(out),
                                int(accumulate), stream()), "dfm_bilinear_fwd")
+    if ACCOUNT is not None:
+        _acct(0, (B * Hi * Wi + B * Ho * Wo * (1 + bool(accumulate))) * C * _es(x))
     return out
 
 
@@ -311,6 +364,8 @@ def bilinear_bwd(dy, in_hw, out_hw, B, dx=None, accumulate=False):
         accumulate = False
     check(lib.dfm_bilinear_bwd(dtype_code(dy), B, Hi, Wi, Ho, Wo, C, ptr(dy), ld(dy), ptr(dx), ld(dx),
                                int(accumulate), stream()), "dfm_bilinear_bwd")
+    if ACCOUNT is not None:
+        _acct(0, (B * Hi * Wi * (1 + bool(accumulate)) + B * Ho * Wo) * C * _es(dy))
     return dx
 
 
@@ -323,6 +378,8 @@ def pooled_attn(q, k, v, B, heads, N, dh, scale, out=None):
     assert ld(k) == ld(v)
     check(lib.dfm_pooled_attn_fwd(dtype_code(q), B, heads, N, dh, ptr(q), ld(q), ptr(k), ptr(v), ld(k), scale,
                                   ptr(out), ld(out), ptr(lse), ptr(ws), stream()), "dfm_pooled_attn_fwd")
+    if ACCOUNT is not None:
+        _acct(4.0 * B * heads * 49 * N * dh, _es(q) * (2 * B * 49 * heads * dh + 2 * B * N * heads * dh))
     return out, lse
 
 
@@ -332,14 +389,20 @@ def pooled_attn_bwd(q, k, v, o, dout, lse, B, heads, N, dh, scale, dq, dk, dv):
     check(lib.dfm_pooled_attn_bwd(dtype_code(q), B, heads, N, dh, ptr(q), ld(q), ptr(k), ptr(v), ld(k), scale,
                                   ptr(o), ld(o), ptr(dout), ld(dout), ptr(lse), ptr(dq), ptr(dk), ptr(dv), ld(dk),
                                   ptr(ws), stream()), "dfm_pooled_attn_bwd")
+    if ACCOUNT is not None:
+        hd = heads * dh
+        _acct(10.0 * B * heads * 49 * N * dh, _es(q) * (4 * B * 49 * hd + 4 * B * N * hd))
 
 
 # ---------------------------------------------------------------------------------- BatchNorm
 def bn_stats(x):
+    """float32 [3, C]: (sum (x-K), sum (x-K)^2, K) with the per-column shift K = x[0]."""
     rows, C = x.shape
-    st = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    st = torch.empty(3, C, device=x.device, dtype=torch.float32)
     ws = _ws(lib.dfm_bn_workspace(rows, C), x.device)
     check(lib.dfm_bn_stats(dtype_code(x), rows, C, ptr(x), ld(x), ptr(st), ptr(ws), stream()), "dfm_bn_stats")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x))
     return st
 
 
@@ -359,6 +422,8 @@ def bn_apply(x, mean, rstd, gamma, beta, res=None, act=0, out=None):
     check(lib.dfm_bn_apply(dtype_code(x), rows, C, ptr(x), ld(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
                            ptr(res), ld(res) if res is not None else 0, act, ptr(out), ld(out), stream()),
           "dfm_bn_apply")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * (2 + (res is not None)))
     return out
 
 
@@ -368,6 +433,8 @@ def bn_bwd_stats(x, dy, mean, rstd):
     ws = _ws(lib.dfm_bn_workspace(rows, C), x.device)
     check(lib.dfm_bn_bwd_stats(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(mean), ptr(rstd),
                                ptr(st), ptr(ws), stream()), "dfm_bn_bwd_stats")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * 2)
     return st
 
 
@@ -379,6 +446,8 @@ def bn_bwd_apply(x, dy, mean, rstd, gamma, stats2, count, dx=None, accumulate=Fa
     check(lib.dfm_bn_bwd_apply(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(mean), ptr(rstd),
                                ptr(gamma), ptr(stats2), float(count), ptr(dx), ld(dx), int(accumulate), stream()),
           "dfm_bn_bwd_apply")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * (3 + bool(accumulate)))
     return dx
 
 
@@ -387,6 +456,8 @@ def nmf_update(a, num, den, eps=1e-6, out=None):
     if out is None:
         out = torch.empty_like(a)
     check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), stream()), "dfm_nmf_update")
+    if ACCOUNT is not None:
+        _acct(0, a.numel() * 16)
     return out
 
 
@@ -398,12 +469,16 @@ def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6):
     gden = torch.empty_like(a)
     check(lib.dfm_nmf_update_bwd(a.numel(), ptr(g), ptr(a), ptr(num), ptr(den), ptr(out), eps, ptr(ga),
                                  int(accumulate), ptr(gnum), ptr(gden), stream()), "dfm_nmf_update_bwd")
+    if ACCOUNT is not None:
+        _acct(0, a.numel() * 4 * (8 + bool(accumulate)))
     return ga, gnum, gden
 
 
 def softmax_rows(x):
     y = torch.empty_like(x)
     check(lib.dfm_softmax_rows(x.numel() // x.shape[-1], x.shape[-1], ptr(x), ptr(y), stream()), "dfm_softmax_rows")
+    if ACCOUNT is not None:
+        _acct(0, x.numel() * 8)
     return y
 
 
@@ -413,6 +488,8 @@ def softmax_rows_bwd(y, dy, dx=None, accumulate=False):
         accumulate = False
     check(lib.dfm_softmax_rows_bwd(y.numel() // y.shape[-1], y.shape[-1], ptr(y), ptr(dy), ptr(dx), int(accumulate),
                                    stream()), "dfm_softmax_rows_bwd")
+    if ACCOUNT is not None:
+        _acct(0, y.numel() * 4 * (3 + bool(accumulate)))
     return dx
 
 
@@ -423,6 +500,8 @@ def seg_loss_fwd(logits, B, h, w, ncls, label, ignore=255):
     ws = _ws(lib.dfm_seg_loss_workspace(B, H, W), logits.device)
     check(lib.dfm_seg_loss_fwd(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore, None,
                                ptr(out), ptr(ws), stream()), "dfm_seg_loss_fwd")
+    if ACCOUNT is not None:
+        _acct(0, logits.numel() * _es(logits) + label.numel() * 8)
     return out
 
 
@@ -431,6 +510,8 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
     dl = torch.empty(B * h * w, ncls, device=logits.device, dtype=torch.float32)
     check(lib.dfm_seg_loss_bwd(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore, None,
                                ptr(loss_out), ptr(gscale), ptr(dl), stream()), "dfm_seg_loss_bwd")
+    if ACCOUNT is not None:
+        _acct(0, logits.numel() * (_es(logits) + 4) + label.numel() * 8)
     return dl
 
 
@@ -438,3 +519,5 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
 def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None):
     check(lib.dfm_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), lr, beta1, beta2, eps, weight_decay, step,
                         grad_scale, ptr(bf16_copy), stream()), "dfm_adamw")
+    if ACCOUNT is not None:
+        _acct(0, p.numel() * (28 + (2 if bf16_copy is not None else 0)))

@@ -18,6 +18,22 @@ BACKBONES = {"DFormer-Tiny": (DFormer_Tiny, [32, 64, 128, 256]), "DFormer-Small"
              "DFormer-Base": (DFormer_Base, [64, 128, 256, 512]), "DFormer-Large": (DFormer_Large, [96, 192, 288, 576])}
 
 
+def _check_criterion(criterion, ignore_index):
+    """The loss is the fused kernel of builder.py:203,230: unweighted CrossEntropyLoss(reduction='none',
+    ignore_index=cfg.background) followed by the mean over valid pixels (what train.py:189-194
+    passes). Anything else would be silently ignored, so it is rejected."""
+    if criterion is None:
+        return
+    ok = (isinstance(criterion, nn.CrossEntropyLoss) and criterion.weight is None and
+          criterion.reduction == "none" and criterion.ignore_index == ignore_index and
+          float(getattr(criterion, "label_smoothing", 0.0)) == 0.0)
+    if not ok:
+        raise NotImplementedError(
+            f"EncoderDecoder: the fused segmentation loss implements CrossEntropyLoss(reduction='none', "
+            f"ignore_index={ignore_index}) without class weights or label smoothing (utils/train.py:189-194); "
+            f"got {criterion!r}")
+
+
 class EncoderDecoder(nn.Module):
     def __init__(self, cfg=None, criterion=None, norm_layer=nn.BatchNorm2d, syncbn=False):
         super().__init__()
@@ -40,6 +56,7 @@ class EncoderDecoder(nn.Module):
         else:
             raise NotImplementedError(f"decoder {cfg.decoder!r} is outside the hot path (SURVEY.md §2)")
         self.aux_head = None
+        _check_criterion(criterion, getattr(cfg, "background", 255))
         self.criterion = criterion
         self.ignore_index = getattr(cfg, "background", 255)
         self.return_logits = True

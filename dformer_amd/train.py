@@ -103,6 +103,7 @@ class GradBuckets:
                 self._add(g, members, start)
         self.pending = [len(b[1]) for b in self.buckets]
         self.copies = [[] for _ in self.buckets]
+        self.fired = set()  # ids of parameters whose gradient arrived this step
         for p in self.owner:
             p.register_post_accumulate_grad_hook(self._hook)
 
@@ -119,6 +120,7 @@ class GradBuckets:
         if p.grad.data_ptr() != g.grad.data_ptr() + 4 * off:  # kernels usually wrote the slot directly
             self.copies[bi].append((g.grad[off:off + k], p.grad.reshape(-1)))
         p.grad = None
+        self.fired.add(id(p))
         self.pending[bi] -= 1
         if self.pending[bi] == 0:
             self._flush(bi)
@@ -134,15 +136,24 @@ class GradBuckets:
             self.copies[bi] = []
 
     def finish(self):
-        # buckets with a parameter that got no gradient this step (unused branch): reduce them now
+        """Join the step's all-reduces. Buckets holding a parameter that got no gradient this step
+        (an unused branch) are completed here: the slots of such parameters are zeroed first (they
+        still hold the previous step's gradient, and torch's AdamW after zero_grad() would see no
+        gradient either), then the bucket is reduced like the others."""
         for bi, b in enumerate(self.buckets):
-            if 0 < self.pending[bi] < len(b[1]) or (self.pending[bi] == len(b[1]) and self.copies[bi]):
+            if self.pending[bi] > 0:
+                for p in b[1]:
+                    if id(p) not in self.fired:
+                        g = self.owner[p][1]
+                        off, k = g.slots[p]
+                        g.grad[off:off + k].zero_()
                 self._flush(bi)
                 if self.world > 1:
                     self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
             h.wait()
         self.handles = []
+        self.fired = set()
         self.pending = [len(b[1]) for b in self.buckets]
 
 

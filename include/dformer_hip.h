@@ -39,6 +39,20 @@ typedef void* dfm_stream_t;
 const char* dfm_last_error(void);
 int dfm_abi_version(void);
 
+/* ---------------------------------------------------------------- launch tracer (measurement)
+ * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
+ * recorded (dfm_trace_take returns and clears them: the kernels one entry point launched);
+ * DFM_TRACE_TIME: launches of the kernel whose demangled name is `probe_name` (NULL or "" = every
+ * kernel) are bracketed by HIP events on their own stream; dfm_trace_read synchronises on the last
+ * event and returns per-launch milliseconds. dfm_kernel_name: the demangled name rocprofv3 prints.
+ * Used by bench.py (per-kernel FLOP/byte accounting and the dominant kernel's live roofline). */
+#define DFM_TRACE_RECORD 1
+#define DFM_TRACE_TIME 2
+int dfm_trace_set(int flags, const char* probe_name);
+int dfm_trace_take(const void** funcs, int max);
+int dfm_trace_read(const void** funcs, float* ms, int max);
+const char* dfm_kernel_name(const void* func);
+
 /* ---------------------------------------------------------------- GEMM (MFMA)
  * C[b][m][n] = epilogue( alpha * sum_k A(b,m,k) * B(b,k,n) )
  *   A(m,k) = A[m*lda + k] if a_kcontig else A[k*lda + m]
@@ -171,8 +185,10 @@ int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, const void* 
 
 /* ---------------------------------------------------------------- BatchNorm (+ SyncBN stats)
  * mmcv ConvModule norm / nn.BatchNorm2d / SyncBatchNorm over NHWC rows (ham_head.py:204-220,
- * MLPDecoder.py:53). stats: float32 [2][C] = (sum, sumsq) to be all-reduced by the caller for
- * SyncBN. apply: y = act((x - mean) * rstd * gamma + beta) [+ res] ; mean/rstd float32 [C]. */
+ * MLPDecoder.py:53). stats: float32 [3][C] = (sum (x-K), sum (x-K)^2, K) with the shift K = x[row 0]
+ * (no E[x^2]-E[x]^2 cancellation when |mean| >> std); finalize: mean = K + S1/n,
+ * var = S2/n - (S1/n)^2. For SyncBN the caller merges per-rank (n, mean, M2) (Chan) into
+ * (0, M2, mean). apply: y = act((x - mean) * rstd * gamma + beta) [+ res] ; mean/rstd float32 [C]. */
 size_t dfm_bn_workspace(long rows, int C);
 int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx, float* stats, void* workspace,
                  dfm_stream_t stream);

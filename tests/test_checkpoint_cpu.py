@@ -145,3 +145,33 @@ def test_pretrained_backbone_prefixes_and_freeze(tmp_path):
         for n, prm in dst.named_parameters():
             loaded = any(n == k or n.startswith(k + ".") for k in part)
             assert prm.requires_grad == (not loaded) or "stem_e_fc" in n, n
+
+
+def test_freeze_after_optimizer_is_rejected():
+    """load_pretrained_backbone(freeze=True) must not silently leave frozen parameters inside a live
+    FusedAdamW (the reference freezes in the constructor, before the optimizer exists)."""
+    import pytest
+    torch.manual_seed(0)
+    net = _Net()
+    opt = FusedAdamW(net, compute_dtype=torch.float32)
+    with pytest.raises(RuntimeError, match="after FusedAdamW"):
+        ckpt.load_pretrained_backbone(net, {"state_dict": {k: v.clone() for k, v in net.state_dict().items()}})
+    assert all(p.requires_grad for p in (net.fc.weight, net.conv.weight))
+    del opt
+    net2 = _Net()  # load + freeze first, then build the optimizer: fine
+    ckpt.load_pretrained_backbone(net2, {"state_dict": {k: v.clone() for k, v in net.state_dict().items()}})
+    assert not net2.fc.weight.requires_grad
+
+
+def test_segmentor_rejects_unsupported_criterion():
+    import pytest
+    import bench
+    from dformer_amd.segmentor import EncoderDecoder
+    cfg = bench.make_cfg("DFormer-Tiny", "ham")
+    EncoderDecoder(cfg=cfg, criterion=nn.CrossEntropyLoss(reduction="none", ignore_index=255))
+    for bad in (nn.CrossEntropyLoss(weight=torch.ones(40), reduction="none", ignore_index=255),
+                nn.CrossEntropyLoss(reduction="mean", ignore_index=255),
+                nn.CrossEntropyLoss(reduction="none", ignore_index=0),
+                nn.CrossEntropyLoss(reduction="none", ignore_index=255, label_smoothing=0.1)):
+        with pytest.raises(NotImplementedError):
+            EncoderDecoder(cfg=cfg, criterion=bad)

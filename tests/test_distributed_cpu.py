@@ -37,10 +37,12 @@ class _Net(nn.Module):
         self.fc1 = nn.Linear(8, 16)
         self.fc2 = nn.Linear(16, 5, bias=False)
         self.ln = nn.LayerNorm(16)
+        self.extra = nn.Linear(5, 5)  # an unused branch in odd steps (its slots must be zeroed)
 
-    def forward(self, x):
+    def forward(self, x, use_extra=True):
         y = torch.relu(self.bn(self.conv(x))).mean(dim=(2, 3))
-        return self.fc2(self.ln(torch.relu(self.fc1(y))))
+        out = self.fc2(self.ln(torch.relu(self.fc1(y))))
+        return out + self.extra(out) if use_extra else out
 
 
 def _worker(rank, world, port, bucket_bytes, q):
@@ -56,20 +58,22 @@ def _worker(rank, world, port, bucket_bytes, q):
         groups = [_FlatGroup(decay, 0.01, "cpu", torch.float32), _FlatGroup(no_decay, 0.0, "cpu", torch.float32)]
         buckets = GradBuckets(groups, world, bucket_bytes)
         ok = True
-        for step in range(2):
+        for step in range(3):
             g = torch.Generator().manual_seed(100 * rank + step)
             x = torch.randn(4, 3, 6, 7, generator=g)
-            # local reference gradients (a parameter copy, no hooks)
+            use_extra = step != 1
+            # local reference gradients (a parameter copy, no hooks); no gradient = zeros
             ref = _Net()
             ref.load_state_dict(net.state_dict())
-            ref(x).square().mean().backward()
-            local = {n: p.grad.detach().clone() for n, p in ref.named_parameters()}
+            ref(x, use_extra).square().mean().backward()
+            local = {n: (p.grad.detach().clone() if p.grad is not None else torch.zeros_like(p))
+                     for n, p in ref.named_parameters()}
             summed = {n: t.clone() for n, t in local.items()}
             for t in summed.values():
                 dist.all_reduce(t)
-            for gr in groups:
-                gr.grad.zero_()
-            net(x).square().mean().backward()
+            # no manual zeroing of the flat buffer: finish() must clear the slots of parameters
+            # whose gradient did not arrive (the `extra` branch in step 1)
+            net(x, use_extra).square().mean().backward()
             buckets.finish()
             names = {id(p): n for n, p in net.named_parameters()}
             for gr in groups:
@@ -117,3 +121,104 @@ def test_group_weight_reference_groups():
     left = [(n, p) for n, p in model.named_parameters() if id(p) not in grouped]
     assert all("layer_scale" in n or ".norm" in n for n, _ in left), [n for n, _ in left][:5]
     assert len(left) == 236 and sum(p.numel() for _, p in left) == 41024
+
+
+def _real_model_worker(rank, world, port, q):
+    """GradBuckets over the real DFormer-B + ham parameter set (CPU tensors, gloo): bucket
+    membership and order, the summed gradients, and parameters that got no gradient."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from dformer_amd.functional import clear_grad_slots
+        from dformer_amd.segmentor import EncoderDecoder
+        from dformer_amd.train import GradBuckets, _FlatGroup, group_weight
+        torch.manual_seed(0)
+        model = EncoderDecoder(cfg=bench.make_cfg("DFormer-Base", "ham"))
+        decay, no_decay = group_weight(model)
+        groups = [_FlatGroup(decay, 0.01, "cpu", torch.float32), _FlatGroup(no_decay, 0.0, "cpu", torch.float32)]
+        buckets = GradBuckets(groups, world)
+        ok = []
+        # membership: every grouped parameter in exactly one bucket; buckets are contiguous slices
+        members = [p for _, ps in buckets.buckets for p in ps]
+        ok.append(len(members) == len(set(map(id, members))) == sum(len(g.slots) for g in groups))
+        for t, ps in buckets.buckets:
+            g = buckets.owner[next(iter(ps))][1]
+            lo = min(g.slots[p][0] for p in ps)
+            hi = max(g.slots[p][0] + g.slots[p][1] for p in ps)
+            ok.append(t.numel() == hi - lo == sum(g.slots[p][1] for p in ps))
+            ok.append(t.numel() * 4 <= (25 << 20) + max(g.slots[p][1] for p in ps) * 4)
+        # order: reverse registration within a group (the first bucket holds the last parameters)
+        first = buckets.buckets[0][1]
+        g0 = groups[0]
+        ok.append(max(g0.slots[p][0] for p in g0.params) in {g0.slots[p][0] for p in first})
+        # one backward: a per-rank random gradient for every grouped parameter except the decoder's
+        # conv_seg (no gradient this step -> its slots, pre-filled with garbage, must come out zero)
+        names = {id(p): n for n, p in model.named_parameters()}
+        for g in groups:
+            g.grad.fill_(7.0)
+        skip = {id(model.decode_head.conv_seg.weight), id(model.decode_head.conv_seg.bias)}
+        gen = torch.Generator().manual_seed(rank + 1)
+        loss = 0.0
+        want = {}
+        for g in groups:
+            for p in g.params:
+                if id(p) in skip:
+                    want[id(p)] = torch.zeros_like(p)
+                    continue
+                gp = torch.randn(p.shape, generator=gen)
+                want[id(p)] = gp.clone()
+                loss = loss + (p * gp).sum()
+        for t in want.values():
+            dist.all_reduce(t)
+        loss.backward()
+        buckets.finish()
+        bad = []
+        for g in groups:
+            for p, (off, k) in g.slots.items():
+                if not torch.allclose(g.grad[off:off + k].view_as(p), want[id(p)], rtol=1e-5, atol=1e-5):
+                    bad.append(names[id(p)])
+        ok.append(not bad)
+        q.put((rank, all(ok), bad[:5], len(buckets.buckets)))
+        clear_grad_slots()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_buckets_real_model_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_real_model_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _, _ in res), res
+    assert len({n for *_, n in res}) == 1 and res[0][3] >= 4  # 119 MB fp32 of grads in ~25 MB buckets
+
+
+def test_syncbn_merge_matches_full_batch():
+    """SyncBN's Chan merge of per-shard shifted sums (decoders.merge_bn_stats) = full-batch
+    statistics, for uneven shards and |mean| >> std."""
+    from dformer_amd.decoders import merge_bn_stats
+    torch.manual_seed(0)
+    C = 24
+    x = torch.randn(5000, C, dtype=torch.float64) * 0.3 + torch.linspace(-50, 80, C, dtype=torch.float64)
+    cuts = [0, 700, 2900, 5000]
+    parts, counts = [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        xs = x[a:b]
+        k = xs[0]
+        d = xs - k
+        parts.append(torch.stack([d.sum(0), (d * d).sum(0), k]).float())
+        counts.append(b - a)
+    st = merge_bn_stats(torch.stack(parts), torch.tensor(counts, dtype=torch.float32)).double()
+    n = x.shape[0]
+    mean = st[2] + st[0] / n
+    var = st[1] / n - (st[0] / n) ** 2
+    assert torch.allclose(mean, x.mean(0), rtol=1e-6, atol=1e-5)
+    assert torch.allclose(var, x.var(0, unbiased=False), rtol=1e-4, atol=1e-6)

@@ -365,6 +365,25 @@ def test_batchnorm(dt):
     assert rel(st2[0], br.grad) < TOL[dt] * 2
 
 
+@pytest.mark.parametrize("C", [16, 32, 512])
+def test_batchnorm_shifted_stats_large_offset(C):
+    """|mean| >> std over ~1M rows (the cancellation regime of one-pass E[x^2]-E[x]^2): the
+    shifted statistics must still give torch's fp32 batch_norm mean / variance / output."""
+    k = K()
+    rows = (1 << 20) if C <= 32 else (1 << 17)
+    mu = torch.linspace(-300, 300, C, device=DEV)
+    x = torch.randn(rows, C, device=DEV) * 0.5 + mu
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, rstd = k.bn_finalize(k.bn_stats(x), rows, 1e-5, 0.1, rm, rv)
+    xd = x.double()
+    assert rel(mean, xd.mean(0)) < 1e-6
+    assert rel(1.0 / rstd.double() ** 2 - 1e-5, xd.var(0, unbiased=False)) < 1e-3
+    g, b = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    y = k.bn_apply(x, mean, rstd, g, b)
+    ref = (xd - xd.mean(0)) / torch.sqrt(xd.var(0, unbiased=False) + 1e-5)
+    assert rel(y.double(), ref) < 1e-3
+
+
 def test_nmf_update_softmax():
     k = K()
     a, num, den = (torch.rand(4, 100, 64, device=DEV) for _ in range(3))

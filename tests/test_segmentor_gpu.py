@@ -99,10 +99,14 @@ def test_nmf2d_vs_reference(train):
 
 @pytest.mark.gpu
 def test_ham_head_vs_reference():
+    """LightHamHead fwd + bwd vs the reference (fp64 golden) at 1e-3. The golden's inputs were drawn
+    (oracle/make_goldens.py golden_ham) so that every ReLU input is >= 1e-5 x max away from the
+    kink: the fp32 HIP path then takes the same activation pattern as fp64 everywhere."""
     from dformer_amd.decoders import LightHamHead
     name = "ham_tiny"
     g = load(name)
-    B, H, W, ncls, train, *in_ch = [int(v) for v in g["meta"]]
+    B, H, W, ncls, train, seed, *in_ch = [int(v) for v in g["meta"]]
+    tag = f"{name}#{seed}"
     head = LightHamHead(in_channels=in_ch, num_classes=ncls, channels=512, norm_cfg=dict(type="BN"))
     head.dropout_ratio = 0.0
     sd = head.state_dict()
@@ -111,29 +115,18 @@ def test_ham_head_vs_reference():
     head = head.cuda().train()
     from dformer_amd.functional import invalidate_weights
     invalidate_weights()
-    head.hamburger.ham.injected_bases = torch.from_numpy(gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
-    feats = [torch.from_numpy(gen.normal(name + f"/f{i}", (B, c, H >> i, W >> i))).float().cuda()
+    head.hamburger.ham.injected_bases = torch.from_numpy(gen.nmf_bases(B, 512, 64, name=tag + "/bases")).float()
+    feats = [torch.from_numpy(gen.normal(tag + f"/f{i}", (B, c, H >> i, W >> i))).float().cuda()
              for i, c in enumerate(in_ch)]
     leaves = [f.permute(0, 2, 3, 1).contiguous().requires_grad_() for f in feats]
     y = head([None] + [t.permute(0, 3, 1, 2) for t in leaves])
-    gy = torch.from_numpy(gen.normal(name + "/gy", tuple(y.shape))).float().cuda()
+    gy = torch.from_numpy(gen.normal(tag + "/gy", tuple(y.shape))).float().cuda()
     y.backward(gy)
     assert rel_err(y.detach().cpu(), g["y"]) < 1e-3
-    # The forward and the gradients ahead of the Hamburger's output ReLU are well-posed: 1e-3.
-    # Behind it the check is ill-conditioned for this case: relu(x + BN(ham_out(.))) has inputs
-    # within fp32 rounding of the kink, so a 1e-7 relative perturbation of the decoder input
-    # (rounding of the resize kernels, or HAM_PERTURB in tools/ham_debug.py) flips 1-2 of its
-    # 196,608 outputs (tools/ham_compare.py), and through the train-mode BatchNorm backward one
-    # flip moves every gradient behind it by 0.1-2 %: gated at 5e-2 there.
-    behind = 5e-2
     for i, t in enumerate(leaves):
-        assert rel_err(t.grad.permute(0, 3, 1, 2).cpu(), g[f"gf{i + 1}"]) < behind
+        assert rel_err(t.grad.permute(0, 3, 1, 2).cpu(), g[f"gf{i + 1}"]) < 1e-3, i
     grads = {k: p.grad.cpu() for k, p in head.named_parameters() if p.grad is not None}
-    ahead = ("conv_seg.", "align.")
-    check_param_grads({k: v for k, v in g.items() if k.split("/", 1)[-1].startswith(ahead)}, grads, 2e-3,
-                      atol=1e-6)
-    check_param_grads({k: v for k, v in g.items() if not k.split("/", 1)[-1].startswith(ahead)}, grads, behind,
-                      atol=1e-6)
+    check_param_grads(g, grads, 1e-3, atol=1e-6)
     for k, v in g.items():
         if k.startswith("buf/"):
             assert rel_err(dict(head.named_buffers())[k[4:]].cpu(), v) < 1e-4
@@ -183,3 +176,103 @@ def test_train_step_bf16_runs_and_decreases_loss():
     losses = [train_step(model, opt, rgb, dep, lab).item() for _ in range(8)]
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.gpu
+def test_tiny_full_480x640_fp32_vs_reference():
+    """BASELINE config 1 shape on the HIP path: DFormer-Tiny + ham forward at 2x3x480x640 (+ depth),
+    fp32, against the reference's fp64 fingerprints (sum, abs-sum, l2, 64 strided samples) of the
+    four encoder maps, the 1/8 logits and the full-resolution upsampled logits, gate 1e-3."""
+    name = "e2e_tiny_full_fwd"
+    g = load(name)
+    B, H, W, ncls = [int(v) for v in g["meta"]]
+    model = build("DFormer-Tiny", "ham", ncls, "cuda").train()
+    model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
+        gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
+    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb = torch.from_numpy(rgb_np).float().cuda()
+    dep = torch.from_numpy(dep_np).float().cuda()
+    with torch.no_grad():
+        feats = model.encoder_backbone(rgb, dep)[0]
+        low = model.decode_head(feats)
+        out = model._upsample(low, (H, W))
+    torch.cuda.synchronize()
+    errs = {f"feat{i}": fp_rel_err(gen.fingerprint(f.double().cpu().numpy()), g[f"feat{i}_fp"])
+            for i, f in enumerate(feats)}
+    errs["low"] = fp_rel_err(gen.fingerprint(low.double().cpu().numpy()), g["low_fp"])
+    errs["out"] = fp_rel_err(gen.fingerprint(out.double().cpu().numpy()), g["out_fp"])
+    assert max(errs.values()) < 1e-3, errs
+
+
+# bf16 end-to-end gates, relative to the reference's OWN bf16 autocast error on the same golden
+# (tests/golden/bf16env_*.npz, oracle/make_goldens.py golden_bf16_env; SURVEY §8c: the reference's
+# autocast misses a flat 1e-2 logits gate by itself — 1.0-2.1e-2 here, and a median 2-7e-2 on the
+# parameter-gradient fingerprints). The HIP path keeps LayerNorm / BatchNorm / softmax / NMF state in
+# fp32 but, unlike autocast, also stores the residual stream in bf16; measured on MI355X it lands at
+# 1.01-1.18x the reference's own error. Gates:
+BF16_LOW = 1.25     # logits rel-to-max  <= 1.25 x reference autocast
+BF16_LOSS = 1e-3    # |loss - golden| / golden  (the reference's own is ~1e-5)
+BF16_GRAD_MED = 1.25  # median over parameters of the gradient-fingerprint error <= 1.25 x the reference's
+BF16_GRAD_P = 2.0   # every parameter: error <= max(2 x the reference's error on it, 0.1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,arch,dec,ncls", E2E)
+def test_segmentor_bf16_vs_reference_envelope(name, arch, dec, ncls):
+    g = load(name)
+    env = load("bf16env_" + name)
+    B, H, W, _ = [int(v) for v in g["meta"]]
+    model = build(arch, dec, ncls, "cuda").set_compute_dtype(torch.bfloat16)
+    model.train()
+    if dec == "ham":
+        model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
+            gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
+    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb = torch.from_numpy(rgb_np).float().cuda().requires_grad_()
+    dep = torch.from_numpy(dep_np).float().cuda().requires_grad_()
+    lab = torch.from_numpy(gen.labels(B, H, W, ncls)).cuda()
+    feats = model.encoder_backbone(rgb, dep)[0]
+    low = model.decode_head(feats)
+    from dformer_amd.decoders import SegLossFn, _nhwc_rows
+    rows, (b, h, w) = _nhwc_rows(low)
+    loss = SegLossFn.apply(rows.contiguous(), b, h, w, lab, 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    e_low = rel_err(low.float().cpu(), g["low"])
+    assert e_low <= BF16_LOW * float(env["env/low"]), (e_low, float(env["env/low"]))
+    assert abs(loss.item() - float(g["loss"])) <= BF16_LOSS * abs(float(g["loss"]))
+    params = dict(model.named_parameters())
+    ours, refs, bad = [], [], []
+    for k, v in g.items():
+        if not k.startswith("gfp/"):
+            continue
+        e = fp_rel_err(gen.fingerprint(params[k[4:]].grad.double().cpu().numpy(), 16), v, atol=1e-4)
+        r = float(env["env/" + k])
+        ours.append(e)
+        refs.append(r)
+        if e > max(BF16_GRAD_P * r, 0.1):
+            bad.append((k[4:], round(e, 4), round(r, 4)))
+    assert np.median(ours) <= BF16_GRAD_MED * np.median(refs), (np.median(ours), np.median(refs))
+    assert not bad, bad[:8]
+
+
+@pytest.mark.gpu
+def test_syncbn_two_half_batches_equal_full_batch():
+    """SyncBN statistics as the DP path forms them: the library's shifted (sum, sumsq, shift) of two
+    half-batches, Chan-merged (decoders.merge_bn_stats), finalize to the full batch's mean / var."""
+    from dformer_amd import kernels as K
+    from dformer_amd.decoders import merge_bn_stats
+    torch.manual_seed(0)
+    x = (torch.randn(60000, 128, device="cuda") * 0.7 + torch.linspace(-20, 40, 128, device="cuda"))
+    halves = [x[:26000], x[26000:]]
+    parts = torch.stack([K.bn_stats(h) for h in halves])
+    st = merge_bn_stats(parts, torch.tensor([26000.0, 34000.0], device="cuda"))
+    rm, rv = torch.zeros(128, device="cuda"), torch.ones(128, device="cuda")
+    mean, rstd = K.bn_finalize(st, 60000, 1e-5, 0.1, rm, rv)
+    full_mean, full_rstd = K.bn_finalize(K.bn_stats(x), 60000, 1e-5, 0.1)
+    xd = x.double()
+    assert rel_err(mean.cpu(), xd.mean(0).cpu()) < 1e-6
+    assert rel_err(mean.cpu(), full_mean.cpu()) < 1e-6
+    assert rel_err(rstd.cpu(), full_rstd.cpu()) < 1e-4
+    assert rel_err((1 / rstd.double() ** 2 - 1e-5).cpu(), xd.var(0, unbiased=False).cpu()) < 1e-4
+    assert rel_err(rv.cpu(), (0.9 + 0.1 * xd.var(0, unbiased=True)).cpu()) < 1e-4
