@@ -106,12 +106,23 @@ def census(step_fn):
     timed = K.trace_read()
     K.trace(0)
     acct, K.ACCOUNT = K.ACCOUNT, None
+    tags, tagk = {}, {}
+    i = 0  # launches are recorded in order: each accounted call owns the next len(funcs) timings
+    for funcs, *_rest in acct:
+        tag = _rest[-1] or "other"
+        for _ in funcs:
+            if i < len(timed):
+                tags[tag] = tags.get(tag, 0.0) + timed[i][1]
+                key = (tag, timed[i][0][:90])
+                n, t = tagk.get(key, (0, 0.0))
+                tagk[key] = (n + 1, t + timed[i][1])
+            i += 1
     table = {}
     for name, ms in timed:
         r = table.setdefault(name, dict(launches=0, measured_ms=0.0, flops=0.0, bytes=0.0, ideal_ms=0.0, peak=None))
         r["launches"] += 1
         r["measured_ms"] += ms
-    for funcs, flops, nbytes, peak in acct:
+    for funcs, flops, nbytes, peak, _tag in acct:
         if not funcs:
             continue
         name = K.kernel_name(funcs[0])
@@ -120,6 +131,8 @@ def census(step_fn):
         r["bytes"] += nbytes
         r["peak"] = peak
         r["ideal_ms"] += max(flops / (MFMA_PEAK_TFS[peak] * 1e12), nbytes / (HBM_PEAK_GBS * 1e9)) * 1e3
+    census.tags = tags
+    census.tag_kernels = tagk
     return table
 
 
@@ -307,6 +320,10 @@ def main():
                 os.makedirs(os.path.dirname(os.path.abspath(args.table_out)), exist_ok=True)
                 with open(args.table_out, "w") as f:
                     json.dump({"config": result["config"], "ms_per_step": result["ms_per_step"],
+                               "by_component_ms": {k: round(v, 4) for k, v in sorted(census.tags.items(),
+                                                                                     key=lambda kv: -kv[1])},
+                               "by_component_kernel": [[t, k, n, round(ms, 4)] for (t, k), (n, ms) in
+                                                       sorted(census.tag_kernels.items(), key=lambda kv: -kv[1][1])],
                                "peaks": {"hbm_GBs": HBM_PEAK_GBS, "mfma_TFs": MFMA_PEAK_TFS},
                                "kernels": {n: {k: (round(v, 6) if isinstance(v, float) else v) for k, v in r.items()}
                                            for n, r in sorted(table.items(), key=lambda kv: -kv[1]["measured_ms"])}},

@@ -81,6 +81,12 @@ _SIGS = {
     "dfm_seg_loss_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P]),
     "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P]),
     "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, P]),
+    "dfm_convffn_supported": (c_int, [c_int, c_int, c_int]),
+    "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
+                                P, P, c_long, P, c_long, P]),
+    "dfm_convffn_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "dfm_convffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
+                                c_long, P, c_long, P, c_long, P, P, P, P]),
     "dfm_trace_set": (c_int, [c_int, ctypes.c_char_p]),
     "dfm_trace_take": (c_int, [ctypes.POINTER(c_void_p), c_int]),
     "dfm_trace_read": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_float), c_int]),

@@ -91,6 +91,7 @@ class ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        K.TAG = "decoder.bwd"
         x, w, y0, y, mean, rstd, gamma = ctx.saved_tensors
         dy = dy.contiguous()
         if ctx.act == 2:
@@ -118,6 +119,7 @@ class LinearActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        K.TAG = "decoder.bwd"
         x, w, b, y = ctx.saved_tensors
         dy = dy.contiguous()
         if ctx.act == 2:
@@ -137,6 +139,7 @@ class CastFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        K.TAG = "decoder.bwd"
         g = g.contiguous()
         return (g if g.dtype == ctx.src else K.cast(g, ctx.src)), None
 
@@ -162,6 +165,7 @@ class ResizeCatFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        K.TAG = "decoder.bwd"
         dout = dout.contiguous()
         H0, W0 = ctx.hw[0]
         grads = []
@@ -195,6 +199,7 @@ class ChannelDropoutLinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        K.TAG = "decoder.bwd"
         xs, w, b, scale = ctx.saved_tensors
         dy = dy.contiguous()
         if dy.dtype != xs.dtype:
@@ -244,6 +249,7 @@ class NMF2DFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        K.TAG = "decoder.bwd"
         x, B0, coef0 = ctx.saved_tensors
         eps = ctx.eps
         gy = gy.contiguous()
@@ -488,6 +494,7 @@ class FuseBNReLUFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        K.TAG = "decoder.bwd"
         cat, Wc, y0, y, mean, rstd, gamma = ctx.saved_tensors
         E = ctx.E
         dy = K.relu_bwd(dy.contiguous(), y)
@@ -514,6 +521,7 @@ class SegLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        K.TAG = "loss.bwd"
         logits_rows, label, out = ctx.saved_tensors
         B, h, w, ncls, ignore = ctx.meta
         gs = g.reshape(1).float().contiguous()

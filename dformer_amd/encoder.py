@@ -106,6 +106,19 @@ class Attention(nn.Module):
         return [vals[n] for n in ATTN_PARAM_NAMES]
 
 
+_SIDE = {}
+_STREAMS = os.environ.get("DFM_STREAMS", "1") != "0"  # DFM_STREAMS=0: one stream (A/B timing)
+
+
+def _side_stream(dev):
+    if not _STREAMS:
+        return None
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 def _drop_path_scale(B, drop_prob, training, dev):
     """mmcv DropPath as a per-sample row scale: floor(keep + U[0,1)) / keep, or None."""
     if drop_prob == 0.0 or not training:
@@ -151,12 +164,34 @@ class Block(nn.Module):
         else:
             rs = [_drop_path_scale(B, self.drop_prob, self.training, x.device) for _ in range(4)]
         ls1e = self.layer_scale_1_e if not self.drop_depth else None
+        st = getattr(self, "stage", "s?")
+        K.TAG = st + ".attn"
         x1, xe1 = AttentionFn.apply(xr, xer, shape, self.attn.num_head, self.attn.window, self.drop_depth, rs[0],
                                     rs[2], *self.attn.fused_params(self.layer_scale_1, ls1e))
-        x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
         if self.drop_depth:
+            K.TAG = st + ".mlp"
+            x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
             return x2.view(B, H, W, C), x_e
-        xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
+        # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
+        # does its backward: autograd replays a node on its forward's stream), which fills the GPU
+        # at the late stages where each kernel alone is latency-bound
+        side = _side_stream(x.device) if x1.is_cuda else None
+        if side is not None:
+            main = torch.cuda.current_stream(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                K.TAG = st + ".mlp_e2"
+                xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
+            xe1.record_stream(side)
+            K.TAG = st + ".mlp"
+            x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
+            main.wait_stream(side)
+            xe2.record_stream(main)
+        else:
+            K.TAG = st + ".mlp"
+            x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
+            K.TAG = st + ".mlp_e2"
+            xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
         return x2.view(B, H, W, C), xe2.view(B, H, W, C // 2)
 
 
@@ -187,6 +222,7 @@ class BNRowsFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        K.TAG = "down.bwd"
         xr, mean, rstd, gamma = ctx.saved_tensors
         B, C, H, W = ctx.shape
         dyr = dy.permute(0, 2, 3, 1).contiguous().view(-1, C)
@@ -254,6 +290,8 @@ class DFormer(nn.Module):
                       norm_cfg=norm_cfg, block_index=depths[i] - j, last_block_index=last_block[i],
                       mlp_ratio=mlp_ratios[i], drop_depth=((i == 3) & (j == depths[i] - 1)))
                 for j in range(depths[i])]))
+            for blk in self.stages[-1]:
+                blk.stage = f"s{i}"
             cur += depths[i]
         for p in (self.stem_e_fc1.weight, self.stem_e_fc1.bias, self.stem_e_fc2.weight, self.stem_e_fc2.bias):
             p.requires_grad_(False)  # never used: excluded from gradients (and DDP buckets)
@@ -297,6 +335,7 @@ class DFormer(nn.Module):
         self._draw_drop_path(x.shape[0], x.device)
         outs = []
         for i in range(4):
+            K.TAG = f"s{i}.down"
             x, x_e = self._downsample(i, x, x_e)
             xh = x.permute(0, 2, 3, 1).to(dt).contiguous()
             eh = x_e.permute(0, 2, 3, 1).to(dt).contiguous()

@@ -9,6 +9,7 @@ Reference semantics (file:line in Originofamonia/DFormer):
   ConvFFNFn     MLP.forward + Block residual/layer-scale/DropPath   DFormer.py:48-67, 173-179
   AttentionFn   Attention.forward + Block residuals                 DFormer.py:70-145, 168-179
 """
+import os
 import weakref
 
 import torch
@@ -103,12 +104,42 @@ def _cat1(*vs):
     return out
 
 
+def wcast_t(dtype, p):
+    """Compute-dtype copy of a 2-D weight's transpose (contiguous), cached like wcast."""
+    key = (id(p), dtype, "T")
+    ptrs = (p.data_ptr(),)
+    hit = _WCACHE.get(key)
+    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
+        return hit[1]
+    w = wcast(dtype, p).t().contiguous()
+    _WCACHE[key] = (_EPOCH[0], w, ptrs)
+    return w
+
+
+# DFM_FUSED_FFN=1 runs the ConvFFN on the fused kernels (csrc/convffn.hip). Off by default: measured
+# on MI355X (tools/ffn_ab.py) the fused forward beats the separate kernels at stage 0 (0.48 vs 0.56 ms)
+# but the fused backward is VALU-bound (depthwise + GELU/GELU' recompute on the halo) and slower
+# (s0: 2.4 vs 1.5 ms fwd+bwd), so the separate kernels stay the default until it is not.
+FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
+
+
+def _ffn_fusable(x, w1, *aligned):
+    """The fused kernels take 16-byte aligned rows and parameter vectors (true for every DFormer
+    size: channel counts are multiples of 16, so flat-buffer offsets are too)."""
+    return (FUSED_FFN and x.is_cuda and x.stride(1) == 1 and x.stride(0) % 8 == 0 and
+            all(t.data_ptr() % 16 == 0 for t in (x,) + aligned) and K.convffn_supported(x, x.shape[1], w1.shape[0]))
+
+
 # ====================================================================== ConvFFN (+ residual)
 class ConvFFNFn(torch.autograd.Function):
     """out = x + rowscale * ls * fc2(GELU(DW3x3(h) + h)),  h = fc1(LN(x))   on [P, C] rows.
 
-    forward kernels: LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
-                     GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue)."""
+    fused (default, csrc/convffn.hip): LN, then one kernel for fc1 -> DW3x3 + identity -> GELU ->
+    fc2 -> residual (the [P, rC] hidden activation stays on chip); backward: residual chain rule,
+    one kernel recomputing h / hpre per tile and producing g, dh, dxn and the depthwise gradients,
+    then the fc2 / fc1 weight-gradient GEMMs and the LN backward.
+    unfused: LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
+             GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue)."""
 
     @staticmethod
     def forward(ctx, x, shape, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls):
@@ -116,18 +147,27 @@ class ConvFFNFn(torch.autograd.Function):
         P, C = x.shape
         dt = x.dtype
         W1, W2 = wcast(dt, w1), wcast(dt, w2)
+        ctx.tag = K.TAG
         xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
+        ctx.shape = shape
+        ctx.fused = _ffn_fusable(x, w1, W1, W2, b1, wpos, bpos)
+        if ctx.fused:
+            out, f = K.convffn_fwd(xn, x, shape, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
+            ctx.save_for_backward(x, xn, mu, rs, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
+            return out
         h = K.linear(xn, W1, b1)
         g = torch.empty_like(h)
         hpre = K.dwconv(h, shape, wpos, bpos, 3, add_identity=True, gelu_out=g)
         f = torch.empty(P, C, device=x.device, dtype=dt)
         out = K.linear(g, W2, b2, preact=f, res=x, colscale=ls, rowscale=rowscale, rows_per_scale=H * W)
         ctx.save_for_backward(x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
-        ctx.shape = shape
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        K.TAG = ctx.tag + ".bwd"
+        if ctx.fused:
+            return ConvFFNFn._backward_fused(ctx, dout)
         x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
         B, H, W = ctx.shape
         dt = x.dtype
@@ -141,6 +181,21 @@ class ConvFFNFn(torch.autograd.Function):
         dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
         dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
         dxn = K.linear_dgrad(dh, W1)
+        dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
+        return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
+                dls)
+
+    @staticmethod
+    def _backward_fused(ctx, dout):
+        x, xn, mu, rs, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
+        B, H, W = ctx.shape
+        dt = x.dtype
+        dout = dout.contiguous()
+        df, dls = K.residual_bwd(dout, f, ls, rowscale, H * W)
+        g, dh, dxn, dwpos, dbpos = K.convffn_bwd(xn, df, ctx.shape, wcast(dt, w1), b1, wpos, bpos, wcast_t(dt, w2),
+                                                 wcast_t(dt, w1), dw=gslot(wpos), db=gslot(bpos))
+        dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
+        dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
         dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
         return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
                 dls)
@@ -164,6 +219,7 @@ class AttentionFn(torch.autograd.Function):
         dt = x.dtype
         dev = x.device
         rps = H * W
+        ctx.tag = K.TAG
         xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
         xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         # q | q_cut | l in one GEMM; GELU (and its pre-activation store) only on the l columns
@@ -213,6 +269,7 @@ class AttentionFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx1, dxe1):
+        K.TAG = ctx.tag + ".bwd"
         sv = ctx.saved_tensors
         (x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1, p1e, rowscale,
          rowscale_e) = sv[:20]

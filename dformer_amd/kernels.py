@@ -23,6 +23,7 @@ GEMM_TRACE = None
 # (inputs read once, outputs written once; workspaces and split-K partials are not algorithmic).
 # The library's launch tracer says which kernels the call enqueued; the first one is charged.
 ACCOUNT = None
+TAG = ""  # component label of the launches that follow (set by the modules; census breakdown)
 _FUNCS = (ctypes.c_void_p * 64)()
 
 
@@ -53,7 +54,7 @@ def kernel_name(func):
 
 def _acct(flops, nbytes, peak="bf16"):
     n = lib.dfm_trace_take(_FUNCS, 64)
-    ACCOUNT.append((tuple(_FUNCS[i] for i in range(min(n, 64))), float(flops), float(nbytes), peak))
+    ACCOUNT.append((tuple(_FUNCS[i] for i in range(min(n, 64))), float(flops), float(nbytes), peak, TAG))
 
 
 def _es(t):
@@ -61,13 +62,15 @@ def _es(t):
 
 
 def _ws(nbytes, dev):
-    """Per-device scratch buffer that only grows (the library never allocates)."""
+    """Scratch buffer per (device, stream) that only grows (the library never allocates); one per
+    stream so kernels running concurrently on a side stream never share a workspace."""
     if nbytes == 0:
         return None
-    buf = _ws_cache.get(dev)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
-        _ws_cache[dev] = buf
+        _ws_cache[key] = buf
     return buf
 
 
@@ -212,6 +215,51 @@ def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
     if ACCOUNT is not None:
         _acct(0, rows * C * _es(dout) * 3)
     return df, dls
+
+
+# ------------------------------------------------------------------------------ fused ConvFFN
+def convffn_supported(x, C, hid):
+    return bool(lib.dfm_convffn_supported(dtype_code(x), C, hid))
+
+
+def convffn_fwd(xn, x, shape, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, out=None, f=None):
+    """out = x + rowscale*ls*(fc2(GELU(DW3(h) + bpos + h)) + b2), h = fc1(xn) + b1; also f = the
+    pre-residual branch (DFormer.py:48-67, 173-179). w1 [hid, C], w2 [C, hid] in the compute dtype."""
+    B, H, W = shape
+    P, C = xn.shape
+    hid = w1.shape[0]
+    if out is None:
+        out = torch.empty(P, C, device=x.device, dtype=x.dtype)
+    if f is None:
+        f = torch.empty(P, C, device=x.device, dtype=x.dtype)
+    check(lib.dfm_convffn_fwd(dtype_code(xn), B, H, W, C, hid, ptr(xn), ld(xn), ptr(x), ld(x), ptr(w1), ptr(b1),
+                              ptr(wpos), ptr(bpos), ptr(w2), ptr(b2), ptr(ls), ptr(rowscale), ptr(out), ld(out),
+                              ptr(f), ld(f), stream()), "dfm_convffn_fwd")
+    if ACCOUNT is not None:
+        _acct(4.0 * P * C * hid + 18.0 * P * hid, _es(x) * P * C * 4 + 2 * _es(x) * C * hid)
+    return out, f
+
+
+def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2t, w1t, dw=None, db=None):
+    """Backward of convffn_fwd given df = dout*ls*rowscale: returns (g, dh, dxn, dwpos, dbpos) with
+    g = GELU(hpre) and dh = dL/dh ([P, hid], for the fc2 / fc1 weight-gradient GEMMs)."""
+    B, H, W = shape
+    P, C = xn.shape
+    hid = w1.shape[0]
+    g = torch.empty(P, hid, device=xn.device, dtype=xn.dtype)
+    dh = torch.empty(P, hid, device=xn.device, dtype=xn.dtype)
+    dxn = torch.empty(P, C, device=xn.device, dtype=xn.dtype)
+    if dw is None:
+        dw = torch.empty(hid, 1, 3, 3, device=xn.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(hid, device=xn.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_convffn_bwd_workspace(dtype_code(xn), B, H, W, C, hid), xn.device)
+    check(lib.dfm_convffn_bwd(dtype_code(xn), B, H, W, C, hid, ptr(xn), ld(xn), ptr(df), ld(df), ptr(w1), ptr(b1),
+                              ptr(wpos), ptr(bpos), ptr(w2t), ptr(w1t), ptr(g), ld(g), ptr(dh), ld(dh), ptr(dxn),
+                              ld(dxn), ptr(dw), ptr(db), ptr(ws), stream()), "dfm_convffn_bwd")
+    if ACCOUNT is not None:
+        _acct(6.0 * P * C * hid + 36.0 * P * hid, _es(xn) * (P * C * 3 + P * hid * 2) + 3 * _es(xn) * C * hid)
+    return g, dh, dxn, dw, db
 
 
 # ---------------------------------------------------------------------------- depthwise conv
@@ -412,6 +460,8 @@ def bn_finalize(stats, count, eps, momentum, running_mean=None, running_var=None
     rstd = torch.empty(C, device=stats.device, dtype=torch.float32)
     check(lib.dfm_bn_finalize(C, ptr(stats), float(count), eps, momentum, ptr(mean), ptr(rstd), ptr(running_mean),
                               ptr(running_var), stream()), "dfm_bn_finalize")
+    if ACCOUNT is not None:
+        _acct(0, C * 4 * (3 + 4 * (running_mean is not None)))
     return mean, rstd
 
 

@@ -72,6 +72,7 @@ class EncoderDecoder(nn.Module):
 
     def _low_logits(self, rgb, modal_x):
         outs = self.encoder_backbone(rgb, modal_x)[0]
+        K.TAG = "decoder"
         return self.decode_head.forward(outs)
 
     def _upsample(self, low, size):
@@ -88,6 +89,7 @@ class EncoderDecoder(nn.Module):
         if label is None:
             return self._upsample(low, rgb.shape[-2:])
         rows, (B, h, w) = _nhwc_rows(low)
+        K.TAG = "loss"
         loss = SegLossFn.apply(rows.contiguous(), B, h, w, label.long(), self.ignore_index)
         out = self._upsample(low.detach(), rgb.shape[-2:]) if self.return_logits else low
         return loss, out

@@ -140,6 +140,30 @@ int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const vo
                           const void* dy, long lddy, float* dw, float* db, void* workspace,
                           dfm_stream_t stream);
 
+/* ---------------------------------------------------------------- fused ConvFFN
+ * DFormer.py:48-67 (MLP: fc1 -> pos = DW3x3 + identity -> GELU -> fc2) inside the Block residual
+ * DFormer.py:173-179, on NHWC rows of B images of H x W:
+ *   fwd: h = xn W1^T + b1 ; hpre = DW3(h) + bpos + h ; f = GELU(hpre) W2^T + b2 ;
+ *        out = x + rowscale[b] * ls[c] * f      (xn = LN(x) computed by dfm_layernorm_fwd)
+ *        writes out and f (the pre-residual branch, for the layer-scale gradient); the [P, hid]
+ *        activations stay on chip.
+ *   bwd: given df = dL/df (dfm_residual_bwd), recomputes h / hpre per tile and writes g = GELU(hpre)
+ *        and dh = dL/dh ([P, hid], the inputs of the fc2 / fc1 weight-gradient GEMMs), dxn = dL/dxn
+ *        [P, C] (for dfm_layernorm_bwd) and dwpos [hid][9], dbpos [hid] (overwritten).
+ * w1 [hid][C], w2 [C][hid], w2t = w2^T [hid][C], w1t = w1^T [C][hid] in `dtype`; b1, b2, wpos
+ * [hid][9], bpos, ls fp32; rowscale fp32 [B] (DropPath) or NULL. Supported shapes:
+ * dfm_convffn_supported (8 <= C <= 256, C % 8 == 0, hid a multiple of the hidden chunk). */
+int dfm_convffn_supported(int dtype, int C, int hid);
+int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* x,
+                    long ldx, const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
+                    const float* b2, const float* ls, const float* rowscale, void* out, long ldout, void* f,
+                    long ldf, dfm_stream_t stream);
+size_t dfm_convffn_bwd_workspace(int dtype, int B, int H, int W, int C, int hid);
+int dfm_convffn_bwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* df,
+                    long lddf, const void* w1, const float* b1, const float* wpos, const float* bpos,
+                    const void* w2t, const void* w1t, void* g, long ldg, void* dh, long lddh, void* dxn,
+                    long lddxn, float* dwpos, float* dbpos, void* workspace, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)
  * (bias grads: nn.Linear backward; layer_scale grads: DFormer.py:173-179). */
