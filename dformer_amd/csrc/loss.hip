@@ -1,13 +1,13 @@
 // Segmentation loss of EncoderDecoder.forward (builder.py:203,230): bilinear upsampling of the
 // low-resolution logits to the label size + cross-entropy(ignore_index) + mean over valid pixels.
 // Fused: the full-resolution logits (786 MB fp32 for DFormer-B bs16) are never materialised.
-// Forward: one thread per label pixel interpolates its ncls logits from the 4 taps (registers,
-//   compile-time unrolled over MAXC classes), computes log-sum-exp and the CE term; block partials
-//   are summed in a fixed order.
-// Backward: a block owns a TY x TX tile of label pixels. Phase 1: every thread writes its pixel's
-//   (softmax - onehot) / count row into LDS. Phase 2 (separable): each pixel row is reduced onto the
-//   patch's low-res columns (<= 2 taps per pixel), then the pixel rows onto its low-res rows.
-//   Phase 3: one global float atomic per (cell, class) per block (a cell is shared by <= ~10 blocks).
+//
+// Forward: one thread per label pixel interpolates its ncls logits from the 4 taps (registers),
+//   computes log-sum-exp and the CE term; block partials are summed in a fixed order.
+// Backward, integer upsampling factor (the DFormer heads: x8 ham, x4 MLP decoder at 480x640):
+//   seg_loss_bwd_tile_kernel + seg_loss_gather_kernel (below): deterministic, no atomics.
+// Backward, other factors: seg_loss_bwd_kernel — per tile of label pixels a separable reduction
+//   in LDS, then one float atomic per (cell, class) per block into a zeroed gradient.
 #include <algorithm>
 
 #include "common.h"
@@ -236,10 +236,154 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
   }
 }
 
+// ---- backward for an integer upsampling factor S (H = S h, W = S w, S even, S*S <= 64): the label
+// pixels y in [S ty - S/2, S ty + S/2) all take their y-taps from low-res rows {ty - 1, ty} (edges
+// clamp), likewise for x, so each S x S pixel tile ("corner tile" (ty, tx), ty in [0, h]) feeds
+// exactly the 2 x 2 low-res cells around its corner. One wave owns 64 / S^2 tiles: every lane
+// forms its pixel's scaled (softmax - onehot) row in LDS, then each lane of a (tile, class) pair sums
+// the tile's pixels into the 4 corner partials (fixed order). seg_loss_gather_kernel adds, for every
+// low-res cell, the 4 corner partials that touch it in a fixed order: deterministic, no atomics.
+constexpr int TILE_NT = 128;  // 2 waves; res[] stays under 64 KB of static LDS at MAXC
+
+template <typename T, int S>
+__global__ __launch_bounds__(TILE_NT) void seg_loss_bwd_tile_kernel(int B, int h, int w, int ncls,
+                                                                    const T* __restrict__ lg, int H, int W,
+                                                                    const long* __restrict__ label, int ignore,
+                                                                    const float* __restrict__ loss_out,
+                                                                    const float* __restrict__ gscale,
+                                                                    float* __restrict__ part, long ntiles) {
+  constexpr int TP = S * S, TPW = 64 / TP;   // pixels per tile, tiles per wave
+  constexpr int RP = MAXC + 1;               // LDS row pitch of a pixel's residual
+  __shared__ float res[TILE_NT][RP];
+  __shared__ float wts[TILE_NT][4];          // per pixel: weights of corner slots (y0 x0, y0 x1, y1 x0, y1 x1)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long tile = ((long)blockIdx.x * (TILE_NT / 64) + wid) * TPW + lane / TP;
+  const int d = lane % TP, dy = d / S, dx = d % S;
+  const int tw = w + 1, th = h + 1;
+  const float inv = (gscale ? gscale[0] : 1.f) / fmaxf(loss_out[1], 1.f);
+  const bool vec = ncls % 8 == 0 && ((uintptr_t)lg & 15) == 0;
+  float* row = res[threadIdx.x];
+  float wv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (tile < ntiles) {
+    const int tx = tile % tw, ty = (tile / tw) % th, b = tile / ((long)tw * th);
+    const int y = S * ty - S / 2 + dy, x = S * tx - S / 2 + dx;
+    long lab = -1;
+    if (y >= 0 && y < H && x >= 0 && x < W) lab = label[((long)b * H + y) * W + x];
+    if (lab != ignore && lab >= 0 && lab < ncls) {
+      float z[MAXC];
+      interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
+      float m = -INFINITY;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) m = fmaxf(m, z[c]);
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        z[c] = c < ncls ? __expf(z[c] - m) : 0.f;
+        se += z[c];
+      }
+      const float rs = inv / se;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncls) row[c] = z[c] * rs - (c == lab ? inv : 0.f);
+      int a0, a1, b0, b1;
+      float ly, lx;
+      src_idx(y, h, H, a0, a1, ly);
+      src_idx(x, w, W, b0, b1, lx);
+      // taps -> the tile's corner slots (row ty - 1 -> 0, ty -> 1; clamped duplicates merge)
+      const float wy[2] = {(a0 == ty - 1 ? 1.f - ly : 0.f) + (a1 == ty - 1 ? ly : 0.f),
+                           (a0 == ty ? 1.f - ly : 0.f) + (a1 == ty ? ly : 0.f)};
+      const float wx[2] = {(b0 == tx - 1 ? 1.f - lx : 0.f) + (b1 == tx - 1 ? lx : 0.f),
+                           (b0 == tx ? 1.f - lx : 0.f) + (b1 == tx ? lx : 0.f)};
+      wv[0] = wy[0] * wx[0]; wv[1] = wy[0] * wx[1]; wv[2] = wy[1] * wx[0]; wv[3] = wy[1] * wx[1];
+    } else {
+      for (int c = 0; c < ncls; ++c) row[c] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wts[threadIdx.x][k] = wv[k];
+  __syncthreads();
+  // (tile of this wave, class) pairs: sum the tile's pixels into the 4 corner partials
+  for (int pr = lane; pr < TPW * ncls; pr += 64) {
+    const int tt = pr / ncls, c = pr % ncls;
+    const long t = ((long)blockIdx.x * (TILE_NT / 64) + wid) * TPW + tt;
+    if (t >= ntiles) continue;
+    const int base = wid * 64 + tt * TP;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < TP; ++q) {
+      const float r = res[base + q][c];
+      s0 = fmaf(wts[base + q][0], r, s0);
+      s1 = fmaf(wts[base + q][1], r, s1);
+      s2 = fmaf(wts[base + q][2], r, s2);
+      s3 = fmaf(wts[base + q][3], r, s3);
+    }
+    float* o = part + t * 4 * ncls + c;
+    o[0] = s0;
+    o[ncls] = s1;
+    o[2 * ncls] = s2;
+    o[3 * ncls] = s3;
+  }
+}
+
+// dlogits[b][i][j][c] = sum of the corner partials of the 4 tiles around cell (i, j), fixed order
+__global__ void seg_loss_gather_kernel(int B, int h, int w, int ncls, const float* __restrict__ part,
+                                       float* __restrict__ dlg) {
+  const long n = (long)B * h * w * ncls;
+  const int tw = w + 1, th = h + 1;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % ncls;
+    const long cell = e / ncls;
+    const int j = cell % w, i = (cell / w) % h, b = cell / ((long)w * h);
+    auto P = [&](int ty, int tx, int slot) { return part[((((long)b * th + ty) * tw + tx) * 4 + slot) * ncls + c]; };
+    // cell (i, j) is slot (row 1, col 1) of tile (i, j), (1, 0) of (i, j + 1), (0, 1) of (i + 1, j),
+    // (0, 0) of (i + 1, j + 1)
+    dlg[e] = P(i, j, 3) + P(i, j + 1, 2) + P(i + 1, j, 1) + P(i + 1, j + 1, 0);
+  }
+}
+
+template <typename T>
+int launch_bwd_tiles(int S, int B, int h, int w, int ncls, const void* lg, int H, int W, const long* label,
+                     int ignore, const float* loss_out, const float* gscale, float* part, float* dlg,
+                     hipStream_t s) {
+  const long ntiles = (long)B * (h + 1) * (w + 1);
+  const long tiles_per_block = (TILE_NT / 64) * (64 / (S * S));
+  const unsigned nb = cdiv(ntiles, tiles_per_block);
+  if (S == 8)
+    DFM_LAUNCH((seg_loss_bwd_tile_kernel<T, 8>), dim3(nb), dim3(TILE_NT), 0, s, B, h, w, ncls, (const T*)lg, H, W,
+               label, ignore, loss_out, gscale, part, ntiles);
+  else if (S == 4)
+    DFM_LAUNCH((seg_loss_bwd_tile_kernel<T, 4>), dim3(nb), dim3(TILE_NT), 0, s, B, h, w, ncls, (const T*)lg, H, W,
+               label, ignore, loss_out, gscale, part, ntiles);
+  else
+    DFM_LAUNCH((seg_loss_bwd_tile_kernel<T, 2>), dim3(nb), dim3(TILE_NT), 0, s, B, h, w, ncls, (const T*)lg, H, W,
+               label, ignore, loss_out, gscale, part, ntiles);
+  DFM_LAUNCH_CHECK();
+  const long n = (long)B * h * w * ncls;
+  DFM_LAUNCH(seg_loss_gather_kernel, dim3(min(8192L, (n + 255) / 256)), dim3(256), 0, s, B, h, w, ncls,
+             (const float*)part, dlg);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+int tile_scale(int h, int w, int H, int W) {
+  for (int S : {8, 4, 2})
+    if (H == S * h && W == S * w) return S;
+  return 0;
+}
+
 constexpr int LOSS_BLOCKS = 1024;
 }  // namespace
 
-extern "C" size_t dfm_seg_loss_workspace(int, int, int) { return LOSS_BLOCKS * 2 * sizeof(float); }
+extern "C" size_t dfm_seg_loss_workspace(int B, int H, int W) {
+  (void)B; (void)H; (void)W;
+  return (size_t)LOSS_BLOCKS * 2 * sizeof(float);
+}
+
+/* backward workspace of the integer-scale tile path: corner partials of every tile (0 otherwise) */
+extern "C" size_t dfm_seg_loss_bwd_workspace(int B, int h, int w, int ncls, int H, int W) {
+  if (!tile_scale(h, w, H, W)) return 0;
+  return (size_t)B * (h + 1) * (w + 1) * 4 * ncls * sizeof(float);
+}
 
 extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                                 const long* label, int ignore, float* lse, float* loss_out, void* workspace,
@@ -249,11 +393,11 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
   const long n = (long)B * H * W;
   const int nblk = (int)min((long)LOSS_BLOCKS, (n + 255) / 256);
   if (dtype == DFM_BF16)
-    DFM_LAUNCH(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H,
-                       W, label, ignore, lse, (float*)workspace);
+    DFM_LAUNCH(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H, W,
+               label, ignore, lse, (float*)workspace);
   else
-    DFM_LAUNCH(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H,
-                       W, label, ignore, lse, (float*)workspace);
+    DFM_LAUNCH(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H, W,
+               label, ignore, lse, (float*)workspace);
   DFM_LAUNCH_CHECK();
   DFM_LAUNCH(seg_loss_sum_kernel, dim3(1), dim3(64), 0, s, nblk, (const float*)workspace, loss_out);
   DFM_LAUNCH_CHECK();
@@ -262,12 +406,21 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
 
 extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                                 const long* label, int ignore, const float* lse, const float* loss_out,
-                                const float* gscale, float* dlogits, dfm_stream_t stream) {
+                                const float* gscale, float* dlogits, void* workspace, dfm_stream_t stream) {
   (void)lse;
   DFM_CHECK_ARG(logits && label && loss_out && dlogits && ncls <= MAXC && h <= H && w <= W,
                 "dfm_seg_loss_bwd: bad argument (needs ncls <= 64 and an upsampling resize)");
   hipStream_t s = (hipStream_t)stream;
   const long nl = (long)B * h * w * ncls;
+  if (workspace && tile_scale(h, w, H, W)) {
+    const int S = tile_scale(h, w, H, W);
+    if (dtype == DFM_BF16)
+      return launch_bwd_tiles<bf16_t>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
+                                      (float*)workspace, dlogits, s);
+    return launch_bwd_tiles<float>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
+                                   (float*)workspace, dlogits, s);
+  }
+  // other scales: the general tile kernel (float atomics into a zeroed gradient)
   DFM_LAUNCH(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
   DFM_LAUNCH_CHECK();
   const unsigned nblk = B * ((H + TY - 1) / TY) * ((W + TX - 1) / TX);

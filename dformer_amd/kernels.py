@@ -558,8 +558,9 @@ def seg_loss_fwd(logits, B, h, w, ncls, label, ignore=255):
 def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255):
     H, W = label.shape[-2:]
     dl = torch.empty(B * h * w, ncls, device=logits.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_seg_loss_bwd_workspace(B, h, w, ncls, H, W), logits.device)
     check(lib.dfm_seg_loss_bwd(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore, None,
-                               ptr(loss_out), ptr(gscale), ptr(dl), stream()), "dfm_seg_loss_bwd")
+                               ptr(loss_out), ptr(gscale), ptr(dl), ptr(ws), stream()), "dfm_seg_loss_bwd")
     if ACCOUNT is not None:
         _acct(0, logits.numel() * (_es(logits) + 4) + label.numel() * 8)
     return dl

@@ -254,9 +254,13 @@ size_t dfm_seg_loss_workspace(int B, int H, int W);
 int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                      const long* label, int ignore, float* lse, float* loss_out, void* workspace,
                      dfm_stream_t stream);
+/* bwd workspace: dfm_seg_loss_bwd_workspace bytes (0 = none needed). With an integer upsampling
+ * factor (H = S h, W = S w, S in {2, 4, 8}) the backward is deterministic (fixed-order sums, no
+ * atomics); other factors fall back to float atomics. */
+size_t dfm_seg_loss_bwd_workspace(int B, int h, int w, int ncls, int H, int W);
 int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                      const long* label, int ignore, const float* lse, const float* loss_out,
-                     const float* gscale, float* dlogits, dfm_stream_t stream);
+                     const float* gscale, float* dlogits, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW step (train.py:210-216) over a flat float32 parameter buffer; optional
