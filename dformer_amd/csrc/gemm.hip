@@ -47,6 +47,8 @@ struct GemmArgs {
   int mul_gelu_grad;
   int stream;      // host: take the M-streaming persistent kernel
   int tiles_n;     // output column tiles (grid.x enumerates tiles_m * tiles_n)
+  int tiles_m;     // output row tiles (glds kernel)
+  int n_fast;      // glds kernel: consecutive (XCD-local) blocks walk column tiles of one row tile
 };
 
 
@@ -724,6 +726,265 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a) {
   epilogue_store<T>(a, b, m, n, v);
 }
 
+// ---------------------------------------------------------------- LDS-DMA pipelined GEMM (bf16)
+// For k-loops of >= 2 whole 64-deep slices over 16-byte aligned operands. Operand tiles go global ->
+// LDS by global_load_lds_dwordx4 (no register staging, so few VGPRs and several blocks per CU)
+// into an NS-deep ring of stages; each wave waits only for its own DMAs of the slice it is about
+// to read with a COUNTED vmcnt (NS-2 slices stay in flight across every barrier; with NS = 2 the
+// next slice's DMA overlaps this slice's MFMAs) and the raw s_barrier publishes them. LDS images are
+// unpadded with XOR-swizzled 16-byte chunks (an LDS-DMA writes lane-linearly, so the swizzle is
+// applied to each lane's SOURCE address): k-contiguous tiles [R][64] hold chunk c of row r at
+// position c ^ ((r >> 1) & 7) (conflict-free ds_read_b128 fragments); row-contiguous tiles [64][R]
+// use tr_swz (read with ds_read_b64_tr_b16). Blocks are renumbered so consecutive logical blocks
+// share an XCD (and its L2): the column tiles of one row tile (n_fast) or the tiles of one split.
+constexpr int GBK = 64;
+
+DFM_INLINE int kc_swz(int r) { return (r >> 1) & 7; }
+
+template <int R, bool KC>
+struct GImg {
+  static constexpr int CHUNKS = R * GBK / 8;           // 16-byte chunks per tile
+  static constexpr int BYTES = CHUNKS * 16;
+  static constexpr int CPR = KC ? GBK / 8 : R / 8;     // chunks per image row
+  // image position q -> (image row, chunk of the source row stored there)
+  DFM_INLINE static void at(int q, int& row, int& chunk) {
+    row = q / CPR;
+    const int p = q % CPR;
+    chunk = KC ? (p ^ kc_swz(row)) : (p ^ tr_swz<R>(row));
+  }
+};
+
+DFM_INLINE bf16x8_t frag_kc_swz(const bf16_t* lds, int r0, int k0, int lane) {
+  const int r = r0 + (lane & 15), c = (k0 >> 3) + (lane >> 4);
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(lds + r * GBK + ((c ^ kc_swz(r)) << 3)));
+}
+
+constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+template <int N>
+DFM_INLINE void wait_vm() { __builtin_amdgcn_s_waitcnt(vmcnt_imm(N)); }
+DFM_INLINE void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8)); }
+
+template <int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
+__global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int WAVES_N = NW / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  using IA = GImg<BM, AK>;
+  using IB = GImg<BN, BKC>;
+  constexpr int WIA = IA::CHUNKS / 64, WIB = IB::CHUNKS / 64;  // wave-instructions per tile
+  static_assert((WIA + WIB) % NW == 0, "every wave must issue the same number of DMAs per slice");
+  constexpr int J = (WIA + WIB) / NW;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  static_assert(NS >= 2, "ring too shallow");
+  (void)NT;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+
+  // XCD-aware renumbering (bijective for any grid size): blocks id and id + 8 share an XCD
+  const int nblk = gridDim.x, id = blockIdx.x;
+  const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+  const int tiles = a.tiles_m * a.tiles_n;
+  const int tile = lid % tiles, zs = lid / tiles;
+  const int bm = (a.n_fast ? tile / a.tiles_n : tile % a.tiles_m) * BM;
+  const int bn = (a.n_fast ? tile % a.tiles_n : tile / a.tiles_m) * BN;
+  const int b = zs / a.splits, split = zs % a.splits;
+
+  const int kper = ((a.K + a.splits - 1) / a.splits + GBK - 1) / GBK * GBK;
+  const int kbeg = split * kper;
+  const int kend = min(a.K, kbeg + kper);
+  const int nk = kend > kbeg ? (kend - kbeg + GBK - 1) / GBK : 0;
+  const int nfull = (kend - kbeg) / GBK;  // >= 2 whenever the host picks this kernel, except short splits
+  const int ones_r = a.colsum != nullptr ? a.N : -1;
+
+  const bf16_t* A = (const bf16_t*)a.A + (long)b * a.sa;
+  const bf16_t* Bp = (const bf16_t*)a.B + (long)b * a.sb;
+
+  // per DMA j of this lane: source of slice 0, per-slice step (elements), LDS offset in a stage,
+  // and (virtual ones column) the element of the chunk to overwrite with 1.0 after it lands
+  const bf16_t* src[J];
+  long step[J];
+  int dst[J], ones_e[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int g = j * NW + wid;  // wave-uniform
+    const bool isA = g < WIA;
+    const int gq = (isA ? g : g - WIA) * 64 + lane;
+    int row, chunk;
+    ones_e[j] = -1;
+    if (isA) {
+      IA::at(gq, row, chunk);
+      if (AK) {
+        const int r = min(bm + row, a.M - 1);
+        src[j] = A + (long)r * a.lda + kbeg + chunk * 8;
+        step[j] = GBK;
+      } else {
+        const int c = bm + chunk * 8;
+        src[j] = A + (long)(kbeg + row) * a.lda + (c < a.M ? c : 0);
+        step[j] = (long)GBK * a.lda;
+      }
+      dst[j] = g * 1024;
+    } else {
+      if (BKC) {
+        IB::at(gq, row, chunk);
+        const int r = min(bn + row, a.N - 1);
+        src[j] = Bp + (long)r * a.ldb + kbeg + chunk * 8;
+        step[j] = GBK;
+      } else {
+        IB::at(gq, row, chunk);
+        const int c = bn + chunk * 8;
+        src[j] = Bp + (long)(kbeg + row) * a.ldb + (c < a.N ? c : 0);
+        step[j] = (long)GBK * a.ldb;
+        if (ones_r >= c && ones_r < c + 8) ones_e[j] = ones_r - c;
+      }
+      dst[j] = IA::BYTES + (g - WIA) * 1024;
+    }
+  }
+  const bool patch = ones_r >= bn && ones_r < bn + BN;  // block-uniform
+
+  auto issue = [&](int t, int stage) {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src[j] + t * step[j]),
+                                       (void __attribute__((address_space(3)))*)(smem + stage * STAGE + dst[j]),
+                                       16, 0, 0);
+  };
+  auto patch_ones = [&](int stage) {  // after this wave's DMAs of the stage landed
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (ones_e[j] >= 0)
+        reinterpret_cast<unsigned short*>(smem + stage * STAGE + dst[j] + lane * 16)[ones_e[j]] = 0x3f80u;
+  };
+
+  float4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto read_frags = [&](int stage, bf16x8_t (&fa)[2][TM], bf16x8_t (&fb)[2][TN]) {
+    const bf16_t* la = reinterpret_cast<const bf16_t*>(smem + stage * STAGE);
+    const bf16_t* lb = reinterpret_cast<const bf16_t*>(smem + stage * STAGE + IA::BYTES);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[h][i] = AK ? frag_kc_swz(la, wm * WM + i * 16, 32 * h, lane)
+                      : frag_bf16<false, BM>(la, wm * WM + i * 16, 32 * h, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[h][j] = BKC ? frag_kc_swz(lb, wn * WN + j * 16, 32 * h, lane)
+                       : frag_bf16<false, BN>(lb, wn * WN + j * 16, 32 * h, lane);
+    }
+  };
+  auto mma = [&](const bf16x8_t (&fa)[2][TM], const bf16x8_t (&fb)[2][TN], int h) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
+  };
+  auto compute = [&](int stage) {
+    bf16x8_t fa[2][TM], fb[2][TN];
+    read_frags(stage, fa, fb);
+    mma(fa, fb, 0);
+    mma(fa, fb, 1);
+  };
+
+  // Software pipeline across the barrier. Iteration u enters with slice u's fragments in
+  // registers; k-step 0 MFMAs -> wait for slice u+1's DMAs -> barrier (slice u+1 visible, stage
+  // u % NS free) -> DMA slice u+NS into it -> read slice u+1's fragments -> k-step 1 MFMAs, so
+  // the LDS reads of the next slice overlap this slice's MFMAs instead of every wave reading,
+  // then every wave multiplying, in lockstep.
+  {
+    // ring: wait for slice t (NS-2 slices stay in flight) -> barrier -> DMA slice t+NS-1 into the
+    // stage read last iteration -> multiply slice t. Measured on the step's GEMM census: a 2-stage
+    // ring at 3-4 blocks per CU (blocks overlap each other's barrier/LDS phases) beats a 4-stage
+    // ring at 1 block per CU, with or without fragment reads pipelined across the barrier.
+#pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < nfull) issue(t, t);
+    for (int t = 0; t < nfull; ++t) {
+      const int stage = t % NS;
+      const int rem = nfull - 1 - t;
+      if (NS > 2 && rem >= NS - 2) wait_vm<J * (NS > 2 ? NS - 2 : 0)>();
+      else if (NS > 3 && rem == 1) wait_vm<J>();
+      else wait_vm<0>();
+      if (patch) patch_ones(stage);
+      wait_lgkm0();
+      __builtin_amdgcn_s_barrier();
+      if (t + NS - 1 < nfull) issue(t + NS - 1, (t + NS - 1) % NS);
+      compute(stage);
+    }
+  }
+  wait_vm<0>();
+  __syncthreads();
+  // guarded tail: the partial last slice (zero fill past kend), staged through registers into stage 0
+  for (int kt = nfull; kt < nk; ++kt) {
+    const int k0 = kbeg + kt * GBK;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int g = j * NW + wid;
+      const bool isA = g < WIA;
+      const int gq = (isA ? g : g - WIA) * 64 + lane;
+      int row, chunk;
+      uint4 v;
+      if (isA) {
+        IA::at(gq, row, chunk);
+        v = AK ? load_vec<bf16_t, true>(A, a.lda, bm + row, k0 + chunk * 8, a.M, kend, true, -1)
+               : load_vec<bf16_t, false>(A, a.lda, bm + chunk * 8, k0 + row, a.M, kend, true, -1);
+      } else {
+        IB::at(gq, row, chunk);
+        v = BKC ? load_vec<bf16_t, true>(Bp, a.ldb, bn + row, k0 + chunk * 8, a.N, kend, true, ones_r)
+                : load_vec<bf16_t, false>(Bp, a.ldb, bn + chunk * 8, k0 + row, a.N, kend, true, ones_r);
+      }
+      *reinterpret_cast<uint4*>(smem + dst[j] + lane * 16) = v;
+    }
+    __syncthreads();
+    compute(0);
+    __syncthreads();
+  }
+  gemm_epilogue<bf16_t, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
+}
+
+template <int BM, int BN, int NW, int WM_, bool AK, bool BKC, int NS, int MINB>
+int launch_glds(GemmArgs& a, hipStream_t s) {
+  using IA = GImg<BM, AK>;
+  using IB = GImg<BN, BKC>;
+  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
+  const size_t lds = std::max((size_t)NS * (IA::BYTES + IB::BYTES), (size_t)RP * (BN + 4) * sizeof(float));
+  auto kern = gemm_glds_kernel<BM, BN, NW, WM_, AK, BKC, NS, MINB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  a.tiles_m = cdiv(a.M, BM);
+  a.tiles_n = cdiv(a.Nw, BN);
+  a.n_fast = a.M >= a.N;
+  const long grid = (long)a.tiles_m * a.tiles_n * a.batch * a.splits;
+  DFM_LAUNCH(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, a);
+  DFM_LAUNCH_CHECK();
+  if (a.splits > 1) {
+    const long total = (long)a.batch * a.M * a.ldw;
+    if (a.splits >= 8)
+      DFM_LAUNCH((splitk_reduce_kernel<bf16_t, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
+    else
+      DFM_LAUNCH((splitk_reduce_kernel<bf16_t, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
+    DFM_LAUNCH_CHECK();
+  }
+  return DFM_OK;
+}
+
+template <int BM, int BN, int NW, int WM_, int NS, int MINB>
+int glds_ak(GemmArgs& a, bool bk, hipStream_t s) {
+  if (bk) return launch_glds<BM, BN, NW, WM_, true, true, NS, MINB>(a, s);
+  return launch_glds<BM, BN, NW, WM_, true, false, NS, MINB>(a, s);
+}
+
 template <typename T, int BM, int BN, int NW, int WM_, int BK, bool AK, bool BKC, int DEPTH>
 int launch_cfg(GemmArgs& a, hipStream_t s) {
   using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
@@ -793,6 +1054,12 @@ template <typename T, int BM, int BN, int NW, int WM_, int BK>
 int launch_depth(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
   const int kper = (a.K + a.splits - 1) / a.splits;
   const long blocks = (long)cdiv(a.M, BM) * cdiv(a.Nw, BN) * a.batch * a.splits;
+  static const int depth_env = [] {  // DFM_GEMM_DEPTH=1|2 forces the register pipeline depth (A/B timing)
+    const char* e = getenv("DFM_GEMM_DEPTH");
+    return e ? atoi(e) : 0;
+  }();
+  if (depth_env == 1) return launch_layout<T, BM, BN, NW, WM_, BK, 1>(a, ak, bk, s);
+  if (depth_env == 2) return launch_layout<T, BM, BN, NW, WM_, BK, 2>(a, ak, bk, s);
   // two register sets cost occupancy: only worth it for long k-loops on a grid that leaves CUs
   // with a single block anyway
   if (kper >= 8 * BK && blocks <= 512) return launch_layout<T, BM, BN, NW, WM_, BK, 2>(a, ak, bk, s);
@@ -868,6 +1135,23 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
     a.stream = stream_env != 0 && sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb && d->K % BKsel == 0 &&
                d->K / BKsel <= 8 && tiles >= 1024;
+  }
+  static const int glds_env = [] {  // DFM_GEMM_GLDS=0 disables the LDS-DMA kernel (A/B timing)
+    const char* e = getenv("DFM_GEMM_GLDS");
+    return e ? atoi(e) : 1;
+  }();
+  // LDS-DMA ring kernel: bf16 with a k-contiguous A (forward, dgrad) and >= 2 whole k-slices. Routing
+  // fitted on the DFormer-B step's GEMM census (tools/gemm_sweep.py --replay, DFM_GEMM_GLDS=0 vs 1):
+  // it wins on the forward except wide-N x short-K, and on dgrad from K = 640 up; with a row-
+  // contiguous A (wgrad) the register-staged kernel stays ahead.
+  if constexpr (sizeof(T) == 2) {
+    const int kper = (d->K + a.splits - 1) / a.splits;
+    const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 640);
+    if (glds_env && route && !a.stream && a.ala && a.alb && kper >= 2 * GBK) {
+      if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
+      if (BN == 64) return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
+      return glds_ak<64, 128, 4, 2, 2, 3>(a, bk, s);
+    }
   }
   if (small_k) {
     constexpr int BKs = sizeof(T) == 2 ? 32 : 16;

@@ -253,23 +253,35 @@ class NMF2DFn(torch.autograd.Function):
         x, B0, coef0 = ctx.saved_tensors
         eps = ctx.eps
         gy = gy.contiguous()
+        Bb, N, D = x.shape
+        R = B0.shape[2]
         Bt, Ct, num, M, den, Cf = ctx.final
         gC = K.bmm(gy, Bt)                                        # gy B         [N,R]
         gB = K.bmm(gy, Cf, a_t=True)                              # gy^T C       [D,R]
-        gx = torch.zeros_like(x)
+        # Every contribution to gx is a rank-R product P Q^T (P [N,R], Q [D,R]); they are gathered
+        # side by side and applied by ONE GEMM over the concatenated K = T*R at the end, instead of
+        # T read-modify-write passes over the [N, D] gradient.
+        T = 2 * len(ctx.hist) + 2
+        Pc = torch.empty(Bb, N, T * R, device=x.device, dtype=torch.float32)
+        Qc = torch.empty(Bb, D, T * R, device=x.device, dtype=torch.float32)
+        slot = [0]
 
-        def upd_bwd(g, a, nm, dn, out, gnum_sinks, gden_sink):
-            return K.nmf_update_bwd(g, a, nm, dn, out, eps=eps)
+        def gx_term(P, Q):
+            i = slot[0]
+            Pc[:, :, i * R:(i + 1) * R].copy_(P)
+            Qc[:, :, i * R:(i + 1) * R].copy_(Q)
+            slot[0] += 1
 
         # final coef update: Cf = Ct * num / (Ct M + eps), num = x B, M = B^T B
         gCt, gnum, gden = K.nmf_update_bwd(gC, Ct, num, den, Cf, eps=eps)
-        _acc_xB(gx, gB, x, Bt, gnum)
+        gx_term(gnum, Bt)                                         # gx += gnum B^T
+        K.bmm(x, gnum, a_t=True, out=gB, beta=1.0)                # gB += x^T gnum
         _acc_CM(gCt, gB, Ct, Bt, M, gden)
         gC = gCt
         for (Bp, Cp, num1, M1, den1, Cn, num2, Q, den2, Bn) in reversed(ctx.hist):
             # B-update: Bn = Bp * num2 / (Bp Q + eps), num2 = x^T-side (x C_n), Q = Cn^T Cn
             gBp, gnum2, gden2 = K.nmf_update_bwd(gB, Bp, num2, den2, Bn, eps=eps)
-            K.bmm(Cn, gnum2, b_t=True, out=gx, beta=1.0)          # gx += Cn gnum2^T
+            gx_term(Cn, gnum2)                                    # gx += Cn gnum2^T
             K.bmm(x, gnum2, out=gC, beta=1.0)                     # gCn += x gnum2
             K.bmm(gden2, Q, out=gBp, beta=1.0)                    # gBp += gden2 Q
             gQ = K.bmm(Bp, gden2, a_t=True)                       # Bp^T gden2
@@ -277,20 +289,17 @@ class NMF2DFn(torch.autograd.Function):
             K.bmm(Cn, gQ, b_t=True, out=gC, beta=1.0)
             # C-update: Cn = Cp * num1 / (Cp M1 + eps), num1 = x B_p, M1 = Bp^T Bp
             gCp, gnum1, gden1 = K.nmf_update_bwd(gC, Cp, num1, den1, Cn, eps=eps)
-            _acc_xB(gx, gBp, x, Bp, gnum1)
+            gx_term(gnum1, Bp)                                    # gx += gnum1 Bp^T
+            K.bmm(x, gnum1, a_t=True, out=gBp, beta=1.0)          # gBp += x^T gnum1
             _acc_CM(gCp, gBp, Cp, Bp, M1, gden1)
             gB, gC = gBp, gCp
         # coef0 = softmax(x B0)  (B0 is a random constant)
         gS = K.softmax_rows_bwd(coef0, gC)
-        K.bmm(gS, B0, b_t=True, out=gx, beta=1.0)
+        gx_term(gS, B0)                                           # gx += gS B0^T
+        assert slot[0] == T
+        gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T
         ctx.hist = ctx.final = None
         return gx, None, None, None
-
-
-def _acc_xB(gx, gB, x, Bt, gnum):
-    """num = x B (x [N,D], B [D,R]):  gx += gnum B^T ; gB += x^T gnum."""
-    K.bmm(gnum, Bt, b_t=True, out=gx, beta=1.0)
-    K.bmm(x, gnum, a_t=True, out=gB, beta=1.0)
 
 
 def _acc_CM(gC, gB, C, Bt, M, gden):

@@ -93,6 +93,37 @@ def test_gemm_splitk_and_strided(dt):
     assert rel(acc, ref) < TOL[dt]
 
 
+@pytest.mark.parametrize("M,N,Kd", [(1000, 128, 256), (777, 200, 1000), (4800, 512, 2048), (130, 40, 136),
+                                    (19200, 256, 1024), (300, 64, 520)])
+def test_gemm_lds_dma_paths(M, N, Kd):
+    """bf16 k-loops of >= 2 whole 64-deep slices take the LDS-DMA ring kernel in all three layouts
+    (forward, dgrad, wgrad with the fused bias-gradient column), incl. k tails, ragged M / N and
+    split-K, with the full forward epilogue."""
+    k = K()
+    dt = torch.bfloat16
+    x = torch.randn(M, Kd, device=DEV).to(dt)
+    w = (torch.randn(N, Kd, device=DEV) / Kd ** 0.5).to(dt)
+    b = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(dt)
+    ls = torch.rand(N, device=DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=dt)
+    y = k.linear(x, w, b, preact=pre, res=res, colscale=ls)
+    f = x.float() @ w.float().t() + b
+    assert rel(pre.float(), f) < TOL[dt]
+    assert rel(y.float(), res.float() + ls * f) < TOL[dt]
+    dy = torch.randn(M, Kd, device=DEV).to(dt)
+    wd = (torch.randn(Kd, N, device=DEV) / Kd ** 0.5).to(dt)   # dx[M, N] = dy[M, Kd] @ wd[Kd, N]
+    dx = k.linear_dgrad(dy, wd)
+    assert rel(dx.float(), dy.float() @ wd.float()) < TOL[dt]
+    g = torch.randn(Kd, M, device=DEV).to(dt)     # wgrad over Kd "pixels": dW[M, N] = g^T x2
+    x2 = torch.randn(Kd, N, device=DEV).to(dt)
+    dw, db = k.linear_wgrad(g, x2, bias_grad=True)
+    assert rel(dw, g.float().t() @ x2.float()) < TOL[dt]
+    assert rel(db, g.float().sum(0)) < TOL[dt]
+    dw2 = k.linear_wgrad(g, x2)
+    assert torch.equal(dw2, dw)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_epilogues(dt):
     k = K()

@@ -21,6 +21,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from dformer_amd import _lib, kernels as K  # noqa: E402
 
+COLD = None  # --cold: a 1 GiB buffer rewritten before every timed launch
+
 PTR_FIELDS = ("bias", "preact", "mul", "res", "colscale", "rowscale", "colsum")
 
 
@@ -94,6 +96,18 @@ def replay(d, splits, iters=20):
 
     for _ in range(3):
         launch()
+    if COLD is not None:  # evict the operands from L2 and the 256 MiB Infinity Cache before every launch
+        ts = []
+        for _ in range(iters // 2):
+            COLD.add_(1)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            launch()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3)
+        ts.sort()
+        return ts[len(ts) // 2]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -120,18 +134,28 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--arch", default="DFormer-Base")
     ap.add_argument("--decoder", default="ham")
+    ap.add_argument("--no-splits", action="store_true", help="time only the default split choice")
+    ap.add_argument("--cold", action="store_true", help="operands evicted from L2 / Infinity Cache per launch")
+    ap.add_argument("--replay", default="", help="replay the shapes of an earlier sweep JSON instead of capturing")
     args = ap.parse_args()
-    tr = capture(args.batch, args.arch, args.decoder)
+    global COLD
+    if args.cold:
+        COLD = torch.zeros(256 << 20, device="cuda")
     groups = collections.OrderedDict()
-    for d in tr:
-        groups.setdefault(key(d), [d, 0])[1] += 1
+    if args.replay:
+        for r in json.load(open(args.replay))["rows"]:
+            d = dict(r["desc"])
+            groups[key(d)] = [d, r["count"]]
+    else:
+        for d in capture(args.batch, args.arch, args.decoder):
+            groups.setdefault(key(d), [d, 0])[1] += 1
     rows = []
     for _, (d, cnt) in groups.items():
         nbytes, flops = algo(d)
         r = {"count": cnt, "desc": {k: (bool(v) if k in PTR_FIELDS else v) for k, v in d.items()},
              "bytes": nbytes, "flops": flops, "t_default": replay(d, 0)}
         cands = {}
-        for sp in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        for sp in (() if args.no_splits else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
             if sp > 1 and d["K"] // sp < 256:
                 break
             cands[sp] = replay(d, sp)
@@ -140,10 +164,11 @@ def main():
         rows.append(r)
         print(f"{cnt:3d}x M={d['M']:6d} N={d['N']:5d} K={d['K']:6d} b={d['batch']:3d} ak={d['a_kcontig']} "
               f"bk={d['b_kcontig']} dt={d['dtype']} def={r['t_default']:8.1f}us best="
-              f"{min(cands.values()):8.1f}us@{min(cands, key=cands.get):3d} ideal={r['ideal_us']:7.1f}us",
+              f"{min(cands.values(), default=r['t_default']):8.1f}us@{min(cands, key=cands.get, default=0):3d} "
+              f"ideal={r['ideal_us']:7.1f}us",
               flush=True)
     tot_def = sum(r["count"] * r["t_default"] for r in rows) / 1e3
-    tot_best = sum(r["count"] * min(r["t_split"].values()) for r in rows) / 1e3
+    tot_best = sum(r["count"] * min(r["t_split"].values(), default=r["t_default"]) for r in rows) / 1e3
     tot_ideal = sum(r["count"] * r["ideal_us"] for r in rows) / 1e3
     print(f"per step: default {tot_def:.2f} ms, best-split {tot_best:.2f} ms, ideal {tot_ideal:.2f} ms")
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
