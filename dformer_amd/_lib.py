@@ -73,8 +73,8 @@ _SIGS = {
     "dfm_bn_bwd_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_double, P, c_long, c_int,
                                  P]),
     "dfm_relu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P]),
-    "dfm_nmf_update": (c_int, [c_long, P, P, P, c_float, P, P]),
-    "dfm_nmf_update_bwd": (c_int, [c_long, P, P, P, P, P, c_float, P, c_int, P, P, P]),
+    "dfm_nmf_update": (c_int, [c_long, P, P, P, c_float, P, P, P]),
+    "dfm_nmf_update_bwd": (c_int, [c_long, P, P, P, P, P, c_float, P, c_int, P, P, P, P]),
     "dfm_softmax_rows": (c_int, [c_long, c_int, P, P, P]),
     "dfm_softmax_rows_bwd": (c_int, [c_long, c_int, P, P, P, c_int, P]),
     "dfm_seg_loss_workspace": (c_size_t, [c_int, c_int, c_int]),

@@ -387,21 +387,29 @@ __global__ void bn_bwd_apply_vec_kernel(long rows, int C, const T* __restrict__ 
 }
 
 // ---- NMF multiplicative update
+// out16 / gnum16 (optional): bf16 copies of the result for the bf16-operand NMF GEMMs
 __global__ void nmf_update_kernel(long n, const float* __restrict__ a, const float* __restrict__ num,
-                                  const float* __restrict__ den, float eps, float* __restrict__ out) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    out[i] = a[i] * num[i] / (den[i] + eps);
+                                  const float* __restrict__ den, float eps, float* __restrict__ out,
+                                  bf16_t* __restrict__ out16) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = a[i] * num[i] / (den[i] + eps);
+    out[i] = v;
+    if (out16) out16[i] = Num<bf16_t>::from_f(v);
+  }
 }
 __global__ void nmf_update_bwd_kernel(long n, const float* __restrict__ g, const float* __restrict__ a,
                                       const float* __restrict__ num, const float* __restrict__ den,
                                       const float* __restrict__ out, float eps, float* __restrict__ ga, int acc,
-                                      float* __restrict__ gnum, float* __restrict__ gden) {
+                                      float* __restrict__ gnum, float* __restrict__ gden,
+                                      bf16_t* __restrict__ gnum16) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float r = 1.f / (den[i] + eps);
     const float gi = g[i];
     const float v = gi * num[i] * r;
     ga[i] = acc ? ga[i] + v : v;
-    gnum[i] = gi * a[i] * r;
+    const float gn = gi * a[i] * r;
+    gnum[i] = gn;
+    if (gnum16) gnum16[i] = Num<bf16_t>::from_f(gn);
     gden[i] = -gi * out[i] * r;
   }
 }
@@ -586,17 +594,18 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
 }
 
 extern "C" int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
-                              dfm_stream_t stream) {
-  DFM_LAUNCH(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out);
+                              void* out16, dfm_stream_t stream) {
+  DFM_LAUNCH(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out,
+             (bf16_t*)out16);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
 extern "C" int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                                   const float* out, float eps, float* ga, int acc, float* gnum, float* gden,
-                                  dfm_stream_t stream) {
+                                  void* gnum16, dfm_stream_t stream) {
   DFM_LAUNCH(nmf_update_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den, out,
-                     eps, ga, acc, gnum, gden);
+                     eps, ga, acc, gnum, gden, (bf16_t*)gnum16);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -215,34 +215,48 @@ class ChannelDropoutLinearFn(torch.autograd.Function):
 
 # ======================================================================================= NMF
 class NMF2DFn(torch.autograd.Function):
-    """NMF2D.forward (ham_head.py:60-145) on NHWC: x [B, N, D] float32 (= the reference's x^T),
-    bases [B, D, R] injected or freshly drawn; gradients flow through every multiplicative step."""
+    """NMF2D.forward (ham_head.py:60-145) on NHWC: x [B, N, D] (= the reference's x^T), bases
+    [B, D, R] injected or freshly drawn; gradients flow through every multiplicative step.
+
+    x float32: every product in float32. x bfloat16 (the bf16 model; the reference's autocast runs
+    these bmm in bf16): the products that stream x (x B, x^T C and their backward twins) and the
+    output B C^T take bf16 operands with float32 accumulation; coef / bases, the small R x R
+    products and every multiplicative update stay float32 (nmf_update emits the bf16 operand copy)."""
 
     @staticmethod
     def forward(ctx, x, bases, steps, eps):
         x = x.contiguous()
+        lp = x.dtype == torch.bfloat16
         B0 = bases.contiguous()
-        coef = K.softmax_rows(K.bmm(x, B0))                      # softmax(x^T B)
+        f32 = dict(device=x.device, dtype=torch.float32)
+
+        def xmm(b16, a_t=False):  # x-streaming product, float32 out
+            Bb, N, D = x.shape
+            R = b16.shape[2]
+            return K.bmm(x, b16, a_t=a_t, out=torch.empty(Bb, D if a_t else N, R, **f32))
+
+        coef = K.softmax_rows(xmm(K.cast(B0, x.dtype) if lp else B0))   # softmax(x^T B)
         hist = []
         Bt, Ct = B0, coef
+        Bt16 = K.cast(B0, x.dtype) if lp else B0
         for _ in range(steps):
-            num1 = K.bmm(x, Bt)                                   # x^T B        [N,R]
+            num1 = xmm(Bt16)                                      # x^T B        [N,R]
             M = K.bmm(Bt, Bt, a_t=True)                           # B^T B        [R,R]
             den1 = K.bmm(Ct, M)                                   # C (B^T B)
-            Cn = K.nmf_update(Ct, num1, den1, eps)
-            num2 = K.bmm(x, Cn, a_t=True)                         # x C          [D,R]
+            Cn, Cn16 = K.nmf_update(Ct, num1, den1, eps, bf16_copy=True) if lp else (K.nmf_update(Ct, num1, den1, eps),) * 2
+            num2 = xmm(Cn16, a_t=True)                            # x C          [D,R]
             Q = K.bmm(Cn, Cn, a_t=True)                           # C^T C        [R,R]
             den2 = K.bmm(Bt, Q)                                   # B (C^T C)
-            Bn = K.nmf_update(Bt, num2, den2, eps)
-            hist.append((Bt, Ct, num1, M, den1, Cn, num2, Q, den2, Bn))
-            Bt, Ct = Bn, Cn
-        num = K.bmm(x, Bt)
+            Bn, Bn16 = K.nmf_update(Bt, num2, den2, eps, bf16_copy=True) if lp else (K.nmf_update(Bt, num2, den2, eps),) * 2
+            hist.append((Bt, Ct, num1, M, den1, Cn, Cn16, num2, Q, den2, Bn))
+            Bt, Ct, Bt16 = Bn, Cn, Bn16
+        num = xmm(Bt16)
         M = K.bmm(Bt, Bt, a_t=True)
         den = K.bmm(Ct, M)
-        Cf = K.nmf_update(Ct, num, den, eps)
-        y = K.bmm(Cf, Bt, b_t=True)                               # (B C^T)^T    [N,D]
+        Cf, Cf16 = K.nmf_update(Ct, num, den, eps, bf16_copy=True) if lp else (K.nmf_update(Ct, num, den, eps),) * 2
+        y = K.bmm(Cf16, Bt16, b_t=True)                           # (B C^T)^T    [N,D], x.dtype
         ctx.hist = hist
-        ctx.final = (Bt, Ct, num, M, den, Cf)
+        ctx.final = (Bt, Bt16, Ct, num, M, den, Cf, Cf16)
         ctx.eps = eps
         ctx.save_for_backward(x, B0, coef)
         return y
@@ -252,18 +266,25 @@ class NMF2DFn(torch.autograd.Function):
         K.TAG = "decoder.bwd"
         x, B0, coef0 = ctx.saved_tensors
         eps = ctx.eps
+        lp = x.dtype == torch.bfloat16
         gy = gy.contiguous()
         Bb, N, D = x.shape
         R = B0.shape[2]
-        Bt, Ct, num, M, den, Cf = ctx.final
-        gC = K.bmm(gy, Bt)                                        # gy B         [N,R]
-        gB = K.bmm(gy, Cf, a_t=True)                              # gy^T C       [D,R]
+        f32 = dict(device=x.device, dtype=torch.float32)
+        Bt, Bt16, Ct, num, M, den, Cf, Cf16 = ctx.final
+        gC = K.bmm(gy, Bt16, out=torch.empty(Bb, N, R, **f32))   # gy B         [N,R]
+        gB = K.bmm(gy, Cf16, a_t=True, out=torch.empty(Bb, D, R, **f32))  # gy^T C  [D,R]
+
+        def upd_bwd(g, a, nm, dn, out):  # -> ga, gnum, gden, gnum operand for the x products
+            r = K.nmf_update_bwd(g, a, nm, dn, out, eps=eps, bf16_copy=lp)
+            return r if lp else (*r, r[1])
+
         # Every contribution to gx is a rank-R product P Q^T (P [N,R], Q [D,R]); they are gathered
         # side by side and applied by ONE GEMM over the concatenated K = T*R at the end, instead of
         # T read-modify-write passes over the [N, D] gradient.
         T = 2 * len(ctx.hist) + 2
-        Pc = torch.empty(Bb, N, T * R, device=x.device, dtype=torch.float32)
-        Qc = torch.empty(Bb, D, T * R, device=x.device, dtype=torch.float32)
+        Pc = torch.empty(Bb, N, T * R, device=x.device, dtype=x.dtype)
+        Qc = torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype)
         slot = [0]
 
         def gx_term(P, Q):
@@ -273,31 +294,31 @@ class NMF2DFn(torch.autograd.Function):
             slot[0] += 1
 
         # final coef update: Cf = Ct * num / (Ct M + eps), num = x B, M = B^T B
-        gCt, gnum, gden = K.nmf_update_bwd(gC, Ct, num, den, Cf, eps=eps)
+        gCt, gnum, gden, gnum16 = upd_bwd(gC, Ct, num, den, Cf)
         gx_term(gnum, Bt)                                         # gx += gnum B^T
-        K.bmm(x, gnum, a_t=True, out=gB, beta=1.0)                # gB += x^T gnum
+        K.bmm(x, gnum16, a_t=True, out=gB, beta=1.0)              # gB += x^T gnum
         _acc_CM(gCt, gB, Ct, Bt, M, gden)
         gC = gCt
-        for (Bp, Cp, num1, M1, den1, Cn, num2, Q, den2, Bn) in reversed(ctx.hist):
+        for (Bp, Cp, num1, M1, den1, Cn, Cn16, num2, Q, den2, Bn) in reversed(ctx.hist):
             # B-update: Bn = Bp * num2 / (Bp Q + eps), num2 = x^T-side (x C_n), Q = Cn^T Cn
-            gBp, gnum2, gden2 = K.nmf_update_bwd(gB, Bp, num2, den2, Bn, eps=eps)
+            gBp, gnum2, gden2, gnum2_16 = upd_bwd(gB, Bp, num2, den2, Bn)
             gx_term(Cn, gnum2)                                    # gx += Cn gnum2^T
-            K.bmm(x, gnum2, out=gC, beta=1.0)                     # gCn += x gnum2
+            K.bmm(x, gnum2_16, out=gC, beta=1.0)                  # gCn += x gnum2
             K.bmm(gden2, Q, out=gBp, beta=1.0)                    # gBp += gden2 Q
             gQ = K.bmm(Bp, gden2, a_t=True)                       # Bp^T gden2
             K.bmm(Cn, gQ, out=gC, beta=1.0)
             K.bmm(Cn, gQ, b_t=True, out=gC, beta=1.0)
             # C-update: Cn = Cp * num1 / (Cp M1 + eps), num1 = x B_p, M1 = Bp^T Bp
-            gCp, gnum1, gden1 = K.nmf_update_bwd(gC, Cp, num1, den1, Cn, eps=eps)
+            gCp, gnum1, gden1, gnum1_16 = upd_bwd(gC, Cp, num1, den1, Cn)
             gx_term(gnum1, Bp)                                    # gx += gnum1 Bp^T
-            K.bmm(x, gnum1, a_t=True, out=gBp, beta=1.0)          # gBp += x^T gnum1
+            K.bmm(x, gnum1_16, a_t=True, out=gBp, beta=1.0)       # gBp += x^T gnum1
             _acc_CM(gCp, gBp, Cp, Bp, M1, gden1)
             gB, gC = gBp, gCp
         # coef0 = softmax(x B0)  (B0 is a random constant)
         gS = K.softmax_rows_bwd(coef0, gC)
         gx_term(gS, B0)                                           # gx += gS B0^T
         assert slot[0] == T
-        gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T
+        gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T, x.dtype
         ctx.hist = ctx.final = None
         return gx, None, None, None
 
@@ -344,7 +365,7 @@ class NMF2D(nn.Module):
         return b / b.norm(dim=1, keepdim=True).clamp_min(1e-12)  # F.normalize(dim=1)
 
     def fused(self, x, B, N):
-        """x: [B*N, D] float32 rows -> [B*N, D] float32."""
+        """x: [B*N, D] rows (float32, or bf16 for the bf16 model) -> [B*N, D] rows of x.dtype."""
         D = x.shape[1]
         bases = self._build_bases(B, D, x.device)
         steps = self.train_steps if self.training else self.eval_steps
@@ -360,7 +381,7 @@ class Hamburger(nn.Module):
         self.ham_out = ConvModule(ham_channels, ham_channels, norm=True, bn_eps=bn_eps)
 
     def fused(self, x, B, N, sync):
-        enjoy = LinearActFn.apply(x, self.ham_in.conv.weight, self.ham_in.conv.bias, 2, True)
+        enjoy = LinearActFn.apply(x, self.ham_in.conv.weight, self.ham_in.conv.bias, 2, False)
         enjoy = self.ham.fused(enjoy, B, N)
         enjoy = CastFn.apply(enjoy, x.dtype)
         return self.ham_out.fused(enjoy, act=2, res=x, sync=sync)  # relu(x + BN(conv(enjoy)))

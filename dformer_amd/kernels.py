@@ -502,26 +502,31 @@ def bn_bwd_apply(x, dy, mean, rstd, gamma, stats2, count, dx=None, accumulate=Fa
 
 
 # ---------------------------------------------------------------------------------------- NMF
-def nmf_update(a, num, den, eps=1e-6, out=None):
+def nmf_update(a, num, den, eps=1e-6, out=None, bf16_copy=False):
+    """out = a * num / (den + eps) (float32); with bf16_copy also returns a bf16 copy of out."""
     if out is None:
         out = torch.empty_like(a)
-    check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), stream()), "dfm_nmf_update")
+    o16 = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if bf16_copy else None
+    check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), ptr(o16), stream()),
+          "dfm_nmf_update")
     if ACCOUNT is not None:
-        _acct(0, a.numel() * 16)
-    return out
+        _acct(0, a.numel() * (16 + 2 * bool(bf16_copy)))
+    return (out, o16) if bf16_copy else out
 
 
-def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6):
+def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6, bf16_copy=False):
+    """-> ga, gnum, gden (float32) [, bf16 copy of gnum]."""
     if ga is None:
         ga = torch.empty_like(a)
         accumulate = False
     gnum = torch.empty_like(a)
     gden = torch.empty_like(a)
+    g16 = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if bf16_copy else None
     check(lib.dfm_nmf_update_bwd(a.numel(), ptr(g), ptr(a), ptr(num), ptr(den), ptr(out), eps, ptr(ga),
-                                 int(accumulate), ptr(gnum), ptr(gden), stream()), "dfm_nmf_update_bwd")
+                                 int(accumulate), ptr(gnum), ptr(gden), ptr(g16), stream()), "dfm_nmf_update_bwd")
     if ACCOUNT is not None:
-        _acct(0, a.numel() * 4 * (8 + bool(accumulate)))
-    return ga, gnum, gden
+        _acct(0, a.numel() * (4 * (8 + bool(accumulate)) + 2 * bool(bf16_copy)))
+    return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
 
 
 def softmax_rows(x):

@@ -235,12 +235,14 @@ int dfm_relu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const v
 /* ---------------------------------------------------------------- NMF2D multiplicative update
  * ham_head.py:120-145:  out = a * num / (den + eps)  (float32), and its backward:
  *   ga (+= when accumulate_ga) = g * num / (den+eps);  gnum = g * a / (den+eps);
- *   gden = -g * out / (den+eps). */
+ *   gden = -g * out / (den+eps).
+ * out16 / gnum16 (nullable): bf16 copies of out / gnum, the operands of the bf16 NMF GEMMs (the
+ * reference's autocast runs ham_head.py's bmm in bf16). */
 int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
-                   dfm_stream_t stream);
+                   void* out16, dfm_stream_t stream);
 int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                        const float* out, float eps, float* ga, int accumulate_ga, float* gnum, float* gden,
-                       dfm_stream_t stream);
+                       void* gnum16, dfm_stream_t stream);
 /* row softmax over R (NMF coef init, ham_head.py:48-49) and its backward */
 int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream);
 int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int accumulate,
