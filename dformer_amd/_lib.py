@@ -82,6 +82,7 @@ _SIGS = {
     "dfm_seg_loss_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P, P]),
     "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, P]),
+    "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, P]),
     "dfm_convffn_supported": (c_int, [c_int, c_int, c_int]),
     "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
                                 P, P, c_long, P, c_long, P]),

@@ -459,6 +459,25 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
     if (copy) copy[i] = f2bf(pi);
   }
 }
+// Same update with lr and step read from device memory (hyper = [lr, step]), so a captured HIP
+// graph replays every optimizer step without host-baked scalars.
+__global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, const float* __restrict__ hyper, float b1, float b2,
+                                 float eps, float wd, float gscale, bf16_t* __restrict__ copy) {
+  const float lr = hyper[0], step = hyper[1];
+  const float bc1 = 1.f - powf(b1, step), bc2_sqrt = sqrtf(1.f - powf(b2, step));
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
+    p[i] = pi;
+    if (copy) copy[i] = f2bf(pi);
+  }
+}
 }  // namespace
 
 // ================================================================ C ABI
@@ -632,6 +651,16 @@ extern "C" int dfm_adamw(long n, float* p, const float* g, float* m, float* v, f
   const float bc2 = 1.f - powf(beta2, (float)step);
   DFM_LAUNCH(adamw_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1, beta2,
                      eps, wd, bc1, sqrtf(bc2), gscale, (bf16_t*)bf16_copy);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* v, const float* hyper, float beta1,
+                             float beta2, float eps, float wd, float gscale, void* bf16_copy, dfm_stream_t stream) {
+  DFM_CHECK_ARG(p && g && m && v && hyper, "dfm_adamw_dev: bad argument");
+  if (n == 0) return DFM_OK;
+  DFM_LAUNCH(adamw_dev_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper, beta1,
+             beta2, eps, wd, gscale, (bf16_t*)bf16_copy);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -572,8 +572,14 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
 
 
 # -------------------------------------------------------------------------------------- AdamW
-def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None):
-    check(lib.dfm_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), lr, beta1, beta2, eps, weight_decay, step,
-                        grad_scale, ptr(bf16_copy), stream()), "dfm_adamw")
+def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None, hyper=None):
+    """AdamW step; with `hyper` (device float32 [lr, step]) lr and step are read on the device
+    (lr / step arguments ignored) so the launch can live in a replayed HIP graph."""
+    if hyper is not None:
+        check(lib.dfm_adamw_dev(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(hyper), beta1, beta2, eps,
+                                weight_decay, grad_scale, ptr(bf16_copy), stream()), "dfm_adamw_dev")
+    else:
+        check(lib.dfm_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), lr, beta1, beta2, eps, weight_decay, step,
+                            grad_scale, ptr(bf16_copy), stream()), "dfm_adamw")
     if ACCOUNT is not None:
         _acct(0, p.numel() * (28 + (2 if bf16_copy is not None else 0)))

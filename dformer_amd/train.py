@@ -170,6 +170,11 @@ class FusedAdamW:
         self.lr, self.betas, self.eps = lr, betas, eps
         self.world = world
         self.step_count = 0
+        # [lr, step] on the device, read by the AdamW kernel: the same arithmetic whether the step
+        # runs eagerly (step() refreshes it) or replays from a captured graph (the graph's owner
+        # refreshes it before every replay and sets external_hyper)
+        self.hyper = torch.zeros(2, device=dev, dtype=torch.float32)
+        self.external_hyper = False
         self.buckets = GradBuckets(self.groups, world, bucket_bytes)
         grouped = {id(p) for g in self.groups for p in g.params}
         # layer_scale_* and the custom LayerNorm params: in no group (never updated, like the reference)
@@ -184,9 +189,12 @@ class FusedAdamW:
             p.grad = None
         self.step_count += 1
         lr = self.lr if lr is None else lr
+        if not self.external_hyper:
+            self.hyper[0].fill_(lr)
+            self.hyper[1].fill_(float(self.step_count))
         for g in self.groups:
             K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, self.step_count,
-                    1.0 / self.world, g.shadow)
+                    1.0 / self.world, g.shadow, hyper=self.hyper)
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
@@ -254,6 +262,52 @@ def all_reduce_mean(t, world):
         dist.all_reduce(t)
         t = t / world
     return t
+
+
+class GraphedTrainStep:
+    """train_step captured once into a HIP graph (torch.cuda.graph) and replayed: the whole
+    forward + loss + backward + AdamW step of ~2.3k kernel launches becomes one graph launch, so
+    the host (~23 us of Python / autograd per eager launch) no longer paces the device.
+
+    rgb / depth / label are the static input buffers: copy each new batch into them in place. The
+    optimizer's lr and step count live in a device tensor refreshed before every replay (the only
+    per-step host state of the step); dropout / DropPath draws advance with torch's graph-safe
+    Philox offsets. Needs every kernel of the step on torch's current stream or streams forked from
+    it (true of this package) and no host synchronisation inside the step."""
+
+    def __init__(self, model, opt, rgb, depth, label, warmup=2):
+        self.model, self.opt = model, opt
+        self.inputs = (rgb, depth, label)
+        side = torch.cuda.Stream(device=rgb.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):  # warm-up on a side stream, as torch.cuda.graph requires
+            for _ in range(warmup):
+                train_step(model, opt, rgb, depth, label)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        opt.external_hyper = True  # inside the graph AdamW only reads hyper
+        try:
+            with torch.cuda.graph(self.graph):
+                self.loss = train_step(model, opt, rgb, depth, label)  # host step_count advanced once here
+        finally:
+            opt.external_hyper = False
+
+    def _set_hyper(self, lr, step):
+        self.opt.hyper[0].fill_(self.opt.lr if lr is None else lr)
+        self.opt.hyper[1].fill_(float(step))
+
+    def __call__(self, lr=None):
+        """One training step (the first call replays the captured step itself)."""
+        if getattr(self, "_replayed", False):
+            self.opt.step_count += 1
+        self._replayed = True
+        self._set_hyper(lr, self.opt.step_count)
+        self.graph.replay()
+        return self.loss
+
+    def eager(self, lr=None):
+        """One step issued from Python on the same model / optimizer / inputs (probe windows)."""
+        return train_step(self.model, self.opt, *self.inputs, lr=lr)
 
 
 def train_step(model, opt, rgb, depth, label, lr=None):

@@ -270,6 +270,11 @@ int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logit
 int dfm_adamw(long n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
               float eps, float weight_decay, int step, float grad_scale, void* bf16_copy,
               dfm_stream_t stream);
+/* The same step with lr and step (as float) read from device memory hyper[2] = {lr, step}: what a
+ * captured HIP graph of the whole training step calls, the host refreshing hyper before a replay. */
+int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* v, const float* hyper, float beta1,
+                  float beta2, float eps, float weight_decay, float grad_scale, void* bf16_copy,
+                  dfm_stream_t stream);
 
 #ifdef __cplusplus
 }
