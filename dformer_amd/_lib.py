@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdformer_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 
 c_int, c_long, c_float, c_double, c_void_p, c_size_t = (ctypes.c_int, ctypes.c_long, ctypes.c_float,
                                                          ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t)
@@ -73,16 +73,31 @@ _SIGS = {
     "dfm_bn_bwd_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_double, P, c_long, c_int,
                                  P]),
     "dfm_relu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P]),
-    "dfm_nmf_update": (c_int, [c_long, P, P, P, c_float, P, P, P]),
-    "dfm_nmf_update_bwd": (c_int, [c_long, P, P, P, P, P, c_float, P, c_int, P, P, P, P]),
+    "dfm_conv3s2_im2col": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_long, P, P, P,
+                                   P, P, c_int, c_int, P, P]),
+    "dfm_conv3s2_col2im": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, c_int, P,
+                                   c_long, c_int, P]),
+    "dfm_conv3s2_col2im_nchw": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_long,
+                                        c_long, c_long, P]),
+    "dfm_conv3_weight_pack": (c_int, [c_int, c_int, c_int, c_int, P, P, P]),
+    "dfm_conv3_weight_unpack": (c_int, [c_int, c_int, c_int, P, P, c_int, P]),
+    "dfm_resize_nchw": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_long, c_long, c_long, c_long, P, c_int,
+                                c_int, c_int, c_int, P, P]),
+    "dfm_msf_accumulate": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, c_int, c_int, c_int, c_int, c_int,
+                                   P, P]),
+    "dfm_seg_confusion": (c_int, [c_long, c_int, P, P, c_int, P, P]),
+    "dfm_nmf_update": (c_int, [c_long, P, P, P, c_float, P, P, c_int, P]),
+    "dfm_nmf_update_bwd": (c_int, [c_long, P, P, P, P, P, c_float, P, c_int, P, P, P, c_int, P]),
+    "dfm_grad_nonfinite": (c_int, [c_long, P, P, P]),
     "dfm_softmax_rows": (c_int, [c_long, c_int, P, P, P]),
     "dfm_softmax_rows_bwd": (c_int, [c_long, c_int, P, P, P, c_int, P]),
     "dfm_seg_loss_workspace": (c_size_t, [c_int, c_int, c_int]),
     "dfm_seg_loss_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P]),
     "dfm_seg_loss_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P, P]),
-    "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, P]),
-    "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, P]),
+    "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, c_int,
+                          P]),
+    "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),
     "dfm_convffn_supported": (c_int, [c_int, c_int, c_int]),
     "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
                                 P, P, c_long, P, c_long, P]),
@@ -122,6 +137,8 @@ def dtype_code(t):
         return F32
     if t.dtype == torch.bfloat16:
         return BF16
+    if t.dtype == torch.float16:
+        return F16
     raise TypeError(f"dformer_amd: unsupported dtype {t.dtype}")
 
 

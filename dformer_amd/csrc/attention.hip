@@ -537,11 +537,11 @@ DFM_INLINE bf16x8_t frag_tr(const bf16_t* lds, int LD, int r0, int k0, int lane)
   return __builtin_bit_cast(bf16x8_t, sv);
 }
 DFM_INLINE void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-#define MFMA16(A, B, C) __builtin_amdgcn_mfma_f32_16x16x32_bf16((A), (B), (C), 0, 0, 0)
+#define MFMA16(A, B, C) mma16<T>((A), (B), (C))
 
 // Forward: S^T = K Q^T (keys as rows), online softmax per query, O^T += V^T P^T.
 // Partials per wave (chunk): unnormalised O [49][DH], running max m and sum l (scaled units).
-template <int DH>
+template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw, int groups) {
   constexpr int KD = (DH + 31) / 32, ND = DH / 16, LDV = DH + 8;
   __shared__ __attribute__((aligned(16))) bf16_t sV[4][32 * LDV];
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
       mrun[nt] = mnew;
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt) o[dt][nt] *= alpha;
-      pf[nt] = pack_bf16x8(sv8);
+      pf[nt] = pack16x8<T>(sv8);
     }
     lds_wave_sync();
 #pragma unroll
@@ -663,7 +663,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
 // Backward per wave chunk: S' = Q K^T and dP' = dO V^T with keys as columns (lane = key), then
 // P' = exp(S' scale - lse), dS' = P' (dP' - D); dV^T += dO^T P', dK^T += Q^T dS' (scale), both
 // complete per 32-key block and stored directly; dQ^T += K^T dS'^T through LDS (partial per chunk).
-template <int DH>
+template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw, int groups) {
   constexpr int KD = (DH + 31) / 32, ND = DH / 16, LDD = DH + 8, LDQ = 64 + 8;
   __shared__ __attribute__((aligned(16))) bf16_t sQ[64 * LDD], sO[64 * LDD];
@@ -693,8 +693,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
     if (q < NQ) {
       for (int d = 0; d < DH; d += 8) {
         float x[8], y[8];
-        ld8<bf16_t>(GO + (long)q * a.lddo + d, x);
-        ld8<bf16_t>(Op + (long)q * a.ldo + d, y);
+        ld8<T>((const T*)(GO + (long)q * a.lddo + d), x);
+        ld8<T>((const T*)(Op + (long)q * a.ldo + d), y);
 #pragma unroll
         for (int e = 0; e < 8; ++e) dsum += x[e] * y[e];
       }
@@ -792,8 +792,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
           p8[e] = p;
           ds8[e] = p * (dp[e >> 2][e & 3] - Dq[qb][e]);
         }
-        pb[kt][qb] = pack_bf16x8(p8);
-        dsb[kt][qb] = pack_bf16x8(ds8);
+        pb[kt][qb] = pack16x8<T>(p8);
+        dsb[kt][qb] = pack16x8<T>(ds8);
         // dS' row (key) -> LDS [key][q] for the dS^T operand of dQ
         *reinterpret_cast<bf16x8_t*>(ss + (16 * kt + j) * LDQ + 32 * qb + 8 * g) = dsb[kt][qb];
       }
@@ -813,10 +813,10 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
         if (key < n1) {
           const int d = 16 * dt + 4 * g;
           uint2 uv, uk;
-          uv.x = (uint32_t)f2bf(v4[0]) | ((uint32_t)f2bf(v4[1]) << 16);
-          uv.y = (uint32_t)f2bf(v4[2]) | ((uint32_t)f2bf(v4[3]) << 16);
-          uk.x = (uint32_t)f2bf(k4[0] * a.scale) | ((uint32_t)f2bf(k4[1] * a.scale) << 16);
-          uk.y = (uint32_t)f2bf(k4[2] * a.scale) | ((uint32_t)f2bf(k4[3] * a.scale) << 16);
+          uv.x = (uint32_t)bits16<T>(v4[0]) | ((uint32_t)bits16<T>(v4[1]) << 16);
+          uv.y = (uint32_t)bits16<T>(v4[2]) | ((uint32_t)bits16<T>(v4[3]) << 16);
+          uk.x = (uint32_t)bits16<T>(k4[0] * a.scale) | ((uint32_t)bits16<T>(k4[1] * a.scale) << 16);
+          uk.y = (uint32_t)bits16<T>(k4[2] * a.scale) | ((uint32_t)bits16<T>(k4[3] * a.scale) << 16);
           *reinterpret_cast<uint2*>(dV + (long)key * a.lddkv + d) = uv;
           *reinterpret_cast<uint2*>(dK + (long)key * a.lddkv + d) = uk;
         }
@@ -846,11 +846,26 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
 }
 #undef MFMA16
 
+// dst[r][h*ddst + d] = d < dsrc ? src[r][h*dsrc + d] : 0   (2-byte elements, d < ddst)
+__global__ void head_repack_kernel(long rows, int heads, int dsrc, long lds, int ddst, long ldd,
+                                   const uint16_t* __restrict__ src, uint16_t* __restrict__ dst) {
+  const long n = rows * heads * ddst;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % ddst);
+    const long t = i / ddst;
+    const int h = (int)(t % heads);
+    const long r = t / heads;
+    dst[r * ldd + (long)h * ddst + d] = d < dsrc ? src[r * lds + (long)h * dsrc + d] : (uint16_t)0;
+  }
+}
+
 unsigned grid_for(long n) { return (unsigned)min((long)8192, max(1L, (n + 255) / 256)); }
 
-template <typename F8, typename F32>
-int dispatch(int dtype, F8 f8, F32 f32) {
-  if (dtype == DFM_BF16) return f8();
+// f16: the 16-bit lambda is generic over its storage type (bf16_t or f16_t)
+template <typename F16, typename F32>
+int dispatch(int dtype, F16 f16, F32 f32) {
+  if (dtype == DFM_BF16) return f16(bf16_t{});
+  if (dtype == DFM_F16) return f16(f16_t{});
   if (dtype == DFM_F32) return f32();
   dfm_set_error("attention: bad dtype");
   return DFM_ERR_DTYPE;
@@ -864,9 +879,10 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,
-        [&] {
-          DFM_LAUNCH(pool7_fwd_vec_kernel<bf16_t>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
-                             (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
+        [&](auto tag16) {
+        using T16 = decltype(tag16);
+          DFM_LAUNCH(pool7_fwd_vec_kernel<T16>, dim3(B * 49), dim3(256), lds, s, B, H, W, C,
+                             (const T16*)x, ldx, (T16*)y, ldy);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
@@ -880,8 +896,9 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
   dim3 grid(B * 49, cdiv(C, 256));
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(pool7_fwd_kernel<bf16_t>, grid, dim3(256), 0, s, B, H, W, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(pool7_fwd_kernel<T16>, grid, dim3(256), 0, s, B, H, W, C, (const T16*)x, ldx, (T16*)y, ldy);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
@@ -899,9 +916,10 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
     const unsigned gv = grid_for((long)B * H * W * (C / 8));
     return dispatch(
         dtype,
-        [&] {
-          DFM_LAUNCH(pool7_bwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy,
-                             lddy, (bf16_t*)dx, lddx, accumulate);
+        [&](auto tag16) {
+        using T16 = decltype(tag16);
+          DFM_LAUNCH(pool7_bwd_vec_kernel<T16>, dim3(gv), dim3(256), 0, s, B, H, W, C, (const T16*)dy,
+                             lddy, (T16*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
@@ -915,8 +933,9 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
   const unsigned g = grid_for((long)B * H * W * C);
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(pool7_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, H, W, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(pool7_bwd_kernel<T16>, dim3(g), dim3(256), 0, s, B, H, W, C, (const T16*)dy, lddy, (T16*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
@@ -934,9 +953,10 @@ extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
     const unsigned gv = grid_for((long)B * Ho * Wo * (C / 8));
     return dispatch(
         dtype,
-        [&] {
-          DFM_LAUNCH(bilinear_fwd_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
-                             (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
+        [&](auto tag16) {
+        using T16 = decltype(tag16);
+          DFM_LAUNCH(bilinear_fwd_vec_kernel<T16>, dim3(gv), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C,
+                             (const T16*)x, ldx, (T16*)y, ldy, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
@@ -950,8 +970,9 @@ extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   const unsigned g = grid_for((long)B * Ho * Wo * C);
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(bilinear_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)x, ldx, (bf16_t*)y, ldy, accumulate);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(bilinear_fwd_kernel<T16>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const T16*)x, ldx, (T16*)y, ldy, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
@@ -971,9 +992,10 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,
-        [&] {
-          DFM_LAUNCH(bilinear_bwd_vec_kernel<bf16_t>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
-                             C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+        [&](auto tag16) {
+        using T16 = decltype(tag16);
+          DFM_LAUNCH(bilinear_bwd_vec_kernel<T16>, dim3(B * Hi * Wi), dim3(256), lds, s, B, Hi, Wi, Ho, Wo,
+                             C, (const T16*)dy, lddy, (T16*)dx, lddx, accumulate);
           DFM_LAUNCH_CHECK();
           return DFM_OK;
         },
@@ -987,8 +1009,9 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   const unsigned g = grid_for((long)B * Hi * Wi * C);
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(bilinear_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const bf16_t*)dy, lddy, (bf16_t*)dx, lddx, accumulate);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(bilinear_bwd_kernel<T16>, dim3(g), dim3(256), 0, s, B, Hi, Wi, Ho, Wo, C, (const T16*)dy, lddy, (T16*)dx, lddx, accumulate);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
@@ -1003,30 +1026,66 @@ static int nchunks(int N) { return (N + NC - 1) / NC; }
 
 // bf16 MFMA path: head dim a multiple of 16 (<= 48), 16-byte aligned rows
 static bool attn_mfma_ok(int dtype, int dh, const void* const* ptrs, const long* lds, int n) {
-  if (dtype != DFM_BF16 || !(dh == 16 || dh == 32 || dh == 48)) return false;
+  if ((dtype != DFM_BF16 && dtype != DFM_F16) || !(dh == 16 || dh == 32 || dh == 48)) return false;
   for (int i = 0; i < n; ++i)
     if ((uintptr_t)ptrs[i] % 16 != 0 || lds[i] % 8 != 0) return false;
   return true;
 }
+// Other bf16 head dims below 48 (DFormer-Large: 576 / 16 heads = 36 in stages 2-3) run the same
+// MFMA kernels on head slices zero-padded to the next multiple of 16 in the workspace: padded
+// dims add 0 to Q K^T and produce 0 output columns, which the unpack drops.
+static int attn_pad_dh(int dtype, int dh) {
+  if ((dtype != DFM_BF16 && dtype != DFM_F16) || dh % 16 == 0 || dh > 48) return 0;
+  return (dh + 15) / 16 * 16;
+}
 static int attn_kpw(int N) { return N >= 2048 ? 128 : 64; }  // keys per wave (a multiple of 32 and of NC)
 
-template <int DH>
+template <typename T, int DH>
 static void attn_mfma_launch(AttnArgs& a, bool bwd, hipStream_t s) {
   const int kpw = attn_kpw(a.N);
   const int groups = (a.nchunk + 3) / 4;
   const dim3 grid((unsigned)(a.B * a.heads * groups));
-  if (bwd) DFM_LAUNCH(attn_bwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
-  else DFM_LAUNCH(attn_fwd_mfma_kernel<DH>, grid, dim3(256), 0, s, a, kpw, groups);
+  if (bwd) DFM_LAUNCH((attn_bwd_mfma_kernel<T, DH>), grid, dim3(256), 0, s, a, kpw, groups);
+  else DFM_LAUNCH((attn_fwd_mfma_kernel<T, DH>), grid, dim3(256), 0, s, a, kpw, groups);
 }
-static void attn_mfma(AttnArgs& a, bool bwd, hipStream_t s) {
-  if (a.dh == 16) attn_mfma_launch<16>(a, bwd, s);
-  else if (a.dh == 32) attn_mfma_launch<32>(a, bwd, s);
-  else attn_mfma_launch<48>(a, bwd, s);
+template <typename T>
+static void attn_mfma_t(AttnArgs& a, bool bwd, hipStream_t s) {
+  if (a.dh == 16) attn_mfma_launch<T, 16>(a, bwd, s);
+  else if (a.dh == 32) attn_mfma_launch<T, 32>(a, bwd, s);
+  else attn_mfma_launch<T, 48>(a, bwd, s);
+}
+// the 16-bit MFMA kernels (bf16 / f16 storage) and their combine / dQ-reduce kernels
+static void attn_mfma(int dtype, AttnArgs& a, bool bwd, hipStream_t s) {
+  if (dtype == DFM_F16) attn_mfma_t<f16_t>(a, bwd, s);
+  else attn_mfma_t<bf16_t>(a, bwd, s);
+}
+static void attn_combine16(int dtype, AttnArgs& a, unsigned g, hipStream_t s) {
+  if (dtype == DFM_F16) DFM_LAUNCH(attn_fwd_combine_kernel<f16_t>, dim3(g), dim3(256), 0, s, a);
+  else DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+}
+static void attn_dq_reduce16(int dtype, AttnArgs& a, unsigned g, hipStream_t s) {
+  if (dtype == DFM_F16) DFM_LAUNCH(attn_dq_reduce_kernel<f16_t>, dim3(g), dim3(256), 0, s, a);
+  else DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
 }
 
+static size_t attn_partials_bytes(int B, int heads, int N, int dh) {
+  return ((size_t)B * heads * nchunks(N) * NQ * (dh + 2) * sizeof(float) + 255) / 256 * 256;
+}
+// padded-head buffers (bf16): Q, O, dO, dQ [B*49][heads*dp]; K, V, dK, dV [B*N][heads*dp]
+static size_t attn_pad_elems_q(int B, int heads, int dp) { return ((size_t)B * NQ * heads * dp + 127) / 128 * 128; }
+static size_t attn_pad_elems_k(int B, int heads, int N, int dp) { return ((size_t)B * N * heads * dp + 127) / 128 * 128; }
+
 extern "C" size_t dfm_pooled_attn_workspace(int B, int heads, int N, int dh) {
-  const long nchk = nchunks(N);
-  return (size_t)B * heads * nchk * NQ * (dh + 2) * sizeof(float);
+  const int dp = attn_pad_dh(DFM_BF16, dh);
+  if (dp == 0) return (size_t)B * heads * nchunks(N) * NQ * (dh + 2) * sizeof(float);
+  return attn_partials_bytes(B, heads, N, dp) +
+         (4 * attn_pad_elems_q(B, heads, dp) + 4 * attn_pad_elems_k(B, heads, N, dp)) * sizeof(uint16_t);
+}
+
+static void head_repack(long rows, int heads, int dsrc, long lds, int ddst, long ldd, const void* src, void* dst,
+                        hipStream_t s) {
+  DFM_LAUNCH(head_repack_kernel, dim3(grid_for(rows * heads * ddst)), dim3(256), 0, s, rows, heads, dsrc, lds, ddst,
+             ldd, (const uint16_t*)src, (uint16_t*)dst);
 }
 
 extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, const void* q, long ldq, const void* k,
@@ -1038,14 +1097,31 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
   a.B = B; a.heads = heads; a.N = N; a.dh = dh; a.nchunk = nchunks(N);
   a.q = q; a.ldq = ldq; a.k = k; a.v = v; a.ldkv = ldkv; a.scale = scale; a.o = o; a.ldo = ldo; a.lse = lse;
   a.ws = (float*)workspace;
+  if (const int dp = attn_pad_dh(dtype, dh)) {
+    uint16_t* pq = (uint16_t*)((char*)workspace + attn_partials_bytes(B, heads, N, dp));
+    uint16_t* po = pq + attn_pad_elems_q(B, heads, dp);
+    uint16_t* pk = po + attn_pad_elems_q(B, heads, dp);
+    uint16_t* pv = pk + attn_pad_elems_k(B, heads, N, dp);
+    const long ldp = (long)heads * dp;
+    head_repack((long)B * NQ, heads, dh, ldq, dp, ldp, q, pq, s);
+    head_repack((long)B * N, heads, dh, ldkv, dp, ldp, k, pk, s);
+    head_repack((long)B * N, heads, dh, ldkv, dp, ldp, v, pv, s);
+    a.dh = dp; a.q = pq; a.ldq = ldp; a.k = pk; a.v = pv; a.ldkv = ldp; a.o = po; a.ldo = ldp;
+    a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
+    attn_mfma(dtype, a, false, s);
+    attn_combine16(dtype, a, grid_for((long)B * heads * NQ * dp), s);
+    head_repack((long)B * NQ, heads, dp, ldp, dh, ldo, po, o, s);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
   {
     const void* ptrs[] = {q, k, v, o};
     const long lds_[] = {ldq, ldkv, ldkv, ldo};
     if (attn_mfma_ok(dtype, dh, ptrs, lds_, 4)) {
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
-      attn_mfma(a, false, s);
+      attn_mfma(dtype, a, false, s);
       DFM_LAUNCH_CHECK();
-      DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      attn_combine16(dtype, a, grid_for((long)B * heads * NQ * dh), s);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
@@ -1056,10 +1132,11 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
   const unsigned g = grid_for((long)B * heads * NQ * dh);
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(attn_fwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(attn_fwd_chunk_kernel<T16>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_fwd_combine_kernel<T16>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },
@@ -1084,14 +1161,41 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
   a.q = q; a.ldq = ldq; a.k = k; a.v = v; a.ldkv = ldkv; a.scale = scale; a.o = const_cast<void*>(o); a.ldo = ldo; a.lse = (float*)lse;
   a.dout = dout; a.lddo = lddo; a.dq = dq; a.dk = dk; a.dv = dv; a.lddkv = lddkv;
   a.ws = (float*)workspace;
+  if (const int dp = attn_pad_dh(dtype, dh)) {
+    const size_t eq = attn_pad_elems_q(B, heads, dp), ek = attn_pad_elems_k(B, heads, N, dp);
+    uint16_t* pq = (uint16_t*)((char*)workspace + attn_partials_bytes(B, heads, N, dp));
+    uint16_t* po = pq + eq;
+    uint16_t* pdo = po + eq;
+    uint16_t* pdq = pdo + eq;
+    uint16_t* pk = pdq + eq;
+    uint16_t* pv = pk + ek;
+    uint16_t* pdk = pv + ek;
+    uint16_t* pdv = pdk + ek;
+    const long ldp = (long)heads * dp;
+    head_repack((long)B * NQ, heads, dh, ldq, dp, ldp, q, pq, s);
+    head_repack((long)B * NQ, heads, dh, ldo, dp, ldp, o, po, s);
+    head_repack((long)B * NQ, heads, dh, lddo, dp, ldp, dout, pdo, s);
+    head_repack((long)B * N, heads, dh, ldkv, dp, ldp, k, pk, s);
+    head_repack((long)B * N, heads, dh, ldkv, dp, ldp, v, pv, s);
+    a.dh = dp; a.q = pq; a.ldq = ldp; a.k = pk; a.v = pv; a.ldkv = ldp; a.o = po; a.ldo = ldp;
+    a.dout = pdo; a.lddo = ldp; a.dq = pdq; a.dk = pdk; a.dv = pdv; a.lddkv = ldp;
+    a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
+    attn_mfma(dtype, a, true, s);
+    attn_dq_reduce16(dtype, a, grid_for((long)B * heads * NQ * dp), s);
+    head_repack((long)B * NQ, heads, dp, ldp, dh, ldq, pdq, dq, s);
+    head_repack((long)B * N, heads, dp, ldp, dh, lddkv, pdk, dk, s);
+    head_repack((long)B * N, heads, dp, ldp, dh, lddkv, pdv, dv, s);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
   {
     const void* ptrs[] = {q, k, v, o, dout, dq, dk, dv};
     const long lds_[] = {ldq, ldkv, ldkv, ldo, lddo, ldq, lddkv, lddkv};
     if (attn_mfma_ok(dtype, dh, ptrs, lds_, 8)) {
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
-      attn_mfma(a, true, s);
+      attn_mfma(dtype, a, true, s);
       DFM_LAUNCH_CHECK();
-      DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(grid_for((long)B * heads * NQ * dh)), dim3(256), 0, s, a);
+      attn_dq_reduce16(dtype, a, grid_for((long)B * heads * NQ * dh), s);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
@@ -1102,10 +1206,11 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
   const unsigned g = grid_for((long)B * heads * NQ * dh);
   return dispatch(
       dtype,
-      [&] {
-        DFM_LAUNCH(attn_bwd_chunk_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, a);
+      [&](auto tag16) {
+        using T16 = decltype(tag16);
+        DFM_LAUNCH(attn_bwd_chunk_kernel<T16>, dim3(nblk), dim3(256), lds, s, a);
         DFM_LAUNCH_CHECK();
-        DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+        DFM_LAUNCH(attn_dq_reduce_kernel<T16>, dim3(g), dim3(256), 0, s, a);
         DFM_LAUNCH_CHECK();
         return DFM_OK;
       },

@@ -6,7 +6,11 @@
 #include "../../include/dformer_hip.h"
 
 typedef uint16_t bf16_t;  // raw bfloat16 bits
+struct f16_t {            // raw IEEE binary16 bits (a distinct type so templates tell it from bf16)
+  uint16_t bits;
+};
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((ext_vector_type(4))) float float4_t;
 
@@ -29,6 +33,13 @@ template <> struct Num<bf16_t> {
   static DFM_INLINE float load(const bf16_t* p) { return bf2f(*p); }
   static DFM_INLINE float to_f(bf16_t v) { return bf2f(v); }
   static DFM_INLINE bf16_t from_f(float v) { return f2bf(v); }
+};
+DFM_INLINE float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+DFM_INLINE uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+template <> struct Num<f16_t> {
+  static DFM_INLINE float load(const f16_t* p) { return h2f(p->bits); }
+  static DFM_INLINE float to_f(f16_t v) { return h2f(v.bits); }
+  static DFM_INLINE f16_t from_f(float v) { return f16_t{f2h(v)}; }
 };
 template <typename T> DFM_INLINE float ldf(const T* p) { return Num<T>::load(p); }
 template <typename T> DFM_INLINE void stf(T* p, float v) { *p = Num<T>::from_f(v); }
@@ -90,6 +101,15 @@ template <> DFM_INLINE void ld8<bf16_t>(const bf16_t* p, float* v) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+template <> DFM_INLINE void ld8<f16_t>(const f16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = h2f((uint16_t)(w[i] & 0xffffu));
+    v[2 * i + 1] = h2f((uint16_t)(w[i] >> 16));
+  }
+}
 template <> DFM_INLINE void ld8<float>(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
@@ -111,6 +131,14 @@ DFM_INLINE void unpack8(const Raw8<bf16_t>& r, float* v) {
     v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+DFM_INLINE void unpack8(const Raw8<f16_t>& r, float* v) {
+  const uint32_t w[4] = {r.w[0].x, r.w[0].y, r.w[0].z, r.w[0].w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = h2f((uint16_t)(w[i] & 0xffffu));
+    v[2 * i + 1] = h2f((uint16_t)(w[i] >> 16));
+  }
+}
 DFM_INLINE void unpack8(const Raw8<float>& r, float* v) {
   v[0] = __uint_as_float(r.w[0].x); v[1] = __uint_as_float(r.w[0].y);
   v[2] = __uint_as_float(r.w[0].z); v[3] = __uint_as_float(r.w[0].w);
@@ -125,11 +153,64 @@ template <> DFM_INLINE void st8<bf16_t>(bf16_t* p, const float* v) {
   for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
+template <> DFM_INLINE void st8<f16_t>(f16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2h(v[2 * i]) | ((uint32_t)f2h(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
 template <> DFM_INLINE void st8<float>(float* p, const float* v) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// ---- 16-bit storage types on MFMA: fragments travel as 8 x 16-bit bit patterns (bf16x8_t is
+// only the container); mma16<T> issues v_mfma_f32_16x16x32_{bf16,f16} (fp32 accumulate).
+template <typename T> struct H16;
+template <> struct H16<bf16_t> { static constexpr unsigned ONE = 0x3f80u; };
+template <> struct H16<f16_t> { static constexpr unsigned ONE = 0x3c00u; };
+template <typename T> DFM_INLINE float4_t mma16(bf16x8_t a, bf16x8_t b, float4_t c);
+template <> DFM_INLINE float4_t mma16<bf16_t>(bf16x8_t a, bf16x8_t b, float4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <> DFM_INLINE float4_t mma16<f16_t>(bf16x8_t a, bf16x8_t b, float4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                0, 0);
+}
+template <typename T> DFM_INLINE uint16_t bits16(float v);
+template <> DFM_INLINE uint16_t bits16<bf16_t>(float v) { return f2bf(v); }
+template <> DFM_INLINE uint16_t bits16<f16_t>(float v) { return f2h(v); }
+// 8 floats -> 8 x 16-bit fragment of T (round to nearest even)
+template <typename T> DFM_INLINE bf16x8_t pack16x8(const float* v);
+template <> DFM_INLINE bf16x8_t pack16x8<bf16_t>(const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(w[0], w[1], w[2], w[3]));
+}
+template <> DFM_INLINE bf16x8_t pack16x8<f16_t>(const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2h(v[2 * i]) | ((uint32_t)f2h(v[2 * i + 1]) << 16);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(w[0], w[1], w[2], w[3]));
+}
+
+// Dispatch a 16-bit-or-float32 body on the dtype code: F(T{}) with T = float, bf16_t or f16_t.
+#define DFM_DTYPE_SWITCH(dtype, T, ...)                      \
+  [&]() -> int {                                             \
+    if ((dtype) == DFM_BF16) {                               \
+      using T = bf16_t;                                      \
+      return __VA_ARGS__;                                    \
+    } else if ((dtype) == DFM_F16) {                         \
+      using T = f16_t;                                       \
+      return __VA_ARGS__;                                    \
+    } else if ((dtype) == DFM_F32) {                         \
+      using T = float;                                       \
+      return __VA_ARGS__;                                    \
+    }                                                        \
+    dfm_set_error("%s: unsupported dtype %d", __func__, (int)(dtype)); \
+    return DFM_ERR_DTYPE;                                    \
+  }()
 
 // ---- second stage of the deterministic two-stage column reductions:
 // out[e] (+)= sum_{b < nblk} part[b * n + e], fixed summation order; 64 columns x 16 row-lanes

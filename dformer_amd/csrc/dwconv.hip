@@ -10,6 +10,8 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
     for (int u = 0; u < TWS + K - 1; ++u) {
       const uint4 q = xr[u * NG];
       if constexpr (sizeof(T) == 2) {
-        Raw8<bf16_t> r8;
+        Raw8<T> r8;
         r8.w[0] = q;
         unpack8(r8, win[u]);
       } else {
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
       const uint4 q = xs[((row + R) * IW + strip * TWS + t + R) * NG + g];
       float xi[CPT];
       if constexpr (sizeof(T) == 2) {
-        Raw8<bf16_t> r8;
+        Raw8<T> r8;
         r8.w[0] = q;
         unpack8(r8, xi);
       } else {
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(256) void dw_tile_wgrad_kernel(int B, int H, int W,
     for (int t = 0; t < TWS; ++t) {
       const uint4 q = ds[(row * TWT + strip * TWS + t) * NG + g];
       if constexpr (sizeof(T) == 2) {
-        Raw8<bf16_t> r8;
+        Raw8<T> r8;
         r8.w[0] = q;
         unpack8(r8, gv[t]);
       } else {
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void dw_tile_wgrad_kernel(int B, int H, int W,
         const uint4 q = xr[u * NG];
         float xv[CPT];
         if constexpr (sizeof(T) == 2) {
-          Raw8<bf16_t> r8;
+          Raw8<T> r8;
           r8.w[0] = q;
           unpack8(r8, xv);
         } else {
@@ -377,7 +379,10 @@ DFM_INLINE uint2 w3_ld(const T* p, bool ok) {
 
 template <typename T>
 DFM_INLINE void w3_unpack(uint2 q, float* v) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (std::is_same<T, f16_t>::value) {
+    v[0] = h2f((uint16_t)(q.x & 0xffffu)); v[1] = h2f((uint16_t)(q.x >> 16));
+    v[2] = h2f((uint16_t)(q.y & 0xffffu)); v[3] = h2f((uint16_t)(q.y >> 16));
+  } else if constexpr (sizeof(T) == 2) {
     v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
     v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
   } else {
@@ -664,8 +669,8 @@ template <typename T>
 DFM_INLINE void w3_store(T* p, const float* v) {
   if constexpr (sizeof(T) == 2) {
     uint2 q;
-    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    q.x = (uint32_t)bits16<T>(v[0]) | ((uint32_t)bits16<T>(v[1]) << 16);
+    q.y = (uint32_t)bits16<T>(v[2]) | ((uint32_t)bits16<T>(v[3]) << 16);
     *reinterpret_cast<uint2*>(p) = q;
   } else {
     *reinterpret_cast<uint2*>(p) = make_uint2(__float_as_uint(v[0]), __float_as_uint(v[1]));
@@ -922,6 +927,7 @@ extern "C" int dfm_dwconv_fwd(int dtype, int B, int H, int W, int C, int k, cons
                               dfm_stream_t stream) {
   DFM_CHECK_ARG(x && w && y && B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_fwd: bad argument");
   if (dtype == DFM_BF16) return dw_fwd<bf16_t, false>(B, H, W, C, k, x, ldx, w, bias, add_identity, y, ldy, 0, gout, ldg, (hipStream_t)stream);
+  else if (dtype == DFM_F16) return dw_fwd<f16_t, false>(B, H, W, C, k, x, ldx, w, bias, add_identity, y, ldy, 0, gout, ldg, (hipStream_t)stream);
   if (dtype == DFM_F32) return dw_fwd<float, false>(B, H, W, C, k, x, ldx, w, bias, add_identity, y, ldy, 0, gout, ldg, (hipStream_t)stream);
   dfm_set_error("dfm_dwconv_fwd: bad dtype");
   return DFM_ERR_DTYPE;
@@ -933,6 +939,9 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
   DFM_CHECK_ARG(dy && w && dx && B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd_data: bad argument");
   if (dtype == DFM_BF16)
     return dw_fwd<bf16_t, true>(B, H, W, C, k, dy, lddy, w, nullptr, add_identity, dx, lddx, accumulate, nullptr, 0,
+                                (hipStream_t)stream);
+  else if (dtype == DFM_F16)
+    return dw_fwd<f16_t, true>(B, H, W, C, k, dy, lddy, w, nullptr, add_identity, dx, lddx, accumulate, nullptr, 0,
                                 (hipStream_t)stream);
   if (dtype == DFM_F32)
     return dw_fwd<float, true>(B, H, W, C, k, dy, lddy, w, nullptr, add_identity, dx, lddx, accumulate, nullptr, 0,
@@ -967,6 +976,13 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
                                  : wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+  }
+  else if (dtype == DFM_F16) {
+    DFM_CHECK_ARG(dw_aligned<f16_t>(C, x, ldx) && dw_aligned<f16_t>(C, dy, lddy), "dwconv wgrad: alignment");
+    nsb = k == 7 ? (w7_enabled() ? w7_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                 : wgrad_dispatch<f16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
+          : w3_enabled() ? w3_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                         : wgrad_dispatch<f16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
     nsb = k == 7 ? (w7_enabled() ? w7_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)

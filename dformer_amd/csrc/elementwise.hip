@@ -253,11 +253,14 @@ int ew2d(int dtype, long rows, int C, const void* a, long lda, const void* b, lo
          const float* rs, long rps, float alpha, void* d, long ldd, int acc, hipStream_t s) {
   if (rows * C == 0) return DFM_OK;
   if (C % 8 == 0 && ew_al<float>(a, lda) && ew_al<float>(b, ldb) && ew_al<float>(d, ldd) &&
-      (dtype == DFM_BF16 || dtype == DFM_F32)) {
+      (dtype == DFM_BF16 || dtype == DFM_F16 || dtype == DFM_F32)) {
     const unsigned gv = ew_grid(rows * C / 8);
     if (dtype == DFM_BF16)
       DFM_LAUNCH((ew2d_vec_kernel<bf16_t, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
                          (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
+    else if (dtype == DFM_F16)
+      DFM_LAUNCH((ew2d_vec_kernel<f16_t, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const f16_t*)a, lda,
+                         (const f16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (f16_t*)d, ldd, acc);
     else
       DFM_LAUNCH((ew2d_vec_kernel<float, OP>), dim3(gv), dim3(256), 0, s, rows, C, (const float*)a, lda,
                          (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
@@ -268,6 +271,9 @@ int ew2d(int dtype, long rows, int C, const void* a, long lda, const void* b, lo
   if (dtype == DFM_BF16)
     DFM_LAUNCH((ew2d_kernel<bf16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)a, lda,
                        (const bf16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (bf16_t*)d, ldd, acc);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH((ew2d_kernel<f16_t, OP>), dim3(g), dim3(256), 0, s, rows, C, (const f16_t*)a, lda,
+                       (const f16_t*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (f16_t*)d, ldd, acc);
   else if (dtype == DFM_F32)
     DFM_LAUNCH((ew2d_kernel<float, OP>), dim3(g), dim3(256), 0, s, rows, C, (const float*)a, lda,
                        (const float*)b, ldb, cs, rs, rps > 0 ? rps : 1, alpha, (float*)d, ldd, acc);
@@ -388,20 +394,22 @@ __global__ void bn_bwd_apply_vec_kernel(long rows, int C, const T* __restrict__ 
 
 // ---- NMF multiplicative update
 // out16 / gnum16 (optional): bf16 copies of the result for the bf16-operand NMF GEMMs
+template <typename TC>
 __global__ void nmf_update_kernel(long n, const float* __restrict__ a, const float* __restrict__ num,
                                   const float* __restrict__ den, float eps, float* __restrict__ out,
-                                  bf16_t* __restrict__ out16) {
+                                  TC* __restrict__ out16) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = a[i] * num[i] / (den[i] + eps);
     out[i] = v;
-    if (out16) out16[i] = Num<bf16_t>::from_f(v);
+    if (out16) out16[i] = Num<TC>::from_f(v);
   }
 }
+template <typename TC>
 __global__ void nmf_update_bwd_kernel(long n, const float* __restrict__ g, const float* __restrict__ a,
                                       const float* __restrict__ num, const float* __restrict__ den,
                                       const float* __restrict__ out, float eps, float* __restrict__ ga, int acc,
                                       float* __restrict__ gnum, float* __restrict__ gden,
-                                      bf16_t* __restrict__ gnum16) {
+                                      TC* __restrict__ gnum16) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float r = 1.f / (den[i] + eps);
     const float gi = g[i];
@@ -409,7 +417,7 @@ __global__ void nmf_update_bwd_kernel(long n, const float* __restrict__ g, const
     ga[i] = acc ? ga[i] + v : v;
     const float gn = gi * a[i] * r;
     gnum[i] = gn;
-    if (gnum16) gnum16[i] = Num<bf16_t>::from_f(gn);
+    if (gnum16) gnum16[i] = Num<TC>::from_f(gn);
     gden[i] = -gi * out[i] * r;
   }
 }
@@ -444,9 +452,10 @@ __global__ void softmax_rows_bwd_kernel(long rows, int R, const float* __restric
 }
 
 // ---- AdamW (torch.optim.AdamW semantics, decoupled weight decay)
+template <typename TC>
 __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                              float* __restrict__ v, float lr, float b1, float b2, float eps, float wd, float bc1,
-                             float bc2_sqrt, float gscale, bf16_t* __restrict__ copy) {
+                             float bc2_sqrt, float gscale, TC* __restrict__ copy) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
     float pi = p[i] * (1.f - lr * wd);
@@ -456,14 +465,15 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
     v[i] = vi;
     pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
     p[i] = pi;
-    if (copy) copy[i] = f2bf(pi);
+    if (copy) copy[i] = Num<TC>::from_f(pi);
   }
 }
 // Same update with lr and step read from device memory (hyper = [lr, step]), so a captured HIP
 // graph replays every optimizer step without host-baked scalars.
+template <typename TC>
 __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                  float* __restrict__ v, const float* __restrict__ hyper, float b1, float b2,
-                                 float eps, float wd, float gscale, bf16_t* __restrict__ copy) {
+                                 float eps, float wd, float gscale, TC* __restrict__ copy) {
   const float lr = hyper[0], step = hyper[1];
   const float bc1 = 1.f - powf(b1, step), bc2_sqrt = sqrtf(1.f - powf(b2, step));
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -475,8 +485,15 @@ __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __r
     v[i] = vi;
     pi -= (lr / bc1) * mi / (sqrtf(vi) / bc2_sqrt + eps);
     p[i] = pi;
-    if (copy) copy[i] = f2bf(pi);
+    if (copy) copy[i] = Num<TC>::from_f(pi);
   }
+}
+// flag[0] = 1 if any element of g is inf / nan (the GradScaler's found_inf, torch/amp/grad_scaler.py)
+__global__ void nonfinite_kernel(long n, const float* __restrict__ g, int* __restrict__ flag) {
+  bool bad = false;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    bad |= !isfinite(g[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1;
 }
 }  // namespace
 
@@ -490,6 +507,7 @@ extern "C" int dfm_colsum(int dtype, long rows, int C, const void* x, long ldx, 
   if (rows == 0) return DFM_OK;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) return colred<bf16_t, 0>(rows, C, x, ldx, mul, ldmul, nullptr, rowscale, rps, out, accumulate, ws, s);
+  else if (dtype == DFM_F16) return colred<f16_t, 0>(rows, C, x, ldx, mul, ldmul, nullptr, rowscale, rps, out, accumulate, ws, s);
   if (dtype == DFM_F32) return colred<float, 0>(rows, C, x, ldx, mul, ldmul, nullptr, rowscale, rps, out, accumulate, ws, s);
   dfm_set_error("dfm_colsum: bad dtype");
   return DFM_ERR_DTYPE;
@@ -503,6 +521,9 @@ extern "C" int dfm_cast(int din, int dout, long n, const void* x, void* y, dfm_s
   else if (din == DFM_BF16 && dout == DFM_F32) DFM_LAUNCH((cast_kernel<bf16_t, float>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (float*)y);
   else if (din == DFM_F32 && dout == DFM_F32) DFM_LAUNCH((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, n, (const float*)x, (float*)y);
   else if (din == DFM_BF16 && dout == DFM_BF16) DFM_LAUNCH((cast_kernel<bf16_t, bf16_t>), dim3(g), dim3(256), 0, s, n, (const bf16_t*)x, (bf16_t*)y);
+  else if (din == DFM_F32 && dout == DFM_F16) DFM_LAUNCH((cast_kernel<float, f16_t>), dim3(g), dim3(256), 0, s, n, (const float*)x, (f16_t*)y);
+  else if (din == DFM_F16 && dout == DFM_F32) DFM_LAUNCH((cast_kernel<f16_t, float>), dim3(g), dim3(256), 0, s, n, (const f16_t*)x, (float*)y);
+  else if (din == DFM_F16 && dout == DFM_F16) DFM_LAUNCH((cast_kernel<f16_t, f16_t>), dim3(g), dim3(256), 0, s, n, (const f16_t*)x, (f16_t*)y);
   else {
     dfm_set_error("dfm_cast: bad dtype");
     return DFM_ERR_DTYPE;
@@ -538,6 +559,8 @@ extern "C" int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx
   DFM_CHECK_ARG(rows > 0, "dfm_bn_stats: no rows");
   if (dtype == DFM_BF16)
     return colred<bf16_t, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s, stats + 2 * C);
+  else if (dtype == DFM_F16)
+    return colred<f16_t, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s, stats + 2 * C);
   if (dtype == DFM_F32)
     return colred<float, 1>(rows, C, x, ldx, nullptr, 0, nullptr, nullptr, 1, stats, 0, ws, s, stats + 2 * C);
   dfm_set_error("dfm_bn_stats: bad dtype");
@@ -561,6 +584,9 @@ extern "C" int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx
     if (dtype == DFM_BF16)
       DFM_LAUNCH(bn_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean,
                          rstd, gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
+    else if (dtype == DFM_F16)
+      DFM_LAUNCH(bn_apply_vec_kernel<f16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const f16_t*)x, ldx, mean,
+                         rstd, gamma, beta, (const f16_t*)res, ldres, act, (f16_t*)y, ldy);
     else
       DFM_LAUNCH(bn_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean,
                          rstd, gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
@@ -571,6 +597,9 @@ extern "C" int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx
   if (dtype == DFM_BF16)
     DFM_LAUNCH(bn_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, mean, rstd,
                        gamma, beta, (const bf16_t*)res, ldres, act, (bf16_t*)y, ldy);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH(bn_apply_kernel<f16_t>, dim3(g), dim3(256), 0, s, rows, C, (const f16_t*)x, ldx, mean, rstd,
+                       gamma, beta, (const f16_t*)res, ldres, act, (f16_t*)y, ldy);
   else
     DFM_LAUNCH(bn_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx, mean, rstd,
                        gamma, beta, (const float*)res, ldres, act, (float*)y, ldy);
@@ -582,6 +611,7 @@ extern "C" int dfm_bn_bwd_stats(int dtype, long rows, int C, const void* x, long
                                 const float* mean, const float* rstd, float* stats2, void* ws, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) return colred<bf16_t, 2>(rows, C, x, ldx, dy, lddy, mean, rstd, 1, stats2, 0, ws, s);
+  else if (dtype == DFM_F16) return colred<f16_t, 2>(rows, C, x, ldx, dy, lddy, mean, rstd, 1, stats2, 0, ws, s);
   return colred<float, 2>(rows, C, x, ldx, dy, lddy, mean, rstd, 1, stats2, 0, ws, s);
 }
 
@@ -595,6 +625,9 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
     if (dtype == DFM_BF16)
       DFM_LAUNCH(bn_bwd_apply_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
                          (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
+    else if (dtype == DFM_F16)
+      DFM_LAUNCH(bn_bwd_apply_vec_kernel<f16_t>, dim3(gv), dim3(256), 0, s, rows, C, (const f16_t*)x, ldx,
+                         (const f16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (f16_t*)dx, lddx, accumulate);
     else
       DFM_LAUNCH(bn_bwd_apply_vec_kernel<float>, dim3(gv), dim3(256), 0, s, rows, C, (const float*)x, ldx,
                          (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
@@ -605,6 +638,9 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
   if (dtype == DFM_BF16)
     DFM_LAUNCH(bn_bwd_apply_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx,
                        (const bf16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (bf16_t*)dx, lddx, accumulate);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH(bn_bwd_apply_kernel<f16_t>, dim3(g), dim3(256), 0, s, rows, C, (const f16_t*)x, ldx,
+                       (const f16_t*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (f16_t*)dx, lddx, accumulate);
   else
     DFM_LAUNCH(bn_bwd_apply_kernel<float>, dim3(g), dim3(256), 0, s, rows, C, (const float*)x, ldx,
                        (const float*)dy, lddy, mean, rstd, gamma, stats2, inv_n, (float*)dx, lddx, accumulate);
@@ -613,18 +649,36 @@ extern "C" int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long
 }
 
 extern "C" int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
-                              void* out16, dfm_stream_t stream) {
-  DFM_LAUNCH(nmf_update_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out,
-             (bf16_t*)out16);
+                              void* out16, int copy_dtype, dfm_stream_t stream) {
+  DFM_CHECK_ARG(!out16 || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_nmf_update: bad copy dtype");
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(nmf_update_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps, out,
+               (f16_t*)out16);
+  else
+    DFM_LAUNCH(nmf_update_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, a, num, den, eps,
+               out, (bf16_t*)out16);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
 extern "C" int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                                   const float* out, float eps, float* ga, int acc, float* gnum, float* gden,
-                                  void* gnum16, dfm_stream_t stream) {
-  DFM_LAUNCH(nmf_update_bwd_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den, out,
-                     eps, ga, acc, gnum, gden, (bf16_t*)gnum16);
+                                  void* gnum16, int copy_dtype, dfm_stream_t stream) {
+  DFM_CHECK_ARG(!gnum16 || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_nmf_update_bwd: bad copy dtype");
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(nmf_update_bwd_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den,
+               out, eps, ga, acc, gnum, gden, (f16_t*)gnum16);
+  else
+    DFM_LAUNCH(nmf_update_bwd_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, a, num, den,
+               out, eps, ga, acc, gnum, gden, (bf16_t*)gnum16);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_grad_nonfinite(long n, const float* g, int* flag, dfm_stream_t stream) {
+  DFM_CHECK_ARG(g && flag && n >= 0, "dfm_grad_nonfinite: bad argument");
+  if (n == 0) return DFM_OK;
+  DFM_LAUNCH(nonfinite_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, g, flag);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
@@ -644,23 +698,35 @@ extern "C" int dfm_softmax_rows_bwd(long rows, int R, const float* y, const floa
 }
 
 extern "C" int dfm_adamw(long n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
-                         float eps, float wd, int step, float gscale, void* bf16_copy, dfm_stream_t stream) {
+                         float eps, float wd, int step, float gscale, void* copy, int copy_dtype,
+                         dfm_stream_t stream) {
   DFM_CHECK_ARG(p && g && m && v && step >= 1, "dfm_adamw: bad argument");
+  DFM_CHECK_ARG(!copy || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_adamw: bad copy dtype");
   if (n == 0) return DFM_OK;
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2 = 1.f - powf(beta2, (float)step);
-  DFM_LAUNCH(adamw_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1, beta2,
-                     eps, wd, bc1, sqrtf(bc2), gscale, (bf16_t*)bf16_copy);
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(adamw_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1,
+               beta2, eps, wd, bc1, sqrtf(bc2), gscale, (f16_t*)copy);
+  else
+    DFM_LAUNCH(adamw_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, lr, beta1,
+               beta2, eps, wd, bc1, sqrtf(bc2), gscale, (bf16_t*)copy);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
 extern "C" int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* v, const float* hyper, float beta1,
-                             float beta2, float eps, float wd, float gscale, void* bf16_copy, dfm_stream_t stream) {
+                             float beta2, float eps, float wd, float gscale, void* copy, int copy_dtype,
+                             dfm_stream_t stream) {
   DFM_CHECK_ARG(p && g && m && v && hyper, "dfm_adamw_dev: bad argument");
+  DFM_CHECK_ARG(!copy || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_adamw_dev: bad copy dtype");
   if (n == 0) return DFM_OK;
-  DFM_LAUNCH(adamw_dev_kernel, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper, beta1,
-             beta2, eps, wd, gscale, (bf16_t*)bf16_copy);
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(adamw_dev_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
+               beta1, beta2, eps, wd, gscale, (f16_t*)copy);
+  else
+    DFM_LAUNCH(adamw_dev_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
+               beta1, beta2, eps, wd, gscale, (bf16_t*)copy);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
@@ -730,6 +796,9 @@ extern "C" int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, l
   if (dtype == DFM_BF16)
     DFM_LAUNCH(residual_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, rows, C, (const bf16_t*)dout, lddout,
                        (const bf16_t*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (bf16_t*)df, lddf, (float*)ws);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH(residual_bwd_kernel<f16_t>, dim3(nblk), dim3(256), 0, s, rows, C, (const f16_t*)dout, lddout,
+                       (const f16_t*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (f16_t*)df, lddf, (float*)ws);
   else if (dtype == DFM_F32)
     DFM_LAUNCH(residual_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, rows, C, (const float*)dout, lddout,
                        (const float*)f, ldf_, colscale, rowscale, rps > 0 ? rps : 1, (float*)df, lddf, (float*)ws);

@@ -14,6 +14,7 @@
 // output side is a coalesced 16-byte access (these GEMMs are mostly HBM-bound: K <= 2048).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -59,6 +60,7 @@ template <> struct Mf<bf16_t> {
   static constexpr int PADK = 16;  // k-contiguous row pad: rows 160 B apart, conflict-free ds_read_b128 fragments
   static constexpr int PADR = 0;   // row-contiguous rows: no pad, 16-byte chunks XOR-swizzled (tr_swz)
 };
+template <> struct Mf<f16_t> : Mf<bf16_t> {};
 template <> struct Mf<float> {
   static constexpr int VEC = 4;
   static constexpr int KSTEP = 4;
@@ -85,7 +87,7 @@ DFM_INLINE uint4 load_vec(const T* __restrict__ p, long ld, int r, int k, int ro
     if (aligned && k + VEC <= K) return *reinterpret_cast<const uint4*>(src);
     T tmp[VEC];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) tmp[e] = (k + e < K) ? src[e] : T(0);
+    for (int e = 0; e < VEC; ++e) tmp[e] = (k + e < K) ? src[e] : Num<T>::from_f(0.f);
     return *reinterpret_cast<uint4*>(tmp);
   } else {
     if (k >= K) return out;
@@ -165,8 +167,11 @@ DFM_INLINE void stage_load_fast(uint4* regs, __amdgpu_buffer_rsrc_t rsrc, int so
 
 // After a fast load: write the virtual all-ones operand row `ones_r` (fused bias gradient) into
 // the staged registers. Applied right before the LDS store, when the loads have landed anyway.
+// bits of 1.0 in one 16-bit element (bf16 0x3f80, f16 0x3c00)
 template <typename T>
-DFM_INLINE unsigned one_bits() { return sizeof(T) == 2 ? 0x3f80u : 0x3f800000u; }
+constexpr unsigned one16() { return std::is_same<T, f16_t>::value ? 0x3c00u : 0x3f80u; }
+template <typename T>
+DFM_INLINE unsigned one_bits() { return sizeof(T) == 2 ? one16<T>() : 0x3f800000u; }
 
 template <typename T>
 DFM_INLINE uint4 set_one(uint4 u, int e) {  // element e (0 <= e < VEC, or no-op) := 1.0
@@ -174,8 +179,8 @@ DFM_INLINE uint4 set_one(uint4 u, int e) {  // element e (0 <= e < VEC, or no-op
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     if (sizeof(T) == 2) {
-      w[j] = (e == 2 * j) ? ((w[j] & 0xffff0000u) | 0x3f80u) : w[j];
-      w[j] = (e == 2 * j + 1) ? ((w[j] & 0x0000ffffu) | 0x3f800000u) : w[j];
+      w[j] = (e == 2 * j) ? ((w[j] & 0xffff0000u) | one16<T>()) : w[j];
+      w[j] = (e == 2 * j + 1) ? ((w[j] & 0x0000ffffu) | (one16<T>() << 16)) : w[j];
     } else {
       w[j] = (e == j) ? 0x3f800000u : w[j];
     }
@@ -187,7 +192,7 @@ template <typename T, int R, int BK, bool KC, int NT>
 DFM_INLINE void patch_ones(uint4* regs, int r0, int ones_r) {
   using G = TileGeom<T, R, BK, KC, NT>;
   constexpr int VEC = G::VEC;
-  const unsigned one = sizeof(T) == 2 ? 0x3f803f80u : 0x3f800000u;
+  const unsigned one = sizeof(T) == 2 ? (one16<T>() | (one16<T>() << 16)) : 0x3f800000u;
 #pragma unroll
   for (int i = 0; i < G::NVEC; ++i) {
     const int v = threadIdx.x + i * NT;
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mma16<T>(fa[i], fb[j], acc[i][j]);
       } else {
         float fa[TM], fb[TN];
 #pragma unroll
@@ -641,7 +646,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int ti
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mma16<T>(fa[i], fb[j], acc[i][j]);
       } else {
         float fa[TM], fb[TN];
 #pragma unroll
@@ -1144,7 +1149,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // fitted on the DFormer-B step's GEMM census (tools/gemm_sweep.py --replay, DFM_GEMM_GLDS=0 vs 1):
   // it wins on the forward except wide-N x short-K, and on dgrad from K = 640 up; with a row-
   // contiguous A (wgrad) the register-staged kernel stays ahead.
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
     const int kper = (d->K + a.splits - 1) / a.splits;
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 640);
     if (glds_env && route && !a.stream && a.ala && a.alb && kper >= 2 * GBK) {
@@ -1185,6 +1190,7 @@ extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const vo
   DFM_CHECK_ARG(d->colsum == nullptr || d->batch <= 1, "dfm_gemm: colsum needs batch 1");
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) return gemm_typed<bf16_t>(d, A, B, C, ws, s);
+  if (dtype == DFM_F16) return gemm_typed<f16_t>(d, A, B, C, ws, s);
   if (dtype == DFM_F32) return gemm_typed<float>(d, A, B, C, ws, s);
   dfm_set_error("dfm_gemm: unsupported dtype %d", dtype);
   return DFM_ERR_DTYPE;

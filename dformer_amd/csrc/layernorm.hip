@@ -433,6 +433,7 @@ extern "C" int dfm_layernorm_fwd(int dtype, long rows, int C, const void* x, lon
   DFM_CHECK_ARG(x && y && gamma && beta && mean && rstd, "dfm_layernorm_fwd: null argument");
   if (rows == 0) return DFM_OK;
   if (dtype == DFM_BF16) return ln_fwd<bf16_t>(rows, C, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, (hipStream_t)stream);
+  else if (dtype == DFM_F16) return ln_fwd<f16_t>(rows, C, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, (hipStream_t)stream);
   if (dtype == DFM_F32) return ln_fwd<float>(rows, C, x, ldx, gamma, beta, eps, y, ldy, mean, rstd, (hipStream_t)stream);
   dfm_set_error("dfm_layernorm_fwd: bad dtype");
   return DFM_ERR_DTYPE;
@@ -453,6 +454,9 @@ extern "C" int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, lon
   if (rows == 0) return DFM_OK;
   if (dtype == DFM_BF16)
     return ln_bwd<bf16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
+                          workspace, (hipStream_t)stream);
+  else if (dtype == DFM_F16)
+    return ln_bwd<f16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
                           workspace, (hipStream_t)stream);
   if (dtype == DFM_F32)
     return ln_bwd<float>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,

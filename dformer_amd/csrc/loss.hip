@@ -395,6 +395,9 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
   if (dtype == DFM_BF16)
     DFM_LAUNCH(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H, W,
                label, ignore, lse, (float*)workspace);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH(seg_loss_fwd_kernel<f16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const f16_t*)logits, H, W,
+               label, ignore, lse, (float*)workspace);
   else
     DFM_LAUNCH(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H, W,
                label, ignore, lse, (float*)workspace);
@@ -417,6 +420,9 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
     if (dtype == DFM_BF16)
       return launch_bwd_tiles<bf16_t>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
                                       (float*)workspace, dlogits, s);
+    else if (dtype == DFM_F16)
+      return launch_bwd_tiles<f16_t>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
+                                      (float*)workspace, dlogits, s);
     return launch_bwd_tiles<float>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
                                    (float*)workspace, dlogits, s);
   }
@@ -436,6 +442,9 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
   }
   if (dtype == DFM_BF16)
     DFM_LAUNCH(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
+                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
+  else if (dtype == DFM_F16)
+    DFM_LAUNCH(seg_loss_bwd_kernel<f16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const f16_t*)logits,
                        H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
   else
     DFM_LAUNCH(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,

@@ -226,7 +226,7 @@ class NMF2DFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, bases, steps, eps):
         x = x.contiguous()
-        lp = x.dtype == torch.bfloat16
+        lp = x.dtype in (torch.bfloat16, torch.float16)
         B0 = bases.contiguous()
         f32 = dict(device=x.device, dtype=torch.float32)
 
@@ -243,17 +243,17 @@ class NMF2DFn(torch.autograd.Function):
             num1 = xmm(Bt16)                                      # x^T B        [N,R]
             M = K.bmm(Bt, Bt, a_t=True)                           # B^T B        [R,R]
             den1 = K.bmm(Ct, M)                                   # C (B^T B)
-            Cn, Cn16 = K.nmf_update(Ct, num1, den1, eps, bf16_copy=True) if lp else (K.nmf_update(Ct, num1, den1, eps),) * 2
+            Cn, Cn16 = K.nmf_update(Ct, num1, den1, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Ct, num1, den1, eps),) * 2
             num2 = xmm(Cn16, a_t=True)                            # x C          [D,R]
             Q = K.bmm(Cn, Cn, a_t=True)                           # C^T C        [R,R]
             den2 = K.bmm(Bt, Q)                                   # B (C^T C)
-            Bn, Bn16 = K.nmf_update(Bt, num2, den2, eps, bf16_copy=True) if lp else (K.nmf_update(Bt, num2, den2, eps),) * 2
+            Bn, Bn16 = K.nmf_update(Bt, num2, den2, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Bt, num2, den2, eps),) * 2
             hist.append((Bt, Ct, num1, M, den1, Cn, Cn16, num2, Q, den2, Bn))
             Bt, Ct, Bt16 = Bn, Cn, Bn16
         num = xmm(Bt16)
         M = K.bmm(Bt, Bt, a_t=True)
         den = K.bmm(Ct, M)
-        Cf, Cf16 = K.nmf_update(Ct, num, den, eps, bf16_copy=True) if lp else (K.nmf_update(Ct, num, den, eps),) * 2
+        Cf, Cf16 = K.nmf_update(Ct, num, den, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Ct, num, den, eps),) * 2
         y = K.bmm(Cf16, Bt16, b_t=True)                           # (B C^T)^T    [N,D], x.dtype
         ctx.hist = hist
         ctx.final = (Bt, Bt16, Ct, num, M, den, Cf, Cf16)
@@ -266,7 +266,7 @@ class NMF2DFn(torch.autograd.Function):
         K.TAG = "decoder.bwd"
         x, B0, coef0 = ctx.saved_tensors
         eps = ctx.eps
-        lp = x.dtype == torch.bfloat16
+        lp = x.dtype in (torch.bfloat16, torch.float16)
         gy = gy.contiguous()
         Bb, N, D = x.shape
         R = B0.shape[2]
@@ -276,7 +276,7 @@ class NMF2DFn(torch.autograd.Function):
         gB = K.bmm(gy, Cf16, a_t=True, out=torch.empty(Bb, D, R, **f32))  # gy^T C  [D,R]
 
         def upd_bwd(g, a, nm, dn, out):  # -> ga, gnum, gden, gnum operand for the x products
-            r = K.nmf_update_bwd(g, a, nm, dn, out, eps=eps, bf16_copy=lp)
+            r = K.nmf_update_bwd(g, a, nm, dn, out, eps=eps, bf16_copy=x.dtype if lp else None)
             return r if lp else (*r, r[1])
 
         # Every contribution to gx is a rank-R product P Q^T (P [N,R], Q [D,R]); they are gathered

@@ -4,10 +4,10 @@ keys (Originofamonia/DFormer models/encoders/DFormer.py), computed by HIP kernel
 Layout: inside a stage the activations are NHWC rows in the compute dtype; the reference's
 Block.forward(x [B,H,W,C], x_e [B,H,W,C/2]) -> (x, x_e) surface is kept. nn.Linear / nn.Conv2d
 children are parameter containers only (their forward is never called on the hot path).
-The stems / stage downsampling (BN + conv3x3 s2, DFormer.py:194-228) run their 3x3 stride-2
-convolutions as channels-last PyTorch convolutions (SURVEY.md §8f item 2 lists them as the next
-native target); their BatchNorms run on MIOpen (the library's BNRowsFn with DFM_NATIVE_STEM_BN=1,
-pending shifted / two-pass BN statistics).
+The stems / stage downsampling (BN + conv3x3 s2, DFormer.py:194-228) run on ConvS2Fn: the BN
+statistics on the library's shifted-sum BN kernels, then one gather that folds the BN affine (and
+the stem's GELU) into the convolution operand and one MFMA GEMM (csrc/conv.hip), reading the raw
+input image and the previous stage's NHWC rows in place (no NCHW<->NHWC permute copies).
 """
 import os
 
@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from . import kernels as K
 from .decoders import _allreduce, bn_batch_stats
-from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, invalidate_weights
+from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, gslot, invalidate_weights
 
 _EMPTY = {}
 
@@ -218,6 +218,7 @@ class BNRowsFn(torch.autograd.Function):
         y = K.bn_apply(xr, mean, rstd, gamma, beta)
         ctx.save_for_backward(xr, mean, rstd, gamma)
         ctx.sync, ctx.count, ctx.shape = sync, count, (B, C, H, W)
+        ctx.training = bn.training
         return y.view(B, H, W, C).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -227,18 +228,121 @@ class BNRowsFn(torch.autograd.Function):
         B, C, H, W = ctx.shape
         dyr = dy.permute(0, 2, 3, 1).contiguous().view(-1, C)
         st2 = _allreduce(K.bn_bwd_stats(xr, dyr, mean, rstd), ctx.sync)
-        dx = K.bn_bwd_apply(xr, dyr, mean, rstd, gamma, st2, ctx.count)
+        if ctx.training:
+            dx = K.bn_bwd_apply(xr, dyr, mean, rstd, gamma, st2, ctx.count)
+        else:  # running statistics: BN is a fixed per-channel affine
+            dx = K.scale_mul(dyr, colscale=rstd * gamma)
         return dx.view(B, H, W, C).permute(0, 3, 1, 2), st2[1].clone(), st2[0].clone(), None, None
 
 
-# The stem / downsample BatchNorms run on BNRowsFn (the library's BN kernels, statistics as sums
-# shifted by the first row so the variance does not cancel); DFM_NATIVE_STEM_BN=0 selects torch's
-# BatchNorm (MIOpen) for A/B timing.
+class ConvS2Fn(torch.autograd.Function):
+    """nn.Conv2d(cin, cout, 3, stride 2, pad 1) [preceded by BatchNorm / SyncBatchNorm [+ GELU]]
+    (DFormer.py:194-228: stem conv -> BN -> GELU -> conv; stage i>0: BN -> conv) on the library's
+    kernels: the BN statistics over the input rows, then ONE gather that applies the BN affine and
+    GELU on the fly (csrc/conv.hip) and ONE MFMA GEMM with the conv bias in its epilogue. x is any
+    NCHW-logical tensor (raw image, the depth-channel view, or the previous stage's NHWC rows);
+    returns NHWC rows [B*Ho*Wo, cout] in the compute dtype. Backward: weight / bias gradients
+    from the saved gathered operand, input gradient by the transposed GEMM + deterministic
+    col2im with GELU' recomputed, then the BN backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, bn_w, bn_b, bn, sync, gelu, dt):
+        B, C, H, W = x.shape
+        cout = weight.shape[0]
+        kp = K.conv3s2_kp(C)
+        aff = None
+        count = None
+        xr = None
+        if bn is not None:
+            xr = x.permute(0, 2, 3, 1).reshape(B * H * W, C)  # the NHWC rows (a view for channels-last x)
+            if bn.training:
+                mean, rstd, count = bn_batch_stats(xr, bn, sync)
+            else:
+                mean = bn.running_mean
+                rstd = torch.rsqrt(bn.running_var + bn.eps)
+                count = xr.shape[0]
+            aff = (mean, rstd, bn_w.detach(), bn_b.detach())
+        cols = K.conv3s2_im2col(x, dt, bn=aff, gelu=gelu)
+        wp = K.conv3_weight_pack(weight.detach(), dt, kp)
+        y = K.linear(cols, wp, bias.detach())
+        ctx.shape, ctx.cin, ctx.sync, ctx.gelu, ctx.count = (B, H, W), C, sync, gelu, count
+        ctx.has_bn = bn is not None
+        ctx.training = bn is not None and bn.training
+        ctx.x_dtype = x.dtype
+        ctx.tag = K.TAG
+        ctx.save_for_backward(cols, wp, weight, bias, xr if xr is not None else x.new_empty(0),
+                              *(aff if aff is not None else ()))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        K.TAG = ctx.tag + ".bwd"
+        cols, wp, weight, bias, xr, *aff = ctx.saved_tensors
+        dy = dy.contiguous()
+        cin = ctx.cin
+        dwp, db = K.linear_wgrad(dy, cols, bias_grad=True, bias_out=gslot(bias))
+        dw = K.conv3_weight_unpack(dwp, cin, dw=gslot(weight))
+        dx = dgamma = dbeta = None
+        if not ctx.has_bn:
+            if ctx.needs_input_grad[0]:  # gradient w.r.t. the image (parity tests); not on the training path
+                dx = K.conv3s2_col2im_nchw(K.linear_dgrad(dy, wp), ctx.shape, cin, ctx.x_dtype)
+        elif ctx.needs_input_grad[0] or ctx.needs_input_grad[3] or ctx.needs_input_grad[4]:
+            dcols = K.linear_dgrad(dy, wp)
+            mean, rstd, gamma, beta = aff
+            dz = K.conv3s2_col2im(dcols, ctx.shape, cin, x=xr, bn=aff if ctx.gelu else None, gelu=ctx.gelu)
+            st2 = _allreduce(K.bn_bwd_stats(xr, dz, mean, rstd), ctx.sync)
+            dgamma, dbeta = st2[1].clone(), st2[0].clone()
+            if ctx.needs_input_grad[0]:
+                B, H, W = ctx.shape
+                if ctx.training:
+                    dx = K.bn_bwd_apply(xr, dz, mean, rstd, gamma, st2, ctx.count)
+                else:  # running statistics: BN is a fixed per-channel affine
+                    dx = K.scale_mul(dz, colscale=rstd * gamma)
+                dx = dx.view(B, H, W, cin).permute(0, 3, 1, 2)
+        return dx, dw, db, dgamma, dbeta, None, None, None, None
+
+
+# The stem / downsample layers run natively: 3x3 stride-2 convs as gather + MFMA GEMM with their
+# BatchNorms (+ GELU) folded into the gather (ConvS2Fn), the stem's last BN on BNRowsFn.
+# DFM_NATIVE_STEM=0 selects torch's convolutions (MIOpen) with the library's BN kernels for A/B
+# timing; DFM_NATIVE_STEM_BN=0 additionally puts the BatchNorms back on torch.
+_NATIVE_STEM = os.environ.get("DFM_NATIVE_STEM", "1") == "1"
 _NATIVE_STEM_BN = os.environ.get("DFM_NATIVE_STEM_BN", "1") == "1"
 
 
-def _run_downsample(seq, x):
-    """nn.Sequential of the reference's downsample layer (its BatchNorms on BNRowsFn when enabled)."""
+def _run_downsample_native(seq, x, dt):
+    """The reference's downsample nn.Sequential (stem: Conv, BN, GELU, Conv, BN; stage: BN, Conv)
+    on ConvS2Fn / BNRowsFn. Returns the NCHW-logical view of channels-last rows."""
+    mods = list(seq)
+    i, pend_bn, pend_gelu = 0, None, False
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            if i == len(mods) - 1:  # trailing BN of the stem: applied to the conv output rows
+                x = BNRowsFn.apply(x, m.weight, m.bias, m, isinstance(m, nn.SyncBatchNorm))
+            else:
+                pend_bn = m
+        elif isinstance(m, nn.GELU):
+            assert pend_bn is not None
+            pend_gelu = True
+        else:
+            assert isinstance(m, nn.Conv2d) and m.kernel_size == (3, 3) and m.stride == (2, 2) and m.padding == (1, 1)
+            B, _, H, W = x.shape
+            bn = pend_bn
+            y = ConvS2Fn.apply(x, m.weight, m.bias, bn.weight if bn is not None else None,
+                               bn.bias if bn is not None else None, bn, isinstance(bn, nn.SyncBatchNorm), pend_gelu,
+                               dt)
+            Ho, Wo = (H + 1) // 2, (W + 1) // 2
+            x = y.view(B, Ho, Wo, m.out_channels).permute(0, 3, 1, 2)
+            pend_bn, pend_gelu = None, False
+        i += 1
+    return x
+
+
+def _run_downsample(seq, x, dt=None):
+    """nn.Sequential of the reference's downsample layer (natively, or its BatchNorms on BNRowsFn)."""
+    if _NATIVE_STEM and x.is_cuda and dt is not None:
+        return _run_downsample_native(seq, x, dt)
     if not _NATIVE_STEM_BN:
         return seq(x)
     for m in seq:
@@ -316,6 +420,8 @@ class DFormer(nn.Module):
 
     def _downsample(self, i, x, e):
         dt = self.compute_dtype
+        if _NATIVE_STEM and x.is_cuda:
+            return _run_downsample(self.downsample_layers[i], x, dt), _run_downsample(self.downsample_layers_e[i], e, dt)
         with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
             x = _run_downsample(self.downsample_layers[i], x)
             e = _run_downsample(self.downsample_layers_e[i], e)
@@ -330,8 +436,9 @@ class DFormer(nn.Module):
             x_e = x_e.unsqueeze(2)
         x_e = x_e[:, 0:1]
         dt = self.compute_dtype
-        x = x.to(dt).contiguous(memory_format=torch.channels_last)
-        x_e = x_e.to(dt).contiguous(memory_format=torch.channels_last)
+        if not (_NATIVE_STEM and x.is_cuda):  # the native stem gathers straight from the input tensors
+            x = x.to(dt).contiguous(memory_format=torch.channels_last)
+            x_e = x_e.to(dt).contiguous(memory_format=torch.channels_last)
         self._draw_drop_path(x.shape[0], x.device)
         outs = []
         for i in range(4):

@@ -501,14 +501,127 @@ def bn_bwd_apply(x, dy, mean, rstd, gamma, stats2, count, dx=None, accumulate=Fa
     return dx
 
 
+# ------------------------------------------------------------------- dense 3x3 stride-2 conv
+def conv3s2_kp(cin):
+    """Packed K (columns of the gathered operand): 9*cin rounded up to a multiple of 8."""
+    return (9 * cin + 7) // 8 * 8
+
+
+def conv3s2_im2col(x, dtype, bn=None, gelu=False, out=None):
+    """Gather of nn.Conv2d(cin, cout, 3, 2, 1)'s operand from an NCHW-logical tensor x (any strides),
+    with an optional folded BatchNorm affine bn = (mean, rstd, gamma, beta) and exact GELU.
+    Returns cols [B*Ho*Wo, Kp] in `dtype` (columns (kh, kw, c))."""
+    B, C, H, W = x.shape
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    kp = conv3s2_kp(C)
+    if out is None:
+        out = torch.empty(B * Ho * Wo, kp, device=x.device, dtype=dtype)
+    mean, rstd, gamma, beta = bn if bn is not None else (None,) * 4
+    sb, sc, sh, sw = x.stride()
+    check(lib.dfm_conv3s2_im2col(dtype_code(x), dtype_code(out), B, H, W, C, sb, sc, sh, sw, ptr(x), ptr(mean),
+                                 ptr(rstd), ptr(gamma), ptr(beta), int(gelu), kp, ptr(out), stream()),
+          "dfm_conv3s2_im2col")
+    if ACCOUNT is not None:
+        _acct(0, B * C * H * W * _es(x) + out.numel() * _es(out))
+    return out
+
+
+def conv3s2_col2im(dcols, shape, cin, x=None, bn=None, gelu=False, dx=None, accumulate=False):
+    """Backward of conv3s2_im2col w.r.t. the BN output (rows [B*H*W, cin]); x: the rows the gather
+    read (needed with gelu, to recompute GELU' of the folded BN output)."""
+    B, H, W = shape
+    if dx is None:
+        dx = torch.empty(B * H * W, cin, device=dcols.device, dtype=dcols.dtype)
+        accumulate = False
+    mean, rstd, gamma, beta = bn if bn is not None else (None,) * 4
+    check(lib.dfm_conv3s2_col2im(dtype_code(dcols), B, H, W, cin, ptr(dcols), ld(dcols), ptr(x),
+                                 ld(x) if x is not None else 0, ptr(mean), ptr(rstd), ptr(gamma), ptr(beta),
+                                 int(gelu), ptr(dx), ld(dx), int(accumulate), stream()), "dfm_conv3s2_col2im")
+    if ACCOUNT is not None:
+        _acct(0, dcols.shape[0] * 9 * cin * _es(dcols) + dx.numel() * _es(dx) * (1 + bool(accumulate) + bool(gelu)))
+    return dx
+
+
+def conv3s2_col2im_nchw(dcols, shape, cin, dtype):
+    """Input gradient of a conv with no folded BN: contiguous NCHW [B, cin, H, W] in `dtype`."""
+    B, H, W = shape
+    dx = torch.empty(B, cin, H, W, device=dcols.device, dtype=dtype)
+    sb, sc, sh, sw = dx.stride()
+    check(lib.dfm_conv3s2_col2im_nchw(dtype_code(dcols), dtype_code(dx), B, H, W, cin, ptr(dcols), ld(dcols),
+                                      ptr(dx), sb, sc, sh, sw, stream()), "dfm_conv3s2_col2im_nchw")
+    if ACCOUNT is not None:
+        _acct(0, dcols.shape[0] * 9 * cin * _es(dcols) + dx.numel() * _es(dx))
+    return dx
+
+
+def conv3_weight_pack(w, dtype, kp):
+    cout, cin = w.shape[:2]
+    out = torch.empty(cout, kp, device=w.device, dtype=dtype)
+    check(lib.dfm_conv3_weight_pack(dtype_code(out), cout, cin, kp, ptr(w), ptr(out), stream()),
+          "dfm_conv3_weight_pack")
+    if ACCOUNT is not None:
+        _acct(0, w.numel() * 4 + out.numel() * _es(out))
+    return out
+
+
+def conv3_weight_unpack(dwp, cin, dw=None, accumulate=False):
+    cout, kp = dwp.shape
+    if dw is None:
+        dw = torch.empty(cout, cin, 3, 3, device=dwp.device, dtype=torch.float32)
+        accumulate = False
+    check(lib.dfm_conv3_weight_unpack(cout, cin, kp, ptr(dwp), ptr(dw), int(accumulate), stream()),
+          "dfm_conv3_weight_unpack")
+    if ACCOUNT is not None:
+        _acct(0, dwp.numel() * 4 + dw.numel() * 4)
+    return dw
+
+
+# ------------------------------------------------------------------ multi-scale + flip eval
+def resize_nchw(x, size, align_corners, flip=False, dtype=torch.float32):
+    """F.interpolate(x, size, 'bilinear', align_corners) [then torch.flip(dims=(3,))], x any strides."""
+    B, C, Hi, Wi = x.shape
+    Ho, Wo = size
+    y = torch.empty(B, C, Ho, Wo, device=x.device, dtype=dtype)
+    sb, sc, sh, sw = x.stride()
+    check(lib.dfm_resize_nchw(dtype_code(x), dtype_code(y), B, C, Hi, Wi, sb, sc, sh, sw, ptr(x), Ho, Wo,
+                              int(align_corners), int(flip), ptr(y), stream()), "dfm_resize_nchw")
+    return y
+
+
+def msf_accumulate(low_rows, B, h, w, ncls, scaled_hw, out_hw, flip, acc):
+    """acc [B*H*W, ncls] float32 += softmax(resize_ac(flip?(upsample(low -> scaled_hw))))."""
+    (Hs, Ws), (H, W) = scaled_hw, out_hw
+    check(lib.dfm_msf_accumulate(dtype_code(low_rows), B, h, w, ncls, ptr(low_rows), ld(low_rows), Hs, Ws, H, W,
+                                 int(flip), ptr(acc), stream()), "dfm_msf_accumulate")
+    return acc
+
+
+def seg_confusion(acc, label, ncls, ignore, hist):
+    """hist [ncls*ncls] int64 += bincount(label*ncls + argmax(acc rows)) over label != ignore."""
+    assert label.dtype == torch.int64 and hist.dtype == torch.int64 and acc.is_contiguous()
+    assert label.is_contiguous()
+    check(lib.dfm_seg_confusion(label.numel(), ncls, ptr(acc), ptr(label), ignore, ptr(hist), stream()),
+          "dfm_seg_confusion")
+    return hist
+
+
 # ---------------------------------------------------------------------------------------- NMF
+def _copy_dtype(flag):
+    """bf16_copy argument: False / None (no copy), True (bf16) or a 16-bit torch dtype."""
+    if not flag:
+        return None
+    return torch.bfloat16 if flag is True else flag
+
+
 def nmf_update(a, num, den, eps=1e-6, out=None, bf16_copy=False):
-    """out = a * num / (den + eps) (float32); with bf16_copy also returns a bf16 copy of out."""
+    """out = a * num / (den + eps) (float32); with bf16_copy (True = bf16, or a 16-bit dtype) also
+    returns a 16-bit copy of out."""
     if out is None:
         out = torch.empty_like(a)
-    o16 = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if bf16_copy else None
-    check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), ptr(o16), stream()),
-          "dfm_nmf_update")
+    cdt = _copy_dtype(bf16_copy)
+    o16 = torch.empty(a.shape, device=a.device, dtype=cdt) if cdt is not None else None
+    check(lib.dfm_nmf_update(a.numel(), ptr(a), ptr(num), ptr(den), eps, ptr(out), ptr(o16),
+                             dtype_code(o16) if o16 is not None else 0, stream()), "dfm_nmf_update")
     if ACCOUNT is not None:
         _acct(0, a.numel() * (16 + 2 * bool(bf16_copy)))
     return (out, o16) if bf16_copy else out
@@ -521,9 +634,11 @@ def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6, bf1
         accumulate = False
     gnum = torch.empty_like(a)
     gden = torch.empty_like(a)
-    g16 = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16) if bf16_copy else None
+    cdt = _copy_dtype(bf16_copy)
+    g16 = torch.empty(a.shape, device=a.device, dtype=cdt) if cdt is not None else None
     check(lib.dfm_nmf_update_bwd(a.numel(), ptr(g), ptr(a), ptr(num), ptr(den), ptr(out), eps, ptr(ga),
-                                 int(accumulate), ptr(gnum), ptr(gden), ptr(g16), stream()), "dfm_nmf_update_bwd")
+                                 int(accumulate), ptr(gnum), ptr(gden), ptr(g16),
+                                 dtype_code(g16) if g16 is not None else 0, stream()), "dfm_nmf_update_bwd")
     if ACCOUNT is not None:
         _acct(0, a.numel() * (4 * (8 + bool(accumulate)) + 2 * bool(bf16_copy)))
     return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
@@ -572,14 +687,21 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
 
 
 # -------------------------------------------------------------------------------------- AdamW
+def grad_nonfinite(g, flag):
+    """flag (int32 [1], zeroed by the caller) := 1 if any element of g is inf / nan."""
+    check(lib.dfm_grad_nonfinite(g.numel(), ptr(g), ptr(flag), stream()), "dfm_grad_nonfinite")
+    return flag
+
+
 def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None, hyper=None):
     """AdamW step; with `hyper` (device float32 [lr, step]) lr and step are read on the device
     (lr / step arguments ignored) so the launch can live in a replayed HIP graph."""
+    cdt = dtype_code(bf16_copy) if bf16_copy is not None else 0
     if hyper is not None:
         check(lib.dfm_adamw_dev(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(hyper), beta1, beta2, eps,
-                                weight_decay, grad_scale, ptr(bf16_copy), stream()), "dfm_adamw_dev")
+                                weight_decay, grad_scale, ptr(bf16_copy), cdt, stream()), "dfm_adamw_dev")
     else:
         check(lib.dfm_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), lr, beta1, beta2, eps, weight_decay, step,
-                            grad_scale, ptr(bf16_copy), stream()), "dfm_adamw")
+                            grad_scale, ptr(bf16_copy), cdt, stream()), "dfm_adamw")
     if ACCOUNT is not None:
         _acct(0, p.numel() * (28 + (2 if bf16_copy is not None else 0)))

@@ -7,6 +7,9 @@
   WarmUpPolyLR      utils/lr_policy.py:22-36
   GradBuckets       DDP-style bucketed gradient all-reduce (SUM, /world folded into AdamW), launched
                     from post-accumulate-grad hooks so RCCL overlaps the rest of the backward pass
+  LossScaler        torch.cuda.amp.GradScaler() of the fp16 path (utils/train.py:288-289, 327-337):
+                    scaled backward, inf/nan check over the flat gradients on the device, skipped
+                    step + backoff on overflow, growth every 2000 clean steps
 """
 import torch
 import torch.distributed as dist
@@ -157,6 +160,37 @@ class GradBuckets:
         self.pending = [len(b[1]) for b in self.buckets]
 
 
+class LossScaler:
+    """torch.cuda.amp.GradScaler defaults (init 2**16, growth 2.0, backoff 0.5, interval 2000) for
+    the fp16 compute dtype: the loss gradient is seeded with `scale`, the optimizer checks every
+    flat gradient buffer for inf / nan (one kernel per group, one host read per step), skips the
+    update on overflow and unscales by 1/scale otherwise."""
+
+    def __init__(self, device, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000):
+        self.scale = float(init_scale)
+        self.growth_factor, self.backoff_factor, self.growth_interval = growth_factor, backoff_factor, growth_interval
+        self.growth_tracker = 0
+        self.found_inf = torch.zeros(1, device=device, dtype=torch.int32)
+        self.skipped = 0
+
+    def check(self, grads):
+        self.found_inf.zero_()
+        for g in grads:
+            K.grad_nonfinite(g, self.found_inf)
+        return bool(self.found_inf.item())
+
+    def update(self, found_inf):
+        if found_inf:
+            self.scale *= self.backoff_factor
+            self.growth_tracker = 0
+            self.skipped += 1
+        else:
+            self.growth_tracker += 1
+            if self.growth_tracker == self.growth_interval:
+                self.scale *= self.growth_factor
+                self.growth_tracker = 0
+
+
 class FusedAdamW:
     """torch.optim.AdamW semantics over the two group_weight groups (decay wd, no-decay 0)."""
 
@@ -182,11 +216,21 @@ class FusedAdamW:
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
+        # fp16 compute (BASELINE config 5, the reference's --amp): dynamic loss scaling
+        self.scaler = LossScaler(dev) if compute_dtype == torch.float16 else None
 
     def step(self, lr=None):
         self.buckets.finish()
         for p in self.ungrouped:
             p.grad = None
+        gscale = 1.0 / self.world
+        if self.scaler is not None:
+            used = self.scaler.scale  # the scale this step's backward was seeded with
+            inf = self.scaler.check([g.grad for g in self.groups])
+            self.scaler.update(inf)
+            if inf:  # GradScaler.step: the optimizer step is skipped (its step count too)
+                return
+            gscale /= used
         self.step_count += 1
         lr = self.lr if lr is None else lr
         if not self.external_hyper:
@@ -194,7 +238,7 @@ class FusedAdamW:
             self.hyper[1].fill_(float(self.step_count))
         for g in self.groups:
             K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, self.step_count,
-                    1.0 / self.world, g.shadow, hyper=self.hyper)
+                    gscale, g.shadow, hyper=self.hyper)
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
@@ -315,6 +359,9 @@ def train_step(model, opt, rgb, depth, label, lr=None):
     RCCL all-reduce overlapping it), loss all-reduce, AdamW step. Returns the (device) mean loss."""
     loss, _ = model(rgb, depth, label)
     reduce_loss = all_reduce_mean(loss.detach(), opt.world)
-    loss.backward()
+    if opt.scaler is not None:  # scaler.scale(loss).backward()
+        loss.backward(torch.full_like(loss, opt.scaler.scale))
+    else:
+        loss.backward()
     opt.step(lr)
     return reduce_loss

@@ -8,7 +8,8 @@
  *     (a hipStream_t passed as void*; NULL = default stream);
  *   - return 0 on success, negative on bad arguments / unsupported dtype / launch failure;
  *     dfm_last_error() returns a thread-local message for the last failure;
- *   - dtype selects the storage type of activations: DFM_F32 or DFM_BF16. Statistics,
+ *   - dtype selects the storage type of activations: DFM_F32, DFM_BF16 or DFM_F16 (IEEE half,
+ *     the reference's torch.autocast(float16) path, utils/train.py:289). Statistics,
  *     accumulators, LayerNorm / BatchNorm affine params, biases, depthwise weights and
  *     gradients of parameters are always float32.
  *   - layouts are NHWC ("channels-last"): pixel p of image b at row (b*H + h)*W + w,
@@ -33,6 +34,7 @@ extern "C" {
 
 #define DFM_F32 0
 #define DFM_BF16 1
+#define DFM_F16 2
 
 typedef void* dfm_stream_t;
 
@@ -232,17 +234,63 @@ int dfm_bn_bwd_apply(int dtype, long rows, int C, const void* x, long ldx, const
 int dfm_relu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* y, long ldy, void* dx,
                  long lddx, dfm_stream_t stream);
 
+/* ---------------------------------------------------------------- dense 3x3 stride-2 conv
+ * Stems / stage downsampling (DFormer.py:194-228, 295-303: nn.Conv2d(cin, cout, 3, 2, 1) after
+ * BN/SyncBN, or after BN + GELU inside the stem) as gather + dfm_gemm over NHWC rows.
+ * im2col: cols[m][(kh*3+kw)*Cin + c] = act(bn(x[b][c][2*oh-1+kh][2*ow-1+kw])), zero outside the
+ *   image and for columns >= 9*Cin up to Kp (Kp % 8 == 0); m = (b*Ho + oh)*Wo + ow,
+ *   Ho = (H+1)/2, Wo = (W+1)/2. x is NCHW-logical with element strides (sb, sc, sh, sw), so the
+ *   raw float32 image, a channel view and NHWC rows (sc = 1) are all read in place.
+ *   bn (mean/rstd/gamma/beta, nullable together): (v - mean)*rstd*gamma + beta; gelu: exact GELU.
+ * col2im (backward data): dx[p][c] (+)= act'(.) * sum over the taps of p of dcols (fixed order,
+ *   deterministic); x / bn / gelu recompute the GELU derivative at the folded BN output. dx is
+ *   the gradient w.r.t. the BN output (the BN backward runs on dfm_bn_bwd_*). Cin % 8 == 0.
+ * weight_pack: w float32 [Cout][Cin][3][3] -> wp [Cout][Kp] in (kh, kw, c) column order;
+ * weight_unpack: the weight gradient of the packed layout back to [Cout][Cin][3][3]. */
+int dfm_conv3s2_im2col(int dtype_in, int dtype_out, int B, int H, int W, int Cin, long sb, long sc, long sh,
+                       long sw, const void* x, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, int gelu, int Kp, void* cols, dfm_stream_t stream);
+int dfm_conv3s2_col2im(int dtype, int B, int H, int W, int Cin, const void* dcols, long ldc, const void* x,
+                       long ldx, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                       int gelu, void* dx, long lddx, int accumulate, dfm_stream_t stream);
+/* col2im_nchw: the same gather without BN / GELU for any Cin, into dx (dtype_out) with element
+ * strides (sb, sc, sh, sw) — the input gradient of the stem's first conv. */
+int dfm_conv3s2_col2im_nchw(int dtype, int dtype_out, int B, int H, int W, int Cin, const void* dcols, long ldc,
+                            void* dx, long sb, long sc, long sh, long sw, dfm_stream_t stream);
+int dfm_conv3_weight_pack(int dtype_out, int Cout, int Cin, int Kp, const float* w, void* wp,
+                          dfm_stream_t stream);
+int dfm_conv3_weight_unpack(int Cout, int Cin, int Kp, const float* dwp, float* dw, int accumulate,
+                            dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- multi-scale + flip evaluation
+ * utils/val_mm.py:325-472 evaluate_msf, utils/metrics_new.py:16-20 Metrics.update.
+ * resize_nchw: y [B][C][Ho][Wo] (contiguous) = F.interpolate(x, (Ho, Wo), 'bilinear',
+ *   align_corners), then torch.flip(dims=(3,)) when flip; x NCHW-logical with element strides.
+ * msf_accumulate: acc [B*H*W][ncls] float32 (NHWC rows) += softmax over classes of the decoder's
+ *   low-res logits low [B*h*w][ldl] upsampled to (Hs, Ws) with align_corners=False (the model's
+ *   output at scale s, builder.py:203), flipped back along W when flip, then resized to (H, W)
+ *   with align_corners=True. ncls <= 64.
+ * seg_confusion: hist [ncls*ncls] uint64 += bincount(label * ncls + argmax(acc)) over pixels
+ *   whose label != ignore (and within [0, ncls)). */
+int dfm_resize_nchw(int dtype_in, int dtype_out, int B, int C, int Hi, int Wi, long sb, long sc, long sh, long sw,
+                    const void* x, int Ho, int Wo, int align_corners, int flip, void* y, dfm_stream_t stream);
+int dfm_msf_accumulate(int dtype, int B, int h, int w, int ncls, const void* low, long ldl, int Hs, int Ws, int H,
+                       int W, int flip, float* acc, dfm_stream_t stream);
+int dfm_seg_confusion(long npix, int ncls, const float* acc, const long long* label, int ignore,
+                      unsigned long long* hist, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- NMF2D multiplicative update
  * ham_head.py:120-145:  out = a * num / (den + eps)  (float32), and its backward:
  *   ga (+= when accumulate_ga) = g * num / (den+eps);  gnum = g * a / (den+eps);
  *   gden = -g * out / (den+eps).
- * out16 / gnum16 (nullable): bf16 copies of out / gnum, the operands of the bf16 NMF GEMMs (the
- * reference's autocast runs ham_head.py's bmm in bf16). */
+ * out16 / gnum16 (nullable): 16-bit copies (copy_dtype DFM_BF16 or DFM_F16) of out / gnum, the
+ * operands of the 16-bit NMF GEMMs (the reference's autocast runs ham_head.py's bmm in the
+ * autocast dtype). */
 int dfm_nmf_update(long n, const float* a, const float* num, const float* den, float eps, float* out,
-                   void* out16, dfm_stream_t stream);
+                   void* out16, int copy_dtype, dfm_stream_t stream);
 int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                        const float* out, float eps, float* ga, int accumulate_ga, float* gnum, float* gden,
-                       void* gnum16, dfm_stream_t stream);
+                       void* gnum16, int copy_dtype, dfm_stream_t stream);
 /* row softmax over R (NMF coef init, ham_head.py:48-49) and its backward */
 int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream);
 int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int accumulate,
@@ -266,15 +314,19 @@ int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logit
 
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW step (train.py:210-216) over a flat float32 parameter buffer; optional
- * bf16 shadow copy for the next step's GEMM operands. grad_scale multiplies g (1/world). */
+ * 16-bit shadow copy (copy_dtype DFM_BF16 / DFM_F16) for the next step's GEMM operands.
+ * grad_scale multiplies g (1/world, and 1/loss-scale on the fp16 path). */
 int dfm_adamw(long n, float* p, const float* g, float* m, float* v, float lr, float beta1, float beta2,
-              float eps, float weight_decay, int step, float grad_scale, void* bf16_copy,
+              float eps, float weight_decay, int step, float grad_scale, void* copy, int copy_dtype,
               dfm_stream_t stream);
 /* The same step with lr and step (as float) read from device memory hyper[2] = {lr, step}: what a
  * captured HIP graph of the whole training step calls, the host refreshing hyper before a replay. */
 int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* v, const float* hyper, float beta1,
-                  float beta2, float eps, float weight_decay, float grad_scale, void* bf16_copy,
+                  float beta2, float eps, float weight_decay, float grad_scale, void* copy, int copy_dtype,
                   dfm_stream_t stream);
+/* fp16 loss scaling (utils/train.py:289, 323-345 torch.cuda.amp.GradScaler): flag[0] = 1 when any
+ * gradient element is inf / nan (flag is not cleared: the caller zeroes it per step). */
+int dfm_grad_nonfinite(long n, const float* g, int* flag, dfm_stream_t stream);
 
 #ifdef __cplusplus
 }

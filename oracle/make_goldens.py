@@ -266,7 +266,8 @@ def _fp_rel_err(fa, fb, atol=1e-9):
                abs(fa[2] - fb[2]) / max(fb[2], atol), abs(fa[3:] - fb[3:]).max() / scale)
 
 
-def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512):
+def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, dtype=torch.bfloat16,
+                    prefix="bf16env_"):
     """The reference's OWN bf16 error on an e2e golden: the same model, weights and inputs run in
     float32 under torch.autocast(bfloat16) on CPU (what train.py's --amp does with bf16), compared
     with the fp64 golden. The HIP bf16 path is gated against this envelope (reference
@@ -282,7 +283,7 @@ def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512):
     if bases is not None:
         model.decode_head.hamburger.ham._build_bases = \
             lambda B_, S, D, R, cuda=False: torch.from_numpy(bases.astype(np.float32))
-    with torch.autocast("cpu", dtype=torch.bfloat16):
+    with torch.autocast("cpu", dtype=dtype):
         feats = model.encoder_backbone(rgb, dep)[0]
         low = model.decode_head.forward(feats)
         out = F.interpolate(low, size=rgb.shape[-2:], mode="bilinear", align_corners=False)
@@ -296,9 +297,9 @@ def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512):
         if p.grad is not None and "gfp/" + n in g:
             env["env/gfp/" + n] = _fp_rel_err(gen.fingerprint(p.grad.double().numpy(), 16), g["gfp/" + n], atol=1e-4)
     gv = np.array([v for k, v in env.items() if k.startswith("env/gfp/")])
-    print(f"  bf16 envelope {name}: low {env['env/low']:.3e} loss {env['env/loss']:.3e} grgb {env['env/grgb']:.3e} "
+    print(f"  {prefix} envelope {name}: low {env['env/low']:.3e} loss {env['env/loss']:.3e} grgb {env['env/grgb']:.3e} "
           f"param-grad median {np.median(gv):.3e} p90 {np.quantile(gv, 0.9):.3e} max {gv.max():.3e}")
-    save("bf16env_" + name, **{k: np.array(v) for k, v in env.items()})
+    save(prefix + name, **{k: np.array(v) for k, v in env.items()})
 
 
 def golden_groups():
@@ -334,6 +335,9 @@ def main():
         ("block_base_s3_last", "base", 3, 2, 8, 10, True),
         ("block_large_s1", "large", 1, 1, 9, 11, False),
         ("block_large_s2", "large", 2, 1, 8, 9, False),
+        # DFormer-Large at 530x730 (BASELINE config 5): stage 2 is 34x46, stage 3 17x23
+        ("block_large_s2_34x46", "large", 2, 1, 34, 46, False),
+        ("block_large_s3_17x23", "large", 3, 1, 17, 23, False),
     ]
     for n, mdl, st, B, H, W, last in blocks:
         if want(n):
@@ -363,6 +367,9 @@ def main():
         golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
         golden_bf16_env("e2e_base_small", "DFormer-Base", 2, 64, 80)
         golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37)
+    if want("f16env"):  # the reference's own torch.autocast(float16) error (train.py --amp, config 5)
+        golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37,
+                        dtype=torch.float16, prefix="f16env_")
 
 
 if __name__ == "__main__":
