@@ -56,6 +56,7 @@ _SIGS = {
     "dfm_gelu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, c_int, P]),
     "dfm_scale_mul": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, c_float, P, c_long, c_int,
                               P]),
+    "dfm_dual_mul": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_long, P, c_long, P]),
     "dfm_adaptive_pool7_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P]),
     "dfm_adaptive_pool7_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_int, P]),
     "dfm_bilinear_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, c_int, P]),

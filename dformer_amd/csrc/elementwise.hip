@@ -488,6 +488,31 @@ __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __r
     if (copy) copy[i] = Num<TC>::from_f(pi);
   }
 }
+// o1 = src * m1, o2 = src * m2 (the two products of one gradient against the two factors of
+// an elementwise product, DFormer.py:134-135: d(q*a) -> dq = d*a, da = d*q): one read of src.
+template <typename T>
+__global__ void dual_mul_vec_kernel(long rows, int C, const T* __restrict__ src, long lds, const T* __restrict__ m1,
+                                    long ld1, const T* __restrict__ m2, long ld2, T* __restrict__ o1, long ldo1,
+                                    T* __restrict__ o2, long ldo2) {
+  const int cv = C / 8;
+  const long n = rows * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cv;
+    const int c = (int)(i - r * cv) * 8;
+    float sv[8], a[8], b[8];
+    ld8<T>(src + r * lds + c, sv);
+    ld8<T>(m1 + r * ld1 + c, a);
+    ld8<T>(m2 + r * ld2 + c, b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] *= sv[e];
+      b[e] *= sv[e];
+    }
+    st8<T>(o1 + r * ldo1 + c, a);
+    st8<T>(o2 + r * ldo2 + c, b);
+  }
+}
+
 // flag[0] = 1 if any element of g is inf / nan (the GradScaler's found_inf, torch/amp/grad_scaler.py)
 __global__ void nonfinite_kernel(long n, const float* __restrict__ g, int* __restrict__ flag) {
   bool bad = false;
@@ -550,6 +575,27 @@ extern "C" int dfm_scale_mul(int dtype, long rows, int C, const void* src, long 
   DFM_CHECK_ARG(src && dst, "dfm_scale_mul: null argument");
   return ew2d<0>(dtype, rows, C, src, ldsrc, mul, ldmul, colscale, rowscale, rps, alpha, dst, lddst, accumulate,
                  (hipStream_t)stream);
+}
+
+extern "C" int dfm_dual_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* m1, long ld1,
+                            const void* m2, long ld2, void* o1, long ldo1, void* o2, long ldo2, dfm_stream_t stream) {
+  DFM_CHECK_ARG(src && m1 && m2 && o1 && o2, "dfm_dual_mul: null argument");
+  if (rows * C == 0) return DFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = C % 8 == 0 && ew_al<float>(src, ldsrc) && ew_al<float>(m1, ld1) && ew_al<float>(m2, ld2) &&
+                   ew_al<float>(o1, ldo1) && ew_al<float>(o2, ldo2);
+  if (!vec) {  // two scale_mul passes
+    int rc = ew2d<0>(dtype, rows, C, src, ldsrc, m1, ld1, nullptr, nullptr, 1, 1.f, o1, ldo1, 0, s);
+    if (rc) return rc;
+    return ew2d<0>(dtype, rows, C, src, ldsrc, m2, ld2, nullptr, nullptr, 1, 1.f, o2, ldo2, 0, s);
+  }
+  const unsigned g = ew_grid(rows * C / 8);
+  return DFM_DTYPE_SWITCH(dtype, T, [&] {
+    DFM_LAUNCH(dual_mul_vec_kernel<T>, dim3(g), dim3(256), 0, s, rows, C, (const T*)src, ldsrc, (const T*)m1, ld1,
+               (const T*)m2, ld2, (T*)o1, ldo1, (T*)o2, ldo2);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }());
 }
 
 extern "C" int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx, float* stats, void* ws,

@@ -50,6 +50,7 @@ struct GemmArgs {
   int tiles_n;     // output column tiles (grid.x enumerates tiles_m * tiles_n)
   int tiles_m;     // output row tiles (glds kernel)
   int n_fast;      // glds kernel: consecutive (XCD-local) blocks walk column tiles of one row tile
+  int xcd_map;     // gemm_kernel: XCD-aware block renumbering (DFM_GEMM_XCD=0 disables)
 };
 
 
@@ -449,8 +450,19 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
   const int tiles_m = (a.M + BM - 1) / BM;  // grid.x enumerates M tiles fastest
-  const int bm = (blockIdx.x % tiles_m) * BM, bn = (blockIdx.x / tiles_m) * BN;
-  const int b = blockIdx.z / a.splits, split = blockIdx.z % a.splits;
+  int tile = blockIdx.x, zs = blockIdx.z;
+  if (a.xcd_map) {
+    // XCD-aware renumbering (bijective for any grid size; blocks id and id + 8 share an XCD): the
+    // tiles of one split-K slice — which read the same K range of both operands — run on one XCD,
+    // so the operand slices they share are re-read from that XCD's L2 instead of by all eight.
+    const int nblk = gridDim.x * gridDim.z, id = blockIdx.z * gridDim.x + blockIdx.x;
+    const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+    tile = lid % gridDim.x;
+    zs = lid / gridDim.x;
+  }
+  const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * BN;
+  const int b = zs / a.splits, split = zs % a.splits;
 
   const int kper = ((a.K + a.splits - 1) / a.splits + BK - 1) / BK * BK;
   const int kbeg = split * kper;
@@ -1116,6 +1128,11 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
   a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
+  static const int xcd_env = [] {
+    const char* e = getenv("DFM_GEMM_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd_map = xcd_env;
   int BM, BN;
   pick_tile(d, BM, BN);
   a.splits = choose_splits(d, sizeof(T));

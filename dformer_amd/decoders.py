@@ -45,6 +45,12 @@ def merge_bn_stats(parts, counts):
     return torch.stack([torch.zeros_like(mean), m2, mean]).float()
 
 
+# Per-rank row counts of a SyncBN batch, keyed by (local rows, world): data-parallel ranks see the
+# same batch shape every step, so the counts are exchanged (and read on the host) once per shape.
+_GLOBAL_ROWS = {}
+_GLOBAL_TOTAL = {}
+
+
 def bn_batch_stats(x, bn, sync):
     """Train-mode BatchNorm / SyncBatchNorm statistics of NHWC rows x: (mean, rstd, count), with the
     running statistics updated like torch (momentum, unbiased variance). With SyncBN over a
@@ -56,12 +62,17 @@ def bn_batch_stats(x, bn, sync):
     if world > 1:
         gathered = [torch.empty_like(st) for _ in range(world)]
         dist.all_gather(gathered, st)
-        cnt = torch.tensor([float(rows)], device=x.device)
-        counts = [torch.empty_like(cnt) for _ in range(world)]
-        dist.all_gather(counts, cnt)
-        counts = torch.cat(counts)
+        counts = _GLOBAL_ROWS.get((rows, world))
+        if counts is None:  # first batch of this shape: exchange the per-rank row counts once
+            cnt = torch.tensor([float(rows)], device=x.device)
+            parts = [torch.empty_like(cnt) for _ in range(world)]
+            dist.all_gather(parts, cnt)
+            counts = _GLOBAL_ROWS[(rows, world)] = torch.cat(parts)
         st = merge_bn_stats(torch.stack(gathered), counts)
-        count = int(counts.sum().item())
+        total = _GLOBAL_TOTAL.get((rows, world))
+        if total is None:  # one host read per batch shape, not one per BN layer per step
+            total = _GLOBAL_TOTAL[(rows, world)] = int(counts.sum().item())
+        count = total
     mean, rstd = K.bn_finalize(st, count, bn.eps, bn.momentum if bn.momentum is not None else 0.1, bn.running_mean,
                                bn.running_var)
     bn.num_batches_tracked.add_(1)

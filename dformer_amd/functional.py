@@ -92,6 +92,26 @@ def gslot2(p):
     return None if t is None else t.view(t.shape[0], -1)
 
 
+def gslot_rows(*ps):
+    """One [sum of rows, cols] view over the flat-gradient slots of parameters whose slots are
+    adjacent in that order (e.g. proj.weight, proj_e.weight), or None."""
+    ss = [_slot(p) for p in ps]
+    if any(s is None for s in ss) or any(s[0] is not ss[0][0] for s in ss):
+        return None
+    cols = ss[0][2][1:] if len(ss[0][2]) > 1 else ()
+    off = ss[0][1]
+    rows = 0
+    for s in ss:
+        if s[1] != off or tuple(s[2][1:]) != tuple(cols):
+            return None
+        n = 1
+        for d in s[2]:
+            n *= d
+        off += n
+        rows += s[2][0]
+    return ss[0][0][ss[0][1]:off].view(rows, *cols) if cols else ss[0][0][ss[0][1]:off]
+
+
 def _cat1(*vs):
     """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
     key = tuple(id(v) for v in vs) + ("bias",)
@@ -287,26 +307,29 @@ class AttentionFn(torch.autograd.Function):
         fw = f.shape[1]
         grads = {}
         dx1 = dx1.contiguous()
-        # projections
-        dp1, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps)
-        grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, out=gslot2(wp), bias_grad=True, bias_out=gslot(bp))
-        df = K.linear_dgrad(dp1, wcast(dt, wp))
+        # projections: proj and proj_e read the same f, so their backward runs as ONE weight-gradient
+        # GEMM and ONE input-gradient GEMM over [dp1 | dp1e] (K = C + C/2) against [Wp; Wpe]
         if drop_depth:
+            dp1, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps)
+            grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, out=gslot2(wp), bias_grad=True, bias_out=gslot(bp))
+            df = K.linear_dgrad(dp1, wcast(dt, wp))
             dxe_res = dxe1.contiguous() if dxe1 is not None else None
         else:
             dxe1 = dxe1.contiguous()
-            dp1e, grads["ls1e"] = K.residual_bwd(dxe1, p1e, ls1e, rowscale_e, rps)
-            grads["wpe"], grads["bpe"] = K.linear_wgrad(dp1e, f, out=gslot2(wpe), bias_grad=True,
-                                                        bias_out=gslot(bpe))
-            K.linear_dgrad(dp1e, wcast(dt, wpe), out=df, accumulate=True)
+            dpc = torch.empty(P, C + Ch, device=dev, dtype=dt)
+            _, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps, df=dpc[:, :C])
+            _, grads["ls1e"] = K.residual_bwd(dxe1, p1e, ls1e, rowscale_e, rps, df=dpc[:, C:])
+            dWc, dbc = K.linear_wgrad(dpc, f, out=gslot_rows(wp, wpe), bias_grad=True, bias_out=gslot_rows(bp, bpe))
+            grads["wp"], grads["wpe"] = dWc[:C], dWc[C:]
+            grads["bp"], grads["bpe"] = dbc[:C], dbc[C:]
+            df = K.linear_dgrad(dpc, wcast(dt, wp, wpe))
             dxe_res = dxe1
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
         # depth branch: cxe = cx * xe'
         dcxe = df[:, fw - Ch:]
-        K.scale_mul(dcxe, mul=xep, out=dcx)
-        dxep = K.scale_mul(dcxe, mul=cx)
+        _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
         grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=gslot2(web), bias_grad=True, bias_out=gslot(beb))
         de2 = K.linear_dgrad(dxep, wcast(dt, web))
         grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7, dw=gslot(wec), db=gslot(bec))
@@ -332,8 +355,7 @@ class AttentionFn(torch.autograd.Function):
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
-        K.scale_mul(dqa, mul=a, out=dq)
-        da = K.scale_mul(dqa, mul=q)
+        _, da = K.dual_mul(dqa, a, q, out1=dq)
         grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=gslot2(wa), bias_grad=True, bias_out=gslot(ba))
         dapre = K.linear_dgrad(da, wcast(dt, wa))
         grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=gslot(wconv), db=gslot(bconv))

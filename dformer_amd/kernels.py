@@ -365,6 +365,20 @@ def scale_mul(src, mul=None, colscale=None, rowscale=None, rows_per_scale=1, alp
     return out
 
 
+def dual_mul(src, m1, m2, out1=None, out2=None):
+    """(src * m1, src * m2) in one pass over src (the two gradients of an elementwise product)."""
+    rows, C = src.shape
+    if out1 is None:
+        out1 = torch.empty(rows, C, device=src.device, dtype=src.dtype)
+    if out2 is None:
+        out2 = torch.empty(rows, C, device=src.device, dtype=src.dtype)
+    check(lib.dfm_dual_mul(dtype_code(src), rows, C, ptr(src), ld(src), ptr(m1), ld(m1), ptr(m2), ld(m2), ptr(out1),
+                           ld(out1), ptr(out2), ld(out2), stream()), "dfm_dual_mul")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(src) * 5)
+    return out1, out2
+
+
 # ---------------------------------------------------------------------- pool / bilinear / attn
 def pool7(x, shape, out=None):
     B, H, W = shape

@@ -185,6 +185,11 @@ int dfm_scale_mul(int dtype, long rows, int C, const void* src, long ldsrc, cons
                   const float* colscale, const float* rowscale, long rows_per_scale, float alpha,
                   void* dst, long lddst, int accumulate, dfm_stream_t stream);
 
+/* o1 = src * m1, o2 = src * m2 in one pass over src: the gradients of an elementwise product
+ * d(q*a) -> (d*a, d*q), d(cx*xe') -> (d*xe', d*cx) (DFormer.py:134-135 backward). */
+int dfm_dual_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* m1, long ld1, const void* m2,
+                 long ld2, void* o1, long ldo1, void* o2, long ldo2, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- pooled-query attention
  * AdaptiveAvgPool2d(7) over NHWC (DFormer.py:92,124): y[b][i*7+j][c] = bin mean. */
 int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, const void* x, long ldx, void* y,

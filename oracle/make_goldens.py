@@ -302,6 +302,46 @@ def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, 
     save(prefix + name, **{k: np.array(v) for k, v in env.items()})
 
 
+def golden_msf(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, scales=(0.75, 1.0, 1.25), flip=True):
+    """The reference's own evaluate_msf (utils/val_mm.py:325-472) over two batches with the model in
+    eval mode (encode_decode with the HEAD tuple bug routed around; NMF bases injected): the summed
+    softmax scores handed to Metrics.update and the final confusion histogram."""
+    import utils.val_mm as val_mm  # noqa: E402  (the reference, read-only)
+    t0 = time.time()
+    model, cfg = build_segmentor(backbone, decoder, ncls, embed)
+    model.eval()
+    bases = gen.nmf_bases(B, 512, 64, name=name + "/bases") if decoder == "ham" else None
+
+    class Wrapped(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.m = model
+
+        def forward(self, rgb, dep):
+            return e2e_forward(self.m, rgb, dep, bases)[2]
+
+    captured = []
+
+    class RecMetrics(val_mm.Metrics):
+        def update(self, pred, target):
+            captured.append(pred.detach().clone())
+            super().update(pred, target)
+
+    val_mm.Metrics = RecMetrics
+    loader = []
+    for i in range(2):
+        rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=8964 + i)
+        loader.append({"rgb": torch.from_numpy(rgb_np), "modal_x": torch.from_numpy(dep_np),
+                       "gt": torch.from_numpy(gen.labels(B, H, W, ncls, seed=8964 + i)).long(), "fn": ["x.png"]})
+    config = Cfg(num_classes=ncls, background=255, dataset_name="NYUDepthv2")
+    engine = Cfg(distributed=False, local_rank=0)
+    with torch.no_grad():
+        metrics = val_mm.evaluate_msf(Wrapped(), loader, config, torch.device("cpu"), list(scales), flip, engine)
+    save(name, scores0=captured[0].numpy().astype(np.float32), scores1=captured[1].numpy().astype(np.float32),
+         hist=metrics.hist.numpy(), scales=np.array(scales), meta=np.array([B, H, W, ncls, int(flip)]))
+    print(f"  {name}: {time.time() - t0:.1f}s")
+
+
 def golden_groups():
     """Optimizer-group membership of group_weight (init_func.py:26-70) for Base + ham."""
     from utils.init_func import group_weight
@@ -363,6 +403,9 @@ def main():
         golden_e2e("e2e_tiny_full_fwd", "DFormer-Tiny", 2, 480, 640, backward=False)
     if want("groups"):
         golden_groups()
+    if want("msf"):
+        golden_msf("msf_tiny_ham", "DFormer-Tiny", 2, 50, 70)
+        golden_msf("msf_tiny_mlp", "DFormer-Tiny", 1, 45, 61, decoder="MLPDecoder", ncls=37, embed=64)
     if want("bf16env"):
         golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
         golden_bf16_env("e2e_base_small", "DFormer-Base", 2, 64, 80)

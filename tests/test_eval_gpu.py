@@ -113,3 +113,40 @@ def test_evaluate_msf_vs_oracle(arch, dec, ncls):
     iou_ref = (h.diag() / (h.sum(0) + h.sum(1) - h.diag())).nan_to_num(0.0)
     assert abs(miou - round(iou_ref.mean().item() * 100, 2)) < 1e-6
     assert len(ious) == ncls
+
+
+@pytest.mark.parametrize("name,arch,dec,ncls,embed", [("msf_tiny_ham", "DFormer-Tiny", "ham", 40, 512),
+                                                      ("msf_tiny_mlp", "DFormer-Tiny", "MLPDecoder", 37, 64)])
+def test_evaluate_msf_vs_reference_golden(name, arch, dec, ncls, embed):
+    """The HIP evaluate_msf against the reference's own evaluate_msf (utils/val_mm.py:325-472, run by
+    oracle/make_goldens.py golden_msf over two batches): the summed softmax scores of every batch at
+    1e-3 (fp32) and the confusion histogram (argmax near-ties may flip a handful of pixels)."""
+    from goldens import load
+    from dformer_amd.evaluate import evaluate_msf, msf_scores
+    from dformer_amd.segmentor import EncoderDecoder
+    g = load(name)
+    B, H, W, _, flip = [int(v) for v in g["meta"]]
+    scales = [float(s) for s in g["scales"]]
+    cfg = Cfg(backbone=arch, decoder=dec, decoder_embed_dim=embed, num_classes=ncls, drop_path_rate=0.0,
+              bn_eps=1e-3, bn_momentum=0.1, background=255)
+    model = EncoderDecoder(cfg=cfg)
+    sd = model.state_dict()
+    vals = gen.state_dict_values([(k, v.shape) for k, v in sd.items()])
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)).to(sd[k].dtype) for k, v in vals.items()})
+    model = model.cuda().eval()
+    if dec == "ham":
+        model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
+            gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
+    loader = []
+    for i in range(2):
+        rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=8964 + i)
+        loader.append({"rgb": torch.from_numpy(rgb_np).float(), "modal_x": torch.from_numpy(dep_np).float(),
+                       "gt": torch.from_numpy(gen.labels(B, H, W, ncls, seed=8964 + i))})
+        acc = msf_scores(model, loader[-1]["rgb"].cuda(), loader[-1]["modal_x"].cuda(), ncls, scales, bool(flip))
+        got = acc.view(B, H, W, ncls).permute(0, 3, 1, 2).cpu()
+        assert rel(got, torch.from_numpy(g[f"scores{i}"])) < 1e-3, (i, rel(got, torch.from_numpy(g[f"scores{i}"])))
+    m = evaluate_msf(model, loader, cfg, DEV, scales, bool(flip))
+    ours, ref = m.hist.cpu().numpy(), g["hist"]
+    valid = ref.sum()
+    assert ours.sum() == valid
+    assert np.abs(ours - ref).sum() / 2 <= max(2, 1e-3 * valid), np.abs(ours - ref).sum() / 2

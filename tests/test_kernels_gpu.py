@@ -515,3 +515,17 @@ def test_dgrad_gelu_grad_epilogue(dt):
     pr = pre.float().requires_grad_()
     torch.nn.functional.gelu(pr).backward(dy.float() @ w.float())
     assert rel(out.float(), pr.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("C", [64, 96, 36])
+def test_dual_mul(dt, C):
+    """(src*m1, src*m2) in one pass, on column slices of wider buffers (vector path) and C % 8 != 0."""
+    k = K()
+    rows = 1000
+    buf = torch.randn(rows, 3 * C + 8, device=DEV).to(dt)
+    src, m1, m2 = buf[:, :C], buf[:, C:2 * C], buf[:, 2 * C:3 * C]
+    outb = torch.empty(rows, 2 * C + 8, device=DEV, dtype=dt)
+    o1, o2 = k.dual_mul(src, m1, m2, out1=outb[:, :C], out2=outb[:, C + 8:2 * C + 8])
+    assert rel(o1.float(), src.float() * m1.float()) < TOL[dt]
+    assert rel(o2.float(), src.float() * m2.float()) < TOL[dt]

@@ -166,3 +166,25 @@ def test_optimizer_groups_golden():
     n_excl = sum(int(np.prod(shapes[n])) for n in excluded)
     assert n_excl == int(g["counts"][0]) == 41024
     assert len(excluded) == 236
+
+
+@pytest.mark.parametrize("name,arch,dec,ncls,embed", [("msf_tiny_ham", "DFormer-Tiny", "ham", 40, 512),
+                                                      ("msf_tiny_mlp", "DFormer-Tiny", "MLPDecoder", 37, 64)])
+def test_msf_golden(name, arch, dec, ncls, embed):
+    """The oracle's evaluate_msf restatement (msf_scores, confusion) against the reference's own
+    evaluate_msf run (utils/val_mm.py:325-472; oracle/make_goldens.py golden_msf)."""
+    g = load(name)
+    B, H, W, _, flip = [int(v) for v in g["meta"]]
+    scales = [float(s) for s in g["scales"]]
+    p = params(R.segmentor_shapes(arch, dec, ncls, embed), requires_grad=False)
+    bufs = {k: v.clone() for k, v in p.items() if "running" in k}
+    bases = torch.from_numpy(gen.nmf_bases(B, 512, 64, name=name + "/bases")) if dec == "ham" else None
+    hist = 0
+    for i in range(2):
+        rgb, dep = (torch.from_numpy(a) for a in gen.rgb_depth(B, H, W, seed=8964 + i))
+        lab = torch.from_numpy(gen.labels(B, H, W, ncls, seed=8964 + i))
+        with torch.no_grad():
+            sc = R.msf_scores(p, arch, dec, rgb, dep, ncls, scales, bool(flip), bases, buffers=bufs)
+        assert rel_err(sc, g[f"scores{i}"]) < 1e-6
+        hist = hist + R.confusion(sc, lab, ncls)
+    assert np.array_equal(hist.numpy(), g["hist"])
