@@ -112,6 +112,48 @@ def gslot_rows(*ps):
     return ss[0][0][ss[0][1]:off].view(rows, *cols) if cols else ss[0][0][ss[0][1]:off]
 
 
+# ---------------------------------------------------------------- weight-gradient stream
+# The weight gradients (split-K wgrad GEMMs, depthwise dW) are off the backward's critical path:
+# nothing consumes them before the optimizer. When they land in flat-gradient slots (persistent
+# buffers, FusedAdamW built) they are issued on a second stream that forks from the current one at
+# each call, so they overlap the data-gradient chain of the following layers (the stage-2/3 kernels
+# alone are latency-bound and leave most CUs idle). FusedAdamW.step and GradBuckets' all-reduces
+# join the stream (join_wgrad). Off by default (DFM_WGRAD_STREAM=1 enables it): measured on MI355X
+# the overlap LOSES — 369.8 vs 381.1 images/s on the DFormer-B step — the split-K wgrad grids
+# (hundreds of blocks) crowd out the latency-bound data-gradient chain instead of filling its gaps.
+_WG_ON = os.environ.get("DFM_WGRAD_STREAM", "0") == "1"
+_WG_STREAM = {}
+
+
+def _wg_stream(dev):
+    s = _WG_STREAM.get(dev)
+    if s is None:
+        s = _WG_STREAM[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def offload_wgrad(outs, inputs, fn):
+    """fn() — weight-gradient launches writing only into `outs` — on the weight-gradient stream when
+    every out is a flat-gradient slot; `inputs` (the tensors fn reads) are recorded on that stream
+    so the allocator does not hand their memory out before it is done."""
+    if not _WG_ON or any(o is None for o in outs) or not inputs[0].is_cuda:
+        return fn()
+    dev = inputs[0].device
+    ws = _wg_stream(dev)
+    ws.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(ws):
+        r = fn()
+    for t in inputs:
+        t.record_stream(ws)
+    return r
+
+
+def join_wgrad():
+    """The current stream waits for every weight-gradient launch issued so far."""
+    for dev, s in _WG_STREAM.items():
+        torch.cuda.current_stream(dev).wait_stream(s)
+
+
 def _cat1(*vs):
     """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
     key = tuple(id(v) for v in vs) + ("bias",)
@@ -195,11 +237,17 @@ class ConvFFNFn(torch.autograd.Function):
         W1, W2 = wcast(dt, w1), wcast(dt, w2)
         rps = H * W
         df, dls = K.residual_bwd(dout, f, ls, rowscale, rps)
-        dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
+        o2, ob2 = gslot2(w2), gslot(b2)
+        dW2, db2 = offload_wgrad((o2, ob2), (df, g),
+                                 lambda: K.linear_wgrad(df, g, out=o2, bias_grad=True, bias_out=ob2))
         dhpre = K.linear_dgrad(df, W2, gelu_grad_of=hpre)  # GELU backward fused into the epilogue
-        dwpos, dbpos = K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=gslot(wpos), db=gslot(bpos))
+        ow, ob = gslot(wpos), gslot(bpos)
+        dwpos, dbpos = offload_wgrad((ow, ob), (h, dhpre),
+                                     lambda: K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=ow, db=ob))
         dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
-        dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
+        o1, ob1 = gslot2(w1), gslot(b1)
+        dW1, db1 = offload_wgrad((o1, ob1), (dh, xn),
+                                 lambda: K.linear_wgrad(dh, xn, out=o1, bias_grad=True, bias_out=ob1))
         dxn = K.linear_dgrad(dh, W1)
         dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
         return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
@@ -319,7 +367,9 @@ class AttentionFn(torch.autograd.Function):
             dpc = torch.empty(P, C + Ch, device=dev, dtype=dt)
             _, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps, df=dpc[:, :C])
             _, grads["ls1e"] = K.residual_bwd(dxe1, p1e, ls1e, rowscale_e, rps, df=dpc[:, C:])
-            dWc, dbc = K.linear_wgrad(dpc, f, out=gslot_rows(wp, wpe), bias_grad=True, bias_out=gslot_rows(bp, bpe))
+            ow, ob = gslot_rows(wp, wpe), gslot_rows(bp, bpe)
+            dWc, dbc = offload_wgrad((ow, ob), (dpc, f),
+                                     lambda: K.linear_wgrad(dpc, f, out=ow, bias_grad=True, bias_out=ob))
             grads["wp"], grads["wpe"] = dWc[:C], dWc[C:]
             grads["bp"], grads["bpe"] = dbc[:C], dbc[C:]
             df = K.linear_dgrad(dpc, wcast(dt, wp, wpe))
@@ -330,11 +380,17 @@ class AttentionFn(torch.autograd.Function):
         # depth branch: cxe = cx * xe'
         dcxe = df[:, fw - Ch:]
         _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
-        grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=gslot2(web), bias_grad=True, bias_out=gslot(beb))
+        ow, ob = gslot2(web), gslot(beb)
+        grads["web"], grads["beb"] = offload_wgrad((ow, ob), (dxep, e2), lambda: K.linear_wgrad(
+            dxep, e2, out=ow, bias_grad=True, bias_out=ob))
         de2 = K.linear_dgrad(dxep, wcast(dt, web))
-        grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7, dw=gslot(wec), db=gslot(bec))
+        ow, ob = gslot(wec), gslot(bec)
+        grads["wec"], grads["bec"] = offload_wgrad((ow, ob), (e1, de2), lambda: K.dwconv_bwd_weight(
+            e1, de2, shape, 7, dw=ow, db=ob))
         de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
-        grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, out=gslot2(wef), bias_grad=True, bias_out=gslot(bef))
+        ow, ob = gslot2(wef), gslot(bef)
+        grads["wef"], grads["bef"] = offload_wgrad((ow, ob), (de1, xen), lambda: K.linear_wgrad(
+            de1, xen, out=ow, bias_grad=True, bias_out=ob))
         dxen = K.linear_dgrad(de1, wcast(dt, wef))
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
@@ -346,19 +402,26 @@ class AttentionFn(torch.autograd.Function):
             dkv = torch.empty(P, C, device=dev, dtype=dt)
             K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
                               dkv[:, :Ch], dkv[:, Ch:])
-            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, out=gslot2(wsc), bias_grad=True,
-                                                        bias_out=gslot(bsc))
+            ow, ob = gslot2(wsc), gslot(bsc)
+            grads["wsc"], grads["bsc"] = offload_wgrad((ow, ob), (dm, pooled), lambda: K.linear_wgrad(
+                dm, pooled, out=ow, bias_grad=True, bias_out=ob))
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
             K.pool7_bwd(dpooled[:, C:], shape, dx=dxen, accumulate=True)
-            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, out=gslot2(wkv), bias_grad=True, bias_out=gslot(bkv))
+            ow, ob = gslot2(wkv), gslot(bkv)
+            grads["wkv"], grads["bkv"] = offload_wgrad((ow, ob), (dkv, g), lambda: K.linear_wgrad(
+                dkv, g, out=ow, bias_grad=True, bias_out=ob))
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
         _, da = K.dual_mul(dqa, a, q, out1=dq)
-        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=gslot2(wa), bias_grad=True, bias_out=gslot(ba))
+        ow, ob = gslot2(wa), gslot(ba)
+        grads["wa"], grads["ba"] = offload_wgrad((ow, ob), (da, apre), lambda: K.linear_wgrad(
+            da, apre, out=ow, bias_grad=True, bias_out=ob))
         dapre = K.linear_dgrad(da, wcast(dt, wa))
-        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=gslot(wconv), db=gslot(bconv))
+        ow, ob = gslot(wconv), gslot(bconv)
+        grads["wconv"], grads["bconv"] = offload_wgrad((ow, ob), (g, dapre), lambda: K.dwconv_bwd_weight(
+            g, dapre, shape, 7, dw=ow, db=ob))
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.gelu_bwd(dg, lpre, out=dl)
         # q | q_cut | l

@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
-from .functional import invalidate_weights, register_grad_slot, register_shadow
+from .functional import invalidate_weights, join_wgrad, register_grad_slot, register_shadow
 
 
 def group_weight(module, norm_layer=nn.BatchNorm2d):
@@ -128,6 +128,7 @@ class GradBuckets:
         if self.pending[bi] == 0:
             self._flush(bi)
             if self.world > 1:
+                join_wgrad()  # weight gradients written on the weight-gradient stream are complete
                 self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
 
     def _flush(self, bi):
@@ -152,6 +153,7 @@ class GradBuckets:
                         g.grad[off:off + k].zero_()
                 self._flush(bi)
                 if self.world > 1:
+                    join_wgrad()
                     self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
             h.wait()
@@ -220,6 +222,7 @@ class FusedAdamW:
         self.scaler = LossScaler(dev) if compute_dtype == torch.float16 else None
 
     def step(self, lr=None):
+        join_wgrad()
         self.buckets.finish()
         for p in self.ungrouped:
             p.grad = None
