@@ -1175,6 +1175,20 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
       return glds_ak<64, 128, 4, 2, 2, 3>(a, bk, s);
     }
   }
+  // Few row tiles (the stage-2/3 GEMMs: M = 19,200 / 4,800 rows) leave CUs idle with 128-row tiles:
+  // 64-row tiles double the blocks (DFM_GEMM_BM64=0 disables; no split-K, N > 64 only).
+  static const int bm64_env = [] {
+    const char* e = getenv("DFM_GEMM_BM64");
+    return e ? atoi(e) : 1;
+  }();
+  if (bm64_env && BN == 128 && a.splits == 1 && (long)cdiv(d->M, 128) * cdiv(a.Nw, 128) * a.batch < 512) {
+    if (small_k) {
+      constexpr int BKs = sizeof(T) == 2 ? 32 : 16;
+      return launch_layout<T, 64, 128, 4, 2, BKs, 1>(a, ak, bk, s);
+    }
+    constexpr int BKl = sizeof(T) == 2 ? 64 : 32;
+    return launch_depth<T, 64, 128, 4, 2, BKl>(a, ak, bk, s);
+  }
   if (small_k) {
     constexpr int BKs = sizeof(T) == 2 ? 32 : 16;
     if (BN == 32) return launch_layout<T, 128, 32, 4, 4, BKs, 1>(a, ak, bk, s);

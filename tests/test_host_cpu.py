@@ -1,0 +1,71 @@
+"""Host-side logic that needs no GPU: flat-gradient slot spans, the fp16 loss-scale schedule, the
+evaluate_msf input sizes and the SyncBN count cache."""
+import torch
+import torch.nn as nn
+
+
+def test_gslot_rows_spans_adjacent_slots_only():
+    from dformer_amd.functional import clear_grad_slots, gslot_rows, register_grad_slot
+    clear_grad_slots()
+    flat = torch.zeros(1000)
+    a = nn.Parameter(torch.zeros(4, 6))
+    b = nn.Parameter(torch.zeros(2, 6))
+    c = nn.Parameter(torch.zeros(3, 5))
+    register_grad_slot(a, flat, 0)
+    register_grad_slot(b, flat, 24)       # right after a
+    register_grad_slot(c, flat, 100)      # not adjacent to b
+    span = gslot_rows(a, b)
+    assert span is not None and span.shape == (6, 6) and span.data_ptr() == flat.data_ptr()
+    span[4:].fill_(1.0)
+    assert flat[24:36].eq(1.0).all() and flat[:24].eq(0.0).all()
+    assert gslot_rows(b, c) is None                      # gap between the slots
+    assert gslot_rows(a, c) is None
+    d = nn.Parameter(torch.zeros(6))
+    e = nn.Parameter(torch.zeros(2))
+    register_grad_slot(d, flat, 200)
+    register_grad_slot(e, flat, 206)
+    v = gslot_rows(d, e)                                 # 1-D slots (biases)
+    assert v is not None and v.shape == (8,)
+    assert gslot_rows(a, nn.Parameter(torch.zeros(1, 6))) is None  # no slot at all
+    clear_grad_slots()
+
+
+def test_loss_scaler_schedule_matches_gradscaler_defaults():
+    """torch.cuda.amp.GradScaler: init 2**16, x0.5 on an inf/nan step, x2 after 2000 clean steps."""
+    from dformer_amd.train import LossScaler
+    s = LossScaler("cpu")
+    assert s.scale == 65536.0
+    s.update(True)
+    assert s.scale == 32768.0 and s.growth_tracker == 0 and s.skipped == 1
+    for _ in range(1999):
+        s.update(False)
+    assert s.scale == 32768.0 and s.growth_tracker == 1999
+    s.update(False)
+    assert s.scale == 65536.0 and s.growth_tracker == 0
+
+
+def test_msf_sizes_follow_val_mm():
+    """val_mm.py:359-364: int(scale * H) rounded up to a multiple of 32."""
+    from dformer_amd.evaluate import msf_size
+    assert msf_size(480, 640, 1.0) == (480, 640)
+    assert msf_size(480, 640, 0.75) == (384, 480)
+    assert msf_size(480, 640, 1.25) == (608, 800)
+    assert msf_size(530, 730, 0.5) == (288, 384)
+    assert msf_size(50, 70, 0.75) == (64, 64)
+
+
+def test_metrics_formulas_match_reference():
+    """utils/metrics_new.py compute_iou / compute_f1 / compute_pixel_acc on a fixed histogram."""
+    from dformer_amd.evaluate import Metrics
+    m = Metrics(3, 255, "cpu")
+    h = torch.tensor([[5, 1, 0], [2, 7, 1], [0, 0, 0]], dtype=torch.int64)
+    m._hist += h.view(-1)
+    ious, miou = m.compute_iou()
+    hf = h.float()  # the reference keeps a float32 histogram
+    want = hf.diag() / (hf.sum(0) + hf.sum(1) - hf.diag())
+    want[want.isnan()] = 0
+    assert ious == (want * 100).numpy().round(2).tolist() and miou == round(want.mean().item() * 100, 2)
+    f1, mf1 = m.compute_f1()
+    assert len(f1) == 3 and f1[2] == 0.0
+    acc, macc = m.compute_pixel_acc()
+    assert abs(acc[0] - 83.33) < 1e-3 and abs(macc - round((5 / 6 + 0.7) / 3 * 100, 2)) < 1e-3
