@@ -1176,10 +1176,12 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     }
   }
   // Few row tiles (the stage-2/3 GEMMs: M = 19,200 / 4,800 rows) leave CUs idle with 128-row tiles:
-  // 64-row tiles double the blocks (DFM_GEMM_BM64=0 disables; no split-K, N > 64 only).
+  // 64-row tiles double the blocks (DFM_GEMM_BM64=1; no split-K, N > 64 only). Off by default:
+  // measured on the DFormer-B step it does not pay (379.4 vs 382.8 images/s) — the per-block k-loop
+  // latency, not the block count, bounds these shapes.
   static const int bm64_env = [] {
     const char* e = getenv("DFM_GEMM_BM64");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   if (bm64_env && BN == 128 && a.splits == 1 && (long)cdiv(d->M, 128) * cdiv(a.Nw, 128) * a.batch < 512) {
     if (small_k) {
