@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void);
+int dfm_abi_version(void); /* 3 (round 2: DFM_F16; copy_dtype on dfm_adamw* / dfm_nmf_update*) */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
