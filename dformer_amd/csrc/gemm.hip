@@ -1057,7 +1057,7 @@ int launch_stream(GemmArgs& a, hipStream_t s) {
 
 template <typename T, int BM, int BN, int NW, int WM_, int BK, int DEPTH>
 int launch_layout(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
-  if constexpr (DEPTH == 1 && BN <= 64 && sizeof(T) == 2) {
+  if constexpr (DEPTH == 1 && BN <= 128 && sizeof(T) == 2) {
     if (a.stream && ak && bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, true>(a, s);
     if (a.stream && ak && !bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, false>(a, s);
   }
@@ -1155,7 +1155,10 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   {  // large M x short K: persistent M-streaming kernel
     const int BKsel = small_k ? (sizeof(T) == 2 ? 32 : 16) : (sizeof(T) == 2 ? 64 : 32);
     const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
-    a.stream = stream_env != 0 && sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb && d->K % BKsel == 0 &&
+    // DFM_GEMM_STREAM=2 also streams 128-wide column tiles (large-M short-K forward GEMMs with
+    // 64 < N, e.g. fc1 / q|q_cut|l at stage 0)
+    a.stream = stream_env != 0 && sizeof(T) == 2 && (BN <= 64 || (stream_env >= 2 && BN == 128)) && ak &&
+               a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb && d->K % BKsel == 0 &&
                d->K / BKsel <= 8 && tiles >= 1024;
   }
   static const int glds_env = [] {  // DFM_GEMM_GLDS=0 disables the LDS-DMA kernel (A/B timing)
