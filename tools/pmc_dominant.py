@@ -10,7 +10,7 @@ algorithmic bytes for the same launches -> profiles/<round>_dominant_pmc.json (r
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; on gfx950 FETCH_SIZE counts wide
 streaming reads at half their bytes, MI355X_MICROARCH.md HBM section). MFMA busy = the per-SIMD
 share of GUI-active cycles the MFMA pipe was busy (SQ_VALU_MFMA_BUSY_CYCLES is summed over the
-1024 SIMDs of the chip)."""
+1024 SIMDs of the chip, GRBM_GUI_ACTIVE over its 8 XCDs)."""
 import csv
 import glob
 import json
@@ -47,7 +47,9 @@ def main():
            "algorithmic_bytes_per_launch": round(algo), "algorithmic_flops_per_launch": round(flops),
            "hbm_read_bytes_per_launch": round(rd), "hbm_write_bytes_per_launch": round(wr),
            "traffic_bytes_per_launch": round(rd + wr), "traffic_over_algorithmic": round((rd + wr) / algo, 3),
-           "mfma_busy_per_simd": round(sum(busy) / max(sum(gui), 1) / 1024, 4) if busy and gui else None,
+           # SQ_VALU_MFMA_BUSY_CYCLES summed over the 1024 SIMDs, GRBM_GUI_ACTIVE over the 8 XCDs
+           # (MI355X_MICROARCH.md): busy share of a SIMD's cycles while the kernel ran
+           "mfma_busy_per_simd": round(8 * sum(busy) / max(sum(gui), 1) / 1024, 4) if busy and gui else None,
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_VALU_MFMA_BUSY_CYCLES+GRBM_GUI_ACTIVE in separate "
                      "passes over bench.py --eager steps, filtered to the kernel; FETCH_SIZE x2 (gfx950); "
                      "averages over every launch of the kernel in the profiled steps"}
