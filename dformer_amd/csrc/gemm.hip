@@ -461,7 +461,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
     tile = lid % gridDim.x;
     zs = lid / gridDim.x;
   }
-  const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * BN;
+  // n_fast: consecutive blocks walk the column tiles of one row tile, so a tall A row block (large-M
+  // forward / dgrad with several column tiles) is re-read from L2 rather than from HBM
+  const int bm = (a.n_fast ? tile / a.tiles_n : tile % tiles_m) * BM;
+  const int bn = (a.n_fast ? tile % a.tiles_n : tile / tiles_m) * BN;
   const int b = zs / a.splits, split = zs % a.splits;
 
   const int kper = ((a.K + a.splits - 1) / a.splits + BK - 1) / BK * BK;
@@ -1011,6 +1014,11 @@ int launch_cfg(GemmArgs& a, hipStream_t s) {
   const size_t lds_c = (size_t)RP * (BN + 4) * sizeof(float);
   const size_t lds = lds_op > lds_c ? lds_op : lds_c;
   a.tiles_n = cdiv(a.Nw, BN);
+  static const int nfast_env = [] {  // DFM_GEMM_NFAST=0: row tiles fastest (A/B timing)
+    const char* e = getenv("DFM_GEMM_NFAST");
+    return e ? atoi(e) : 1;
+  }();
+  a.n_fast = nfast_env && a.tiles_n > 1 && a.M >= a.Nw;
   dim3 grid(cdiv(a.M, BM) * a.tiles_n, 1, a.batch * a.splits);
   static bool attr_set = false;
   if (!attr_set) {
