@@ -50,8 +50,11 @@ def parse():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--arch", default="DFormer-Base")
     ap.add_argument("--decoder", default="ham")
+    ap.add_argument("--ncls", type=int, default=40, help="classes (NYUDepthv2 40, SUNRGBD 37)")
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="compute dtype; fp16 = the reference's --amp (loss scaling, eager launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-census", action="store_true")
@@ -234,19 +237,20 @@ def main():
     from dformer_amd.train import FusedAdamW, GraphedTrainStep, train_step
 
     torch.manual_seed(8964 + rank)
-    cfg = make_cfg(args.arch, args.decoder)
+    cfg = make_cfg(args.arch, args.decoder, args.ncls)
     model = EncoderDecoder(cfg=cfg, syncbn=world > 1)
     for m in model.decode_head.modules():  # init_func.init_weight: kaiming on decoder convs
         if isinstance(m, torch.nn.Conv2d):
             torch.nn.init.kaiming_normal_(m.weight, mode="fan_in", nonlinearity="relu")
     sd_cpu = {k: v.clone() for k, v in model.state_dict().items()} if rank == 0 else None
-    model = model.to(dev).set_compute_dtype(torch.bfloat16)
+    cdt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    model = model.to(dev).set_compute_dtype(cdt)
     if world > 1:
         for t in model.state_dict().values():
             dist.broadcast(t, 0)
     model.return_logits = False
     model.train()
-    opt = FusedAdamW(model, lr=cfg.lr, weight_decay=cfg.weight_decay, world=world, compute_dtype=torch.bfloat16)
+    opt = FusedAdamW(model, lr=cfg.lr, weight_decay=cfg.weight_decay, world=world, compute_dtype=cdt)
     rgb, dep, lab = synthetic_batch(args.batch, args.height, args.width, cfg.num_classes, dev, 8964 + rank)
 
     def step():
@@ -262,6 +266,7 @@ def main():
     # the whole step is captured once and replayed, so ~2.3k kernel launches cost one graph launch
     graph_env = os.environ.get("DFM_GRAPH")
     use_graph = not args.eager and (graph_env == "1" or (graph_env is None and world == 1))
+    use_graph = use_graph and opt.scaler is None  # the fp16 loss scaler reads its overflow flag on the host
     if use_graph:
         step = GraphedTrainStep(model, opt, rgb, dep, lab)
     torch.cuda.synchronize()
@@ -306,7 +311,7 @@ def main():
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights)",
+        "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (random-init weights)",
         "config": {"workload": f"{args.arch}+{args.decoder} train step fwd+bwd+AdamW",
                    "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                    "image": [args.height, args.width], "parallelism": f"dp{world}"},
