@@ -270,6 +270,24 @@ class ConvFFNFn(torch.autograd.Function):
 
 
 # ====================================================================== Attention (+ residuals)
+# The depth branch of the attention forward (LN_e -> e_fore -> DW7x7 -> e_back, DFormer.py:84-88,
+# 133) is independent of the RGB branch until the projections: it runs on a side stream forked at
+# the Block's start and joined before proj (DFM_ATTN_STREAM=1). Off by default: measured on the
+# DFormer-B step it does not pay (381.6 vs 383.4 images/s, two A/B pairs) — unlike the depth-branch
+# ConvFFN stream, the branch is short and the fork/join events cost what the overlap gains.
+_ATTN_SIDE_ON = os.environ.get("DFM_ATTN_STREAM", "0") == "1"
+_ATTN_SIDE = {}
+
+
+def _attn_side(dev):
+    if not _ATTN_SIDE_ON:
+        return None
+    st = _ATTN_SIDE.get(dev)
+    if st is None:
+        st = _ATTN_SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
 class AttentionFn(torch.autograd.Function):
     """(x1, xe1) = (x + rs*ls1*proj(f), xe + rs*ls1e*proj_e(f)),  f = cat(q*a, attn, cx*xe')
 
@@ -288,8 +306,21 @@ class AttentionFn(torch.autograd.Function):
         dev = x.device
         rps = H * W
         ctx.tag = K.TAG
+        side = _attn_side(dev) if x.is_cuda else None
+        main = torch.cuda.current_stream(dev) if side is not None else None
+        fw = 2 * C if window else C + Ch
+        f = torch.empty(P, fw, device=dev, dtype=dt)
+        if side is not None:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):  # depth branch, part 1: LN_e, e_fore, DW7x7
+                xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
+                ev_xen = torch.cuda.Event()
+                ev_xen.record(side)
+                e1 = K.linear(xen, wcast(dt, wef), bef)
+                e2 = K.dwconv(e1, shape, wec, bec, 7)
+        else:
+            xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
-        xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         # q | q_cut | l in one GEMM; GELU (and its pre-activation store) only on the l columns
         Wqcl = wcast(dt, wq, wqc, wl)
         bqcl = _cat1(bq, bqc, bl)
@@ -297,8 +328,11 @@ class AttentionFn(torch.autograd.Function):
         lpre = torch.empty(P, C, device=dev, dtype=dt)
         K.linear(xn, Wqcl, bqcl, act=1, preact=lpre, act_col0=C + Ch, out=qcl)
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
-        fw = 2 * C if window else C + Ch
-        f = torch.empty(P, fw, device=dev, dtype=dt)
+        xep = torch.empty(P, Ch, device=dev, dtype=dt)
+        if side is not None:  # depth branch, part 2: e_back * cx (needs the q|q_cut|l GEMM)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
         # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward)
         apre = K.dwconv(g, shape, wconv, bconv, 7)
         a = torch.empty(P, C, device=dev, dtype=dt)
@@ -309,16 +343,24 @@ class AttentionFn(torch.autograd.Function):
             kv = K.linear(g, wcast(dt, wkv), bkv)
             pooled = torch.empty(B * 49, C + Ch, device=dev, dtype=dt)
             K.pool7(xn, shape, out=pooled[:, :C])
+            if side is not None:
+                main.wait_event(ev_xen)
             K.pool7(xen, shape, out=pooled[:, C:])
             m = K.linear(pooled, wcast(dt, wsc), bsc)
             o, lse = K.pooled_attn(m, kv[:, :Ch], kv[:, Ch:], B, heads, P // B, dh, dh ** -0.5)
             K.bilinear(o, (7, 7), (H, W), B, out=f[:, C:C + Ch])
             saved_attn = (kv, pooled, m, o, lse)
         # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
-        e1 = K.linear(xen, wcast(dt, wef), bef)
-        e2 = K.dwconv(e1, shape, wec, bec, 7)
-        xep = torch.empty(P, Ch, device=dev, dtype=dt)
-        K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
+        if side is None:
+            e1 = K.linear(xen, wcast(dt, wef), bef)
+            e2 = K.dwconv(e1, shape, wec, bec, 7)
+            K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
+        else:  # join; tensors that crossed streams stay alive until both are done with them
+            main.wait_stream(side)
+            for t in (xen, mu2, rs2, e1, e2):
+                t.record_stream(main)
+            for t in (xe, f, qcl, xep):
+                t.record_stream(side)
         # projections with the Block's residual / layer-scale / DropPath epilogue
         p1 = torch.empty(P, C, device=dev, dtype=dt)
         x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
