@@ -333,7 +333,9 @@ def main():
                 "ideal_ms": round(ideal, 3), "frac": round(ideal / ms_step, 4),
                 "survey_bound_ms": round(survey_ms, 3) if survey_ms else None,
                 "survey_frac": round(survey_ms / ms_step, 4) if survey_ms else None,
-                "census_traced_ms": round(traced, 3), "census_untraced_ms": round(per_step[len(per_step) // 2] - traced, 3),
+                "census_traced_ms": round(traced, 3),
+                # per-kernel HIP events serialise and pad short kernels: traced time / graph step time
+                "census_over_step": round(traced / per_step[len(per_step) // 2], 3),
                 "census_launches": sum(r["launches"] for r in table.values()),
                 "top": [{"kernel": n[:120], "ms": round(r["measured_ms"], 3), "ideal_ms": round(r["ideal_ms"], 3),
                          "launches": r["launches"]} for n, r in top]}
