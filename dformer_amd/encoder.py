@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from . import kernels as K
 from .decoders import _allreduce, bn_batch_stats
-from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, gslot, invalidate_weights
+from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, gslot, invalidate_weights, register_side_stream
 
 _EMPTY = {}
 
@@ -116,6 +116,7 @@ def _side_stream(dev):
     s = _SIDE.get(dev)
     if s is None:
         s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        register_side_stream(s)
     return s
 
 

@@ -78,10 +78,14 @@ def msf_size(H, W, scale):
 
 
 @torch.no_grad()
-def msf_scores(model, rgb, modal_x, num_classes, scales, flip):
+def msf_scores(model, rgb, modal_x, num_classes, scales, flip, out_shape=None):
     """Summed softmax scores over scales (and flips) of one batch: float32 [B*H*W, ncls] rows
-    (val_mm.py:355-392 for one batch; `scaled_logits` of the reference, channels last)."""
-    B, _, H, W = rgb.shape
+    (val_mm.py:355-392 for one batch; `scaled_logits` of the reference, channels last). Like the
+    reference (val_mm.py:355-356) the scaled sizes and the score buffer follow the LABEL's
+    (B, H, W) = out_shape (default: the image's own size)."""
+    B, H, W = out_shape if out_shape is not None else (rgb.shape[0], rgb.shape[2], rgb.shape[3])
+    if rgb.shape[0] != B or modal_x.shape[0] != B:
+        raise ValueError(f"msf_scores: batch of the images {rgb.shape[0]} != labels {B}")
     acc = torch.zeros(B * H * W, num_classes, device=rgb.device, dtype=torch.float32)
     for scale in scales:
         size = msf_size(H, W, scale)
@@ -108,7 +112,7 @@ def evaluate_msf(model, dataloader, config, device, scales, flip, engine=None, s
         rgb = batch["rgb"].to(device)
         modal_x = batch["modal_x"].to(device)
         gt = batch["gt"].to(device)
-        acc = msf_scores(model, rgb, modal_x, config.num_classes, scales, flip)
+        acc = msf_scores(model, rgb, modal_x, config.num_classes, scales, flip, out_shape=tuple(gt.shape))
         metrics.update_rows(acc, gt)
     if engine is not None and getattr(engine, "distributed", False):
         all_metrics = [None for _ in range(engine.world_size)]

@@ -154,6 +154,29 @@ def join_wgrad():
         torch.cuda.current_stream(dev).wait_stream(s)
 
 
+_SIDE_STREAMS = []
+
+
+def register_side_stream(s):
+    """Streams besides the step's own on which this package issues gradient-writing kernels (the
+    encoder's depth-branch ConvFFN stream, the attention / weight-gradient streams)."""
+    if all(s is not t for t in _SIDE_STREAMS):
+        _SIDE_STREAMS.append(s)
+
+
+def join_streams(main=None):
+    """The current stream waits for everything issued so far on `main` (the stream the step's
+    backward was started from) and on every side stream of this package, so a collective enqueued
+    next sees every gradient slot complete whichever stream autograd ran its last hook on."""
+    streams = ([main] if main is not None else []) + _SIDE_STREAMS + list(_WG_STREAM.values())
+    if not streams:  # CPU tensors / nothing issued off the current stream
+        return
+    cur = torch.cuda.current_stream()
+    for s in streams:
+        if s is not None and s.device == cur.device and s != cur:
+            cur.wait_stream(s)
+
+
 def _cat1(*vs):
     """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
     key = tuple(id(v) for v in vs) + ("bias",)
@@ -285,6 +308,7 @@ def _attn_side(dev):
     st = _ATTN_SIDE.get(dev)
     if st is None:
         st = _ATTN_SIDE[dev] = torch.cuda.Stream(device=dev)
+        register_side_stream(st)
     return st
 
 

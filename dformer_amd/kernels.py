@@ -63,15 +63,21 @@ def _es(t):
 
 def _ws(nbytes, dev):
     """Scratch buffer per (device, stream) that only grows (the library never allocates); one per
-    stream so kernels running concurrently on a side stream never share a workspace."""
+    stream so kernels running concurrently on a side stream never share a workspace. A buffer that
+    is outgrown is retired, not freed: a HIP graph captured earlier keeps using its pointer."""
     if nbytes == 0:
         return None
     key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:  # a captured graph may still hold the old pointer: never free it
+            _ws_retired.append(buf)
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
     return buf
+
+
+_ws_retired = []
 
 
 def ld(t):
@@ -614,6 +620,8 @@ def seg_confusion(acc, label, ncls, ignore, hist):
     """hist [ncls*ncls] int64 += bincount(label*ncls + argmax(acc rows)) over label != ignore."""
     assert label.dtype == torch.int64 and hist.dtype == torch.int64 and acc.is_contiguous()
     assert label.is_contiguous()
+    if acc.dim() != 2 or acc.shape[1] != ncls or acc.shape[0] != label.numel():
+        raise ValueError(f"seg_confusion: scores {tuple(acc.shape)} do not match {label.numel()} labels x {ncls}")
     check(lib.dfm_seg_confusion(label.numel(), ncls, ptr(acc), ptr(label), ignore, ptr(hist), stream()),
           "dfm_seg_confusion")
     return hist

@@ -16,7 +16,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
-from .functional import invalidate_weights, join_wgrad, register_grad_slot, register_shadow
+from .functional import invalidate_weights, join_streams, register_grad_slot, register_shadow
 
 
 def group_weight(module, norm_layer=nn.BatchNorm2d):
@@ -107,6 +107,8 @@ class GradBuckets:
         self.pending = [len(b[1]) for b in self.buckets]
         self.copies = [[] for _ in self.buckets]
         self.fired = set()  # ids of parameters whose gradient arrived this step
+        self.unfired = []  # (group, off, k) of the last finished step's parameters without a gradient
+        self.main_stream = None  # the stream the step's backward starts from (set by train_step)
         for p in self.owner:
             p.register_post_accumulate_grad_hook(self._hook)
 
@@ -128,7 +130,10 @@ class GradBuckets:
         if self.pending[bi] == 0:
             self._flush(bi)
             if self.world > 1:
-                join_wgrad()  # weight gradients written on the weight-gradient stream are complete
+                # the bucket mixes slots written on the main stream, the depth-branch ConvFFN stream
+                # and the weight-gradient stream, and this hook runs on whichever stream autograd
+                # replays the last AccumulateGrad on: wait for all of them before RCCL reads it
+                join_streams(self.main_stream)
                 self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
 
     def _flush(self, bi):
@@ -143,7 +148,10 @@ class GradBuckets:
         """Join the step's all-reduces. Buckets holding a parameter that got no gradient this step
         (an unused branch) are completed here: the slots of such parameters are zeroed first (they
         still hold the previous step's gradient, and torch's AdamW after zero_grad() would see no
-        gradient either), then the bucket is reduced like the others."""
+        gradient either), then the bucket is reduced like the others. Their (group, offset, numel)
+        are left in `unfired`: torch's AdamW skips a parameter whose .grad is None, so FusedAdamW
+        restores their value and moments after its flat update."""
+        self.unfired = []
         for bi, b in enumerate(self.buckets):
             if self.pending[bi] > 0:
                 for p in b[1]:
@@ -151,9 +159,10 @@ class GradBuckets:
                         g = self.owner[p][1]
                         off, k = g.slots[p]
                         g.grad[off:off + k].zero_()
+                        self.unfired.append((g, off, k))
                 self._flush(bi)
                 if self.world > 1:
-                    join_wgrad()
+                    join_streams(self.main_stream)
                     self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
             h.wait()
@@ -222,7 +231,7 @@ class FusedAdamW:
         self.scaler = LossScaler(dev) if compute_dtype == torch.float16 else None
 
     def step(self, lr=None):
-        join_wgrad()
+        join_streams(self.buckets.main_stream)  # every gradient-writing stream is done
         self.buckets.finish()
         for p in self.ungrouped:
             p.grad = None
@@ -239,9 +248,19 @@ class FusedAdamW:
         if not self.external_hyper:
             self.hyper[0].fill_(lr)
             self.hyper[1].fill_(float(self.step_count))
+        # parameters that got no gradient this step: torch.optim.AdamW skips them (no decay, no
+        # momentum step), so their value / moments are put back after the flat update
+        keep = [(g, off, k, g.flat[off:off + k].clone(), g.m[off:off + k].clone(), g.v[off:off + k].clone())
+                for g, off, k in self.buckets.unfired]
         for g in self.groups:
             K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, self.step_count,
                     gscale, g.shadow, hyper=self.hyper)
+        for g, off, k, p0, m0, v0 in keep:
+            g.flat[off:off + k].copy_(p0)
+            g.m[off:off + k].copy_(m0)
+            g.v[off:off + k].copy_(v0)
+            if g.shadow is not None:
+                g.shadow[off:off + k].copy_(p0)
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
@@ -323,6 +342,9 @@ class GraphedTrainStep:
     it (true of this package) and no host synchronisation inside the step."""
 
     def __init__(self, model, opt, rgb, depth, label, warmup=2):
+        if opt.scaler is not None:
+            raise ValueError("GraphedTrainStep: the fp16 loss scaler reads its overflow flag on the host "
+                             "(a step may be skipped); run the fp16 step eagerly")
         self.model, self.opt = model, opt
         self.inputs = (rgb, depth, label)
         side = torch.cuda.Stream(device=rgb.device)
@@ -362,6 +384,7 @@ def train_step(model, opt, rgb, depth, label, lr=None):
     RCCL all-reduce overlapping it), loss all-reduce, AdamW step. Returns the (device) mean loss."""
     loss, _ = model(rgb, depth, label)
     reduce_loss = all_reduce_mean(loss.detach(), opt.world)
+    opt.buckets.main_stream = torch.cuda.current_stream() if loss.is_cuda else None
     if opt.scaler is not None:  # scaler.scale(loss).backward()
         loss.backward(torch.full_like(loss, opt.scaler.scale))
     else:
