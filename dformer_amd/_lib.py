@@ -103,7 +103,7 @@ _SIGS = {
     "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
                                 P, P, c_long, P, c_long, P]),
     "dfm_convffn_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
-    "dfm_convffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
+    "dfm_convffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P,
                                 c_long, P, c_long, P, c_long, P, P, P, P]),
     "dfm_trace_set": (c_int, [c_int, ctypes.c_char_p]),
     "dfm_trace_take": (c_int, [ctypes.POINTER(c_void_p), c_int]),

@@ -1,54 +1,234 @@
 // Fused ConvFFN for gfx950 — DFormer's MLP (models/encoders/DFormer.py:48-67) inside the Block
 // residual (DFormer.py:173-179):
 //
-//   out = x + rowscale * ls * (fc2(GELU(DW3x3(h) + bpos + h)) + b2),   h = fc1(xn) + b1
+//   out = x + rowscale * ls * f,   f = fc2(GELU(DW3x3(h) + bpos + h)) + b2,   h = fc1(xn) + b1
 //
-// One workgroup owns a TH x TW tile of output pixels of one image. The tile's xn rows plus their
-// 1-pixel halo are staged in LDS once; the workgroup then walks the hidden channels in chunks of
-// HC: the chunk's W1 rows / W2 columns are staged in LDS, fc1 runs on tile + halo (MFMA,
-// h^T = W1c xn^T, so each lane holds 4 consecutive channels of one pixel) -> LDS; depthwise 3x3 +
-// bias + identity + GELU on 8-channel vectors from LDS (zero padding = zero rows for halo pixels
-// outside the image) -> LDS; fc2 of the chunk (MFMA, out^T += W2c g^T) accumulates in registers
-// over all chunks. The [P, r*C] hidden activation never leaves the CU: HBM sees xn and x read
-// once (+ the halo rows of neighbouring tiles, L2) and out / f written once.
+// A workgroup owns a TH x 16 tile of output pixels of one image (one 16-pixel MFMA tile per tile
+// row) and walks the hidden channels in chunks of HC = 32. The [P, hid] hidden activation never
+// leaves the CU in the forward pass:
+//   [A] fc1 on tile + 1-pixel halo: h^T = W1c xn^T (MFMA), + b1, zero outside the image -> LDS as
+//       fp32 "channel planes" hs[plane = ch / 8][pixel][ch % 8] (a plane stride = 4 mod 64 dwords
+//       makes the depthwise reads below bank-conflict free);
+//   [B] every lane computes the depthwise 3x3 (+ bias, identity folded into the centre tap) and GELU
+//       for exactly the 8 (bf16 / f16) hidden channels x 1 pixel that it must hold as the B operand of
+//       the fc2 MFMA (lane l: pixel l & 15, channels 8 (l >> 4) .. + 8), so g goes from VALU registers
+//       straight into v_mfma_f32_16x16x32 without an LDS round trip; out^T += W2c g^T accumulates in
+//       registers over all chunks.
+// The next chunk's weights are fetched into registers under [A] / [B] (and double-buffered in LDS
+// where it fits two workgroups per CU).
 //
-// Backward (convffn_bwd_kernel, below) recomputes h / hpre per tile from xn.
+// Backward (one 512-thread workgroup per CU, TH = 8): per chunk [A] recomputes h on tile + 2-pixel
+// halo and dg = df W2c on tile + 1 halo (MFMA), [B] hpre = DW3(h) + bpos + h, g = GELU(hpre) (tile
+// pixels -> HBM for the fc2 weight-gradient GEMM), dhpre = dg GELU'(hpre) (in LDS), [C] dh = DW3^T
+// (dhpre) + dhpre on the tile straight into the B fragments of dxn^T += W1c^T dh^T (MFMA) and to HBM
+// (fc1 weight-gradient GEMM); the depthwise weight / bias gradient partials of the tile ride along
+// in [B]. Weights are read in their natural layouts (w1 [hid][C], w2 [C][hid]) and transposed while
+// staged into LDS.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
 namespace {
 
-constexpr int NTH = 256;  // threads per workgroup (4 waves)
+constexpr int HC = 32;  // hidden channels per chunk
+constexpr int TW = 16;  // tile width = one 16-pixel MFMA tile per tile row
 
-// ---- MFMA fragment helpers, both operands "k-contiguous per row": lane l holds
-// A[row l&15][k0 + KL*(l>>4) .. +KL] and B[k0 + KL*(l>>4) .. +KL][col l&15]; C/D: col = l&15,
-// rows 4*(l>>4) .. +4 (dtype-independent on gfx950).
-template <typename T> struct MM;
-template <> struct MM<bf16_t> {
-  static constexpr int KS = 32, KL = 8;
+// ---- MFMA operand traits: 16-bit types use v_mfma_f32_16x16x32_{bf16,f16} (lane l holds A[l&15]
+// [8(l>>4) .. +8], B[8(l>>4) .. +8][l&15]); float32 (the parity path) v_mfma_f32_16x16x4_f32 (lane l
+// holds A[l&15][l>>4], B[l>>4][l&15]). C/D: lane l holds rows 4(l>>4) .. +4 of column l&15.
+template <typename T> struct FT {
   using frag = bf16x8_t;
-  static DFM_INLINE frag zero() { return __builtin_bit_cast(frag, make_uint4(0, 0, 0, 0)); }
-  static DFM_INLINE frag load(const bf16_t* p) { return __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(p)); }
-  static DFM_INLINE float4_t mma(float4_t c, frag a, frag b) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  static constexpr int KS = 32;
+  static constexpr int PAD = 16;  // row pitch = K + 16 elements (= 16 mod 32): conflict-free b128 fragments
+  static DFM_INLINE frag ld(const T* row, int k0, int lane) {
+    return __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(row + k0 + 8 * (lane >> 4)));
+  }
+  static DFM_INLINE float4_t mma(frag a, frag b, float4_t c) { return mma16<T>(a, b, c); }
+};
+template <> struct FT<float> {
+  using frag = float;
+  static constexpr int KS = 4;
+  static constexpr int PAD = 4;
+  static DFM_INLINE frag ld(const float* row, int k0, int lane) { return row[k0 + (lane >> 4)]; }
+  static DFM_INLINE float4_t mma(frag a, frag b, float4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
 };
-template <> struct MM<float> {
-  static constexpr int KS = 4, KL = 1;
-  using frag = float;
-  static DFM_INLINE frag zero() { return 0.f; }
-  static DFM_INLINE frag load(const float* p) { return *p; }
-  static DFM_INLINE float4_t mma(float4_t c, frag a, frag b) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// The hidden channel m (0..7) of a lane's 8 in the MFMA B-operand layout of a 32-channel chunk:
+// 16-bit: 8 consecutive channels per lane quarter; float32: k-step m, channel 4 m + quarter.
+template <typename T> DFM_INLINE int lane_ch(int kq, int m) { return sizeof(T) == 2 ? 8 * kq + m : 4 * m + kq; }
+
+// 8 floats -> B fragment(s): 16-bit: one 8 x 16-bit vector; float32: element m is k-step m's operand
+template <typename T> DFM_INLINE typename FT<T>::frag to_frag(const float* v, int m) {
+  if constexpr (sizeof(T) == 2) return pack16x8<T>(v);
+  else return v[m];
+}
+
+// fp32 channel planes: plane p holds channels 8p .. 8p + 7 of every pixel row (32 bytes per row).
+// Plane stride = rows * 8 + RES floats. RES = 4: the lane groups of a ds_read_b128 in the MFMA
+// operand layout (16 consecutive pixels x 4 planes) hit 16 distinct 4-bank slots. RES = 16: the
+// 32-lane groups of a ds_read_b64 over (2 consecutive pixels x 16 channel pairs) hit 32 distinct
+// 2-bank slots (the backward's per-channel-pair depthwise phase).
+template <int ROWS, int RES = 4> struct Planes {
+  static constexpr int PS = ROWS * 8 + RES;  // ROWS * 8 is a multiple of 64 (ROWS % 8 == 0)
+  static constexpr int FLOATS = 4 * PS;  // HC / 8 planes
+  static DFM_INLINE int at(int row, int ch) { return (ch >> 3) * PS + row * 8 + (ch & 7); }
 };
 
-// 4 consecutive values -> LDS (8 bytes bf16 / 16 bytes f32)
-DFM_INLINE void st4(bf16_t* p, const float* v) {
-  const uint32_t lo = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  const uint32_t hi = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+// 8 consecutive floats of channels ch .. ch + 7 (ch % 8 == 0) of one plane row
+DFM_INLINE void ld8p(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
-DFM_INLINE void st4(float* p, const float* v) { *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]); }
+
+// The lane's 8 channels of one pixel row of a plane image (16-bit: one contiguous group; fp32: strided)
+template <typename T, int ROWS>
+DFM_INLINE void ld_lane8(const float* img, int row, int kq, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    ld8p(img + Planes<ROWS>::at(row, 8 * kq), v);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = img[Planes<ROWS>::at(row, lane_ch<T>(kq, m))];
+  }
+}
+
+// 4 consecutive elements (8 bytes for 16-bit types, 16 for float32) <-> floats
+template <typename T> DFM_INLINE void ld4(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    const T* e = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = Num<T>::to_f(e[r]);
+  } else {
+    const float4 u = *reinterpret_cast<const float4*>(p);
+    v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+  }
+}
+template <typename T> DFM_INLINE void st4g(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    T e[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) e[r] = Num<T>::from_f(v[r]);
+    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<const uint2*>(e);
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// Per-chunk fp32 parameters in LDS: pb[0, HC) = b1, pb[HC, 2 HC) = bpos, pb[2 HC + t HC + ch] = tap t
+// of channel ch (tap-major), with the identity of `DW3(h) + h` folded into the centre tap (t = 4).
+constexpr int PB = 11 * HC;
+
+template <typename T> DFM_INLINE void ld_lane8_par(const float* pb, int kq, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    ld8p(pb + 8 * kq, v);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) v[m] = pb[lane_ch<T>(kq, m)];
+  }
+}
+
+// Register-staged prefetch of one chunk of weights / parameters (issued under the previous chunk's
+// work, stored to LDS after it). Rows beyond C are zero-filled.
+//   W1c = w1[c0 .. c0 + HC][0 .. C)        -> dst1[j][c]   (pitch XP)
+//   W2c = w2[0 .. C)[c0 .. c0 + HC)        -> dst2[c][j]   (pitch WP)
+//   b1, bpos, wpos (+1 on the centre tap)  -> pb
+template <typename T, int CT, int NT>
+struct ChunkPrefetch {
+  static constexpr int V = 16 / sizeof(T);                 // elements per 16-byte vector
+  static constexpr int N1 = HC * CT / V, N2 = CT * HC / V;  // vectors of W1c / W2c
+  static constexpr int R1 = (N1 + NT - 1) / NT, R2 = (N2 + NT - 1) / NT;
+  static constexpr int NP = PB;                            // parameter floats
+  static constexpr int RP = (NP + NT - 1) / NT;
+  uint4 w1[R1], w2[R2];
+  float par[RP];
+
+  DFM_INLINE void load(const T* __restrict__ gw1, const T* __restrict__ gw2, const float* __restrict__ b1,
+                       const float* __restrict__ bpos, const float* __restrict__ wpos, int C, int hid, int c0) {
+#pragma unroll
+    for (int i = 0; i < R1; ++i) {
+      const int v = threadIdx.x + i * NT;
+      const int j = v / (CT / V), c = (v % (CT / V)) * V;
+      w1[i] = (v < N1 && c < C) ? *reinterpret_cast<const uint4*>(gw1 + (long)(c0 + j) * C + c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < R2; ++i) {
+      const int v = threadIdx.x + i * NT;
+      const int c = v / (HC / V), j = (v % (HC / V)) * V;
+      w2[i] = (v < N2 && c < C) ? *reinterpret_cast<const uint4*>(gw2 + (long)c * hid + c0 + j) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int e = threadIdx.x + i * NT;
+      float v = 0.f;
+      if (e < HC) v = b1[c0 + e];
+      else if (e < 2 * HC) v = bpos[c0 + e - HC];
+      else if (e < NP) {
+        const int t = (e - 2 * HC) / HC, ch = (e - 2 * HC) % HC;
+        v = wpos[(long)(c0 + ch) * 9 + t] + (t == 4 ? 1.0f : 0.0f);
+      }
+      par[i] = v;
+    }
+  }
+
+  template <int XP, int WP>
+  DFM_INLINE void store(T* dst1, T* dst2, float* pb) const {
+#pragma unroll
+    for (int i = 0; i < R1; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= N1) break;
+      const int j = v / (CT / V), c = (v % (CT / V)) * V;
+      *reinterpret_cast<uint4*>(dst1 + j * XP + c) = w1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < R2; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= N2) break;
+      const int c = v / (HC / V), j = (v % (HC / V)) * V;
+      *reinterpret_cast<uint4*>(dst2 + c * WP + j) = w2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int e = threadIdx.x + i * NT;
+      if (e < NP) pb[e] = par[i];
+    }
+  }
+};
+
+// Rows x C of NHWC activations (row r of the halo image = pixel (y0 + r / rw, x0 + r % rw) of image b,
+// zero outside the image or past `rows`) -> LDS with pitch XP; columns C .. CT zero-filled.
+template <typename T, int CT, int XP, int NT>
+DFM_INLINE void stage_halo(T* dst, const T* __restrict__ src, long ld, int rows, int rows_pad, int rw, int b, int y0,
+                           int x0, int H, int W, int C) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int VPR = CT / V;
+  for (int i = threadIdx.x; i < rows_pad * VPR; i += NT) {
+    const int r = i / VPR, c = (i % VPR) * V;
+    const int yy = y0 + r / rw, xx = x0 + r % rw;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < rows && c < C && yy >= 0 && yy < H && xx >= 0 && xx < W)
+      v = *reinterpret_cast<const uint4*>(src + ((long)(b * H + yy) * W + xx) * ld + c);
+    *reinterpret_cast<uint4*>(dst + r * XP + c) = v;
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not its global
+// loads. __syncthreads()' fence drains vmcnt, which would wait for the next chunk's weight prefetch
+// at every barrier and expose its L2 round trip once per chunk; the inline asm (memory clobber) also
+// keeps the compiler from moving LDS accesses across it.
+DFM_INLINE void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// XCD-aware tile order: neighbouring tiles (which share halo rows) run on one XCD's L2.
+DFM_INLINE int xcd_tile(int id, int n) {
+  const int xcd = id & 7, q8 = n >> 3, r8 = n & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+}
 
 struct FfnArgs {
   int B, H, W, C, hid;
@@ -57,11 +237,11 @@ struct FfnArgs {
   long ldxn;
   const void* x;
   long ldx;
-  const void* w1;  // [hid][C] compute dtype
+  const void* w1;  // [hid][C]
   const float* b1;
   const float* wpos;  // [hid][9]
   const float* bpos;
-  const void* w2;  // [C][hid] compute dtype
+  const void* w2;  // [C][hid]
   const float* b2;
   const float* ls;
   const float* rowscale;  // [B] or null
@@ -71,301 +251,189 @@ struct FfnArgs {
   long ldf;
 };
 
-// LDS pitch (elements) of a row of `n` elements: +16 bytes, so the 8-byte MFMA-layout writes of 16
-// consecutive rows and the 16-byte fragment / vector reads spread over the banks
-template <typename T> constexpr int lpitch(int n) { return n + 16 / (int)sizeof(T); }
-
-// Copy rows x cols (cols % (16/sizeof(T)) == 0) into LDS with pitch lp; rowptr(r) == nullptr -> zeros.
-template <typename T, int NT, typename F>
-DFM_INLINE void stage_rows(T* lds, int lp, int rows, int cols, F rowptr) {
-  constexpr int V = 16 / sizeof(T);
-  const int vpr = cols / V;
-  for (int i = threadIdx.x; i < rows * vpr; i += NT) {
-    const int r = i / vpr, c = (i - r * vpr) * V;
-    const T* src = rowptr(r);
-    const uint4 v = src ? *reinterpret_cast<const uint4*>(src + c) : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(lds + r * lp + c) = v;
-  }
-}
-
-// MFMA over k in [0, K) with A rows / B rows k-contiguous in LDS (pitch lpa / lpb):
-// acc[it] += A[i0 + 16 it + l&15][k] B[j0 + l&15][k]  (C/D: rows i, cols j)
-template <typename T, int NI>
-DFM_INLINE void mma_rows(float4_t (&acc)[NI], const T* A, int lpa, const T* B, int lpb, int K, int lane) {
-  using M = MM<T>;
-  const int kq = M::KL * (lane >> 4);
-  const T* brow = B + (lane & 15) * lpb;
-  const T* arow = A + (lane & 15) * lpa;
-  for (int k0 = 0; k0 < K; k0 += M::KS) {
-    const int k = k0 + kq;
-    const bool ok = k < K;
-    const typename M::frag b = ok ? M::load(brow + k) : M::zero();
-#pragma unroll
-    for (int it = 0; it < NI; ++it) {
-      const typename M::frag av = ok ? M::load(arow + it * 16 * lpa + k) : M::zero();
-      acc[it] = M::mma(acc[it], av, b);
-    }
-  }
-}
-
-// A rows x cols block (cols % (16/sizeof(T)) == 0, row stride ld in global) split over NT threads as
-// 16-byte vectors: load() issues the global loads into registers, store() writes them to LDS later,
-// so a chunk's operands travel while the previous chunk computes.
-template <typename T, int NT, int NV>
-struct Prefetch2D {
-  static constexpr int V = 16 / sizeof(T);
-  uint4 v[NV];
-  DFM_INLINE void load(const T* src, long ld, int rows, int cols) {
-    const int vpr = cols / V;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int i = threadIdx.x + j * NT;
-      if (i < rows * vpr) {
-        const int r = i / vpr, c = (i - r * vpr) * V;
-        v[j] = *reinterpret_cast<const uint4*>(src + r * ld + c);
-      }
-    }
-  }
-  DFM_INLINE void store(T* lds, int lp, int rows, int cols) const {
-    const int vpr = cols / V;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int i = threadIdx.x + j * NT;
-      if (i < rows * vpr) {
-        const int r = i / vpr, c = (i - r * vpr) * V;
-        *reinterpret_cast<uint4*>(lds + r * lp + c) = v[j];
-      }
-    }
-  }
-};
-
-// Per-chunk fp32 parameters of HC hidden channels starting at c0, in LDS as
-//   pb[0, HC) = b1, pb[HC, 2 HC) = bpos, pb[2 HC + t HC + ch] = wpos[c0 + ch][t] (tap-major).
-template <int HC, int NT>
-struct ParamPrefetch {
-  static constexpr int N4 = (2 * HC + 9 * HC) / 4;  // float4 units: b1, bpos, wpos[HC][9]
-  static_assert(N4 <= NT, "one float4 per thread");
-  float4 v;
-  DFM_INLINE void load(const float* b1, const float* bpos, const float* wpos, int c0) {
-    const int i = threadIdx.x;
-    if (i < HC / 4) v = reinterpret_cast<const float4*>(b1 + c0)[i];
-    else if (i < HC / 2) v = reinterpret_cast<const float4*>(bpos + c0)[i - HC / 4];
-    else if (i < N4) v = reinterpret_cast<const float4*>(wpos + (long)c0 * 9)[i - HC / 2];
-  }
-  DFM_INLINE void store(float* pb) const {
-    const int i = threadIdx.x;
-    if (i < HC / 2) {
-      reinterpret_cast<float4*>(pb)[i] = v;
-    } else if (i < N4) {
-      const float f[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int idx = (i - HC / 2) * 4 + e, ch = idx / 9, t = idx - ch * 9;
-        pb[2 * HC + t * HC + ch] = f[e];
-      }
-    }
-  }
-};
-
-// 3x3 depthwise + bias + identity on 8 channels, taps from the LDS parameter block: img points at
-// channel 0 of the group in an LDS image with pitch LP and HW pixels per image row; base = the
-// top-left neighbour; pw = &pb[2 HC + ch0] (tap t at pw[t * HC]), pbias = &pb[HC + ch0] or null.
-template <typename T, int LP, int HW, int HC, bool FLIP>
-DFM_INLINE void dw_unit_lds(const T* img, int base, const float* pw, const float* pbias, float (&sv)[8]) {
-  float cv[8];
-  ld8<T>(img + (base + HW + 1) * LP, cv);
-  if (pbias) {
-    float bv[8];
-    ld8<float>(pbias, bv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sv[e] = bv[e] + cv[e];
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sv[e] = cv[e];
-  }
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    float nv[8], wv[8];
-    const int tt = FLIP ? 8 - t : t;  // FLIP: the transposed conv (backward-data) of the same taps
-    ld8<T>(img + (base + (t / 3) * HW + t % 3) * LP, nv);
-    ld8<float>(pw + tt * HC, wv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) sv[e] = fmaf(wv[e], nv[e], sv[e]);
-  }
-}
-
-template <typename T, int NTHR>
-struct FfnBase {
-  static constexpr int NT = NTHR;
-  static constexpr int NWV = NTHR / 64;
-};
-
-template <typename T, int CT, int TH, int TW, int HC, int NTHR>
-struct FfnGeom : FfnBase<T, NTHR> {
-  static constexpr int HW2 = TW + 2;
-  static constexpr int NH = (TH + 2) * (TW + 2);  // tile + 1-pixel halo
-  static constexpr int NHP = (NH + 15) / 16 * 16;
-  static constexpr int TP = TH * TW;
-  static constexpr int XP = lpitch<T>(CT);  // xn / W1 row pitch
-  static constexpr int HP = lpitch<T>(HC);  // h / g / W2-chunk row pitch
-  static constexpr int SP = CT + 4;         // fp32 epilogue staging pitch
-  static constexpr size_t o_w1 = (size_t)NHP * XP * sizeof(T);
-  static constexpr size_t o_w2 = o_w1 + (size_t)HC * XP * sizeof(T);
-  static constexpr size_t o_h = o_w2 + (size_t)CT * HP * sizeof(T);
-  static constexpr size_t o_g = o_h + (size_t)NHP * HP * sizeof(T);
-  static constexpr size_t o_p = o_g + (size_t)TP * HP * sizeof(T);
-  static constexpr size_t lds_main = o_p + (size_t)11 * HC * sizeof(float);
-  static constexpr size_t lds_stage = (size_t)TP * SP * sizeof(float);
-  static constexpr size_t lds = lds_main > lds_stage ? lds_main : lds_stage;
-};
-
 // ---------------------------------------------------------------- forward
-template <typename T, int CT, int TH, int TW, int HC, int NTHR>
-__global__ __launch_bounds__(NTHR) void convffn_fwd_kernel(FfnArgs a) {
-  using G = FfnGeom<T, CT, TH, TW, HC, NTHR>;
-  constexpr int NT = G::NT, NWV = G::NWV, TP = G::TP, XP = G::XP, HP = G::HP;
-  constexpr int PT = TP / 16;                    // pixel tiles of fc2
-  constexpr int PTW = (PT + NWV - 1) / NWV;      // per wave
-  constexpr int OT = CT / 16;                    // output-channel tiles of fc2
-  constexpr int G8 = HC / 8;                     // 8-channel groups of the depthwise stage
-  constexpr int NT1 = G::NHP / 16;               // fc1 pixel tiles (tile + halo)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* xs = reinterpret_cast<T*>(smem);            // [NHP][XP] xn on tile + halo
-  T* w1s = reinterpret_cast<T*>(smem + G::o_w1);  // [HC][XP] W1 rows of the chunk
-  T* w2s = reinterpret_cast<T*>(smem + G::o_w2);  // [CT][HP] W2[:, chunk]
-  T* hs = reinterpret_cast<T*>(smem + G::o_h);   // [NHP][HP] h chunk
-  T* gs = reinterpret_cast<T*>(smem + G::o_g);   // [TP][HP] GELU output chunk
+template <typename T, int CT, int TH, bool DB>
+struct FwdGeom {
+  static constexpr int NT = 256, NW = 4;  // two workgroups per CU
+  static constexpr int HW2 = TW + 2;
+  static constexpr int NH = (TH + 2) * HW2;
+  static constexpr int NHT = (NH + 15) / 16;  // 16-pixel tiles of tile + halo
+  static constexpr int NHP = NHT * 16;
+  static constexpr int XP = CT + FT<T>::PAD;  // xs / W1c row pitch
+  static constexpr int WP = HC + FT<T>::PAD;  // W2c row pitch
+  static constexpr int NB = DB ? 2 : 1;
+  static constexpr size_t o_w1 = (size_t)NHP * XP * sizeof(T);
+  static constexpr size_t W1B = (size_t)HC * XP * sizeof(T), W2B = (size_t)CT * WP * sizeof(T), PBB = PB * 4;
+  static constexpr size_t o_w2 = o_w1 + NB * W1B;
+  static constexpr size_t o_pb = o_w2 + NB * W2B;
+  static constexpr size_t o_hs = o_pb + NB * PBB;
+  static constexpr size_t lds = o_hs + (size_t)Planes<NHP>::FLOATS * 4;
+};
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, tid = threadIdx.x;
-  const int tile = blockIdx.x;
+template <typename T, int CT, int TH, bool DB>
+__global__ __launch_bounds__(256) void convffn_fwd_kernel(FfnArgs a) {
+  using G = FwdGeom<T, CT, TH, DB>;
+  using F = FT<T>;
+  using HP = Planes<G::NHP>;
+  constexpr int NT = G::NT, NW = G::NW, XP = G::XP, WP = G::WP;
+  constexpr int OT = CT / 16;           // fc2 output-channel tiles
+  constexpr int PTW = 2;                // tile rows per wave (2 w, 2 w + 1)
+  static_assert(TH == 2 * NW, "each wave owns two adjacent tile rows");
+  constexpr int KC = CT / F::KS;        // fc1 k-steps
+  constexpr int K2 = HC / F::KS;        // fc2 k-steps
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* xs = reinterpret_cast<T*>(smem);
+  float* hs = reinterpret_cast<float*>(smem + G::o_hs);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nt = a.B * a.tiles_y * a.tiles_x;
+  const int tile = xcd_tile(blockIdx.x, nt);
   const int b = tile / (a.tiles_y * a.tiles_x);
   const int ty = (tile / a.tiles_x) % a.tiles_y, tx = tile % a.tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
-  const int C = a.C, hid = a.hid;
-  const T* xn = (const T*)a.xn;
-  const T* w1 = (const T*)a.w1;
-  const T* w2 = (const T*)a.w2;
-  auto inside = [&](int yy, int xx) { return yy >= 0 && yy < a.H && xx >= 0 && xx < a.W; };
-  auto halo_ok = [&](int q) {
-    const int yy = y0 - 1 + q / G::HW2, xx = x0 - 1 + q % G::HW2;
-    return q < G::NH && inside(yy, xx);
-  };
+  const int C = a.C, hid = a.hid, H = a.H, W = a.W;
+  const int px = lane & 15, kq = lane >> 4;
 
-  float* pb = reinterpret_cast<float*>(smem + G::o_p);  // [11][HC] b1 | bpos | wpos (tap-major)
-  constexpr int VEC = 16 / sizeof(T);
-  Prefetch2D<T, NT, (HC * CT / VEC + NT - 1) / NT> pw1, pw2;
-  ParamPrefetch<HC, NT> ppar;
-  auto fetch = [&](int c) {
-    pw1.load(w1 + (long)c * C, C, HC, C);
-    pw2.load(w2 + c, hid, C, HC);
-    ppar.load(a.b1, a.bpos, a.wpos, c);
-  };
-  auto put = [&]() {
-    pw1.store(w1s, XP, HC, C);
-    pw2.store(w2s, HP, C, HC);
-    ppar.store(pb);
-  };
-  fetch(0);
-  stage_rows<T, NT>(xs, XP, G::NHP, C, [&](int q) -> const T* {
-    const int yy = y0 - 1 + q / G::HW2, xx = x0 - 1 + q % G::HW2;
-    return (q < G::NH && inside(yy, xx)) ? xn + ((long)(b * a.H + yy) * a.W + xx) * a.ldxn : nullptr;
-  });
-  put();
-
+  ChunkPrefetch<T, CT, NT> pf;
+  pf.load((const T*)a.w1, (const T*)a.w2, a.b1, a.bpos, a.wpos, C, hid, 0);
+  stage_halo<T, CT, XP, NT>(xs, (const T*)a.xn, a.ldxn, G::NH, G::NHP, G::HW2, b, y0 - 1, x0 - 1, H, W, C);
+  pf.template store<XP, WP>(reinterpret_cast<T*>(smem + G::o_w1), reinterpret_cast<T*>(smem + G::o_w2),
+                                   reinterpret_cast<float*>(smem + G::o_pb));
   float4_t acc[PTW][OT];
 #pragma unroll
   for (int i = 0; i < PTW; ++i)
 #pragma unroll
-    for (int j = 0; j < OT; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-  const int g = tid % G8;
+    for (int o = 0; o < OT; ++o) acc[i][o] = float4_t{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
-  for (int c0 = 0; c0 < hid; c0 += HC) {
-    const bool more = c0 + HC < hid;
-    if (more) fetch(c0 + HC);  // next chunk's operands in flight under this chunk's work
-    // ---- fc1 on tile + halo: h^T[hidden][pixel] = W1c xn^T -> hs[pixel][hidden]
-#pragma unroll 1
-    for (int jt = wid; jt < NT1; jt += NWV) {
-      float4_t h[HC / 16];
+  const int nchunk = hid / HC;
+  int buf = 0;
+  for (int ci = 0; ci < nchunk; ++ci) {
+    const T* w1s = reinterpret_cast<const T*>(smem + G::o_w1 + buf * G::W1B);
+    const T* w2s = reinterpret_cast<const T*>(smem + G::o_w2 + buf * G::W2B);
+    const float* pb = reinterpret_cast<const float*>(smem + G::o_pb + buf * G::PBB);
+    const bool more = ci + 1 < nchunk;
+    if (more) pf.load((const T*)a.w1, (const T*)a.w2, a.b1, a.bpos, a.wpos, C, hid, (ci + 1) * HC);
+    // ---- [A] fc1 on tile + halo: h^T[hidden 16][pixel 16] = W1c xn^T, + b1, zero outside the image
+    {
+      typename F::frag aw[2][KC];
 #pragma unroll
-      for (int it = 0; it < HC / 16; ++it) h[it] = float4_t{0.f, 0.f, 0.f, 0.f};
-      mma_rows<T, HC / 16>(h, w1s, XP, xs + jt * 16 * XP, XP, C, lane);
-      const int q = jt * 16 + (lane & 15);
-      const bool val = halo_ok(q);
+      for (int it = 0; it < 2; ++it)
 #pragma unroll
-      for (int it = 0; it < HC / 16; ++it) {
-        const int ch = it * 16 + 4 * (lane >> 4);
-        const float4 bb = *reinterpret_cast<const float4*>(pb + ch);
-        const float v[4] = {val ? h[it][0] + bb.x : 0.f, val ? h[it][1] + bb.y : 0.f, val ? h[it][2] + bb.z : 0.f,
-                            val ? h[it][3] + bb.w : 0.f};
-        st4(hs + q * HP + ch, v);
+        for (int ks = 0; ks < KC; ++ks) aw[it][ks] = F::ld(w1s + (it * 16 + px) * XP, ks * F::KS, lane);
+      float4 bb[2];
+#pragma unroll
+      for (int it = 0; it < 2; ++it) bb[it] = *reinterpret_cast<const float4*>(pb + it * 16 + 4 * kq);
+      for (int jt = wid; jt < G::NHT; jt += NW) {
+        float4_t h[2] = {float4_t{0.f, 0.f, 0.f, 0.f}, float4_t{0.f, 0.f, 0.f, 0.f}};
+        const T* xrow = xs + (jt * 16 + px) * XP;
+#pragma unroll
+        for (int ks = 0; ks < KC; ++ks) {
+          const typename F::frag xb = F::ld(xrow, ks * F::KS, lane);
+#pragma unroll
+          for (int it = 0; it < 2; ++it) h[it] = F::mma(aw[it][ks], xb, h[it]);
+        }
+        const int q = jt * 16 + px;
+        const int yy = y0 - 1 + q / G::HW2, xx = x0 - 1 + q % G::HW2;
+        const bool ok = q < G::NH && yy >= 0 && yy < H && xx >= 0 && xx < W;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const float4 v = ok ? make_float4(h[it][0] + bb[it].x, h[it][1] + bb[it].y, h[it][2] + bb[it].z,
+                                            h[it][3] + bb[it].w)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(hs + HP::at(q, it * 16 + 4 * kq)) = v;
+        }
       }
     }
-    __syncthreads();
-    // ---- depthwise 3x3 + bias + identity + GELU: hs -> gs, one (pixel, 8-channel) unit at a time
-#pragma unroll 1
-    for (int u = tid; u < TP * G8; u += NT) {
-      const int p = u / G8;
-      float sv[8];
-      dw_unit_lds<T, HP, G::HW2, HC, false>(hs + g * 8, (p / TW) * G::HW2 + p % TW, pb + 2 * HC + g * 8,
-                                             pb + HC + g * 8, sv);
+    lds_sync();  // hs complete
+    // ---- [B] depthwise 3x3 (+ bias + identity) + GELU into the fc2 B fragments; out^T += W2c g^T.
+    //          Wave w owns the adjacent tile rows 2w, 2w + 1: the 4 halo rows they touch are read once
+    //          (12 tap positions for 2 output rows instead of 18); taps and bias sit in registers.
+    {
+      float wt[9][8], s0[8], s1[8];
+      ld_lane8_par<T>(pb + HC, kq, s0);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) sv[e] = gelu_f(sv[e]);
-      st8<T>(gs + p * HP + g * 8, sv);
-    }
-    __syncthreads();
-    // ---- fc2 chunk: out^T[c][p] += W2c[c][k] g^T[k][p]
+      for (int t = 0; t < 9; ++t) ld_lane8_par<T>(pb + 2 * HC + t * HC, kq, wt[t]);
 #pragma unroll
-    for (int i = 0; i < PTW; ++i) {
-      const int pj = wid + i * NWV;
-      if (pj < PT) mma_rows<T, OT>(acc[i], w2s, HP, gs + pj * 16 * HP, HP, HC, lane);
+      for (int m = 0; m < 8; ++m) s1[m] = s0[m];
+      typename F::frag a2[OT][K2];
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int ks = 0; ks < K2; ++ks) a2[o][ks] = F::ld(w2s + (o * 16 + px) * WP, ks * F::KS, lane);
+      const int pt0 = 2 * wid;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          float hv[8];
+          ld_lane8<T, G::NHP>(hs, (pt0 + r) * G::HW2 + px + dx, kq, hv);
+          if (r <= 2) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) s0[m] = fmaf(wt[r * 3 + dx][m], hv[m], s0[m]);
+          }
+          if (r >= 1) {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) s1[m] = fmaf(wt[(r - 1) * 3 + dx][m], hv[m], s1[m]);
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        s0[m] = gelu_f(s0[m]);
+        s1[m] = gelu_f(s1[m]);
+      }
+#pragma unroll
+      for (int ks = 0; ks < K2; ++ks) {
+        const typename F::frag g0 = to_frag<T>(s0, ks), g1 = to_frag<T>(s1, ks);
+#pragma unroll
+        for (int o = 0; o < OT; ++o) {
+          acc[0][o] = F::mma(a2[o][ks], g0, acc[0][o]);
+          acc[1][o] = F::mma(a2[o][ks], g1, acc[1][o]);
+        }
+      }
     }
-    if (more) {
-      __syncthreads();  // this chunk's reads of w1s / w2s / pb are done
-      put();
-      __syncthreads();
+    // the next chunk's weights (requested at this chunk's start, landed under [A] / [B]) go to the
+    // other buffer, which nobody has read since the previous chunk-end barrier
+    if (DB && more)
+      pf.template store<XP, WP>(reinterpret_cast<T*>(smem + G::o_w1 + (buf ^ 1) * G::W1B),
+                                       reinterpret_cast<T*>(smem + G::o_w2 + (buf ^ 1) * G::W2B),
+                                       reinterpret_cast<float*>(smem + G::o_pb + (buf ^ 1) * G::PBB));
+    lds_sync();  // [B] done with hs, w2s, pb
+    if (!DB && more) {
+      pf.template store<XP, WP>(reinterpret_cast<T*>(smem + G::o_w1), reinterpret_cast<T*>(smem + G::o_w2),
+                                       reinterpret_cast<float*>(smem + G::o_pb));
+      lds_sync();
     }
+    if (DB) buf ^= 1;
   }
-  __syncthreads();  // chunk images dead: the fp32 staging tile reuses the LDS
-  float* st = reinterpret_cast<float*>(smem);
+  // ---- epilogue: lane holds out[pixel px of tile row pt][channels 16 o + 4 kq .. + 4]
+  const float rs = a.rowscale ? a.rowscale[b] : 1.f;
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pj = wid + i * NWV;
-    if (pj >= PT) break;
+    const int pt = 2 * wid + i;
+    const int yy = y0 + pt, xx = x0 + px;
+    if (yy >= H || xx >= W) continue;
+    const long row = (long)(b * H + yy) * W + xx;
 #pragma unroll
-    for (int ot = 0; ot < OT; ++ot) {
-      const float v[4] = {acc[i][ot][0], acc[i][ot][1], acc[i][ot][2], acc[i][ot][3]};
-      st4(st + (pj * 16 + (lane & 15)) * G::SP + ot * 16 + 4 * (lane >> 4), v);
+    for (int o = 0; o < OT; ++o) {
+      const int c = o * 16 + 4 * kq;
+      if (c >= C) break;
+      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + c);
+      const float4 ll = *reinterpret_cast<const float4*>(a.ls + c);
+      const float fv[4] = {acc[i][o][0] + bb.x, acc[i][o][1] + bb.y, acc[i][o][2] + bb.z, acc[i][o][3] + bb.w};
+      const float lv[4] = {ll.x, ll.y, ll.z, ll.w};
+      float xv[4], ov[4];
+      ld4<T>((const T*)a.x + row * a.ldx + c, xv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ov[r] = xv[r] + lv[r] * rs * fv[r];
+      st4g<T>((T*)a.f + row * a.ldf + c, fv);
+      st4g<T>((T*)a.out + row * a.ldout + c, ov);
     }
-  }
-  __syncthreads();
-  const float rs = a.rowscale ? a.rowscale[b] : 1.f;
-  const int CG = C / 8;
-  for (int u = tid; u < TP * CG; u += NT) {
-    const int p = u / CG, c = (u % CG) * 8;
-    const int yy = y0 + p / TW, xx = x0 + p % TW;
-    if (!inside(yy, xx)) continue;
-    const long row = (long)(b * a.H + yy) * a.W + xx;
-    float v[8], xv[8], o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = st[p * G::SP + c + e] + a.b2[c + e];
-    st8<T>((T*)a.f + row * a.ldf + c, v);
-    ld8<T>((const T*)a.x + row * a.ldx + c, xv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = xv[e] + a.ls[c + e] * rs * v[e];
-    st8<T>((T*)a.out + row * a.ldout + c, o);
   }
 }
 
 // ---------------------------------------------------------------- backward
-// Given df = dout * ls * rowscale (the residual's chain rule, dfm_residual_bwd) the tile stages xn
-// on tile + 2-pixel halo and df on tile + 1-pixel halo in LDS, then per hidden chunk recomputes h
-// (fc1, MFMA) on tile + 2 halo, forms dg = df W2 on tile + 1 halo (MFMA), hpre = DW3(h) + bpos + h
-// and g = GELU(hpre) (VALU), dhpre = dg * GELU'(hpre), dh = DW3^T(dhpre) + dhpre on the tile,
-// dxn += dh W1 (MFMA, accumulated over the chunks) and the depthwise weight / bias gradient
-// partials sum_p dhpre[p] h[p + tap]. It writes g and dh ([P, hid], the inputs of the fc2 / fc1
-// weight-gradient GEMMs), dxn ([P, C]) and one [hid][10] partial per workgroup; hpre / dhpre never
-// reach HBM.
 struct FfnBwdArgs {
   int B, H, W, C, hid;
   int tiles_y, tiles_x;
@@ -373,287 +441,456 @@ struct FfnBwdArgs {
   long ldxn;
   const void* df;
   long lddf;
-  const void* w1;   // [hid][C]
+  const void* w1;  // [hid][C]
   const float* b1;
   const float* wpos;
   const float* bpos;
-  const void* w2t;  // [hid][C]  (fc2 weight, transposed)
-  const void* w1t;  // [C][hid]  (fc1 weight, transposed)
-  void* g;          // [P][ldg] GELU output
+  const void* w2;  // [C][hid]
+  void* g;         // [P][ldg] GELU output
   long ldg;
-  void* dh;         // [P][lddh] fc1-output gradient
+  void* dh;        // [P][lddh] fc1-output gradient
   long lddh;
-  void* dxn;        // [P][lddxn]
+  void* dxn;       // [P][lddxn]
   long lddxn;
-  float* part;      // [nblk][hid * 10] depthwise weight (9) + bias (1) gradient partials
+  float* part;     // [tiles][hid * 10] depthwise weight (9) + bias (1) gradient partials
+  int skip;        // profiling only (DFM_FFN_SKIP): bit i skips phase [A], [B], [C], the reduction
+  long long* stamp;  // profiling only (DFM_FFN_STAMP): s_memtime at the phase boundaries of workgroup 0
 };
 
-template <typename T, int CT, int TH, int TW, int HC, int NTHR>
-struct FfnBwdGeom : FfnBase<T, NTHR> {
+// ---- packed fp32 (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32) for the per-channel-pair phase
+typedef float f2v __attribute__((ext_vector_type(2)));
+DFM_INLINE f2v f2fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+DFM_INLINE f2v f2s(float v) { return f2v{v, v}; }
+// normal_cdf_pdf (common.h) on two values: the same operations in the same order (bitwise identical)
+DFM_INLINE void normal_cdf_pdf2(f2v x, f2v& cdf, f2v& pdf) {
+  const f2v u = x * f2s(0.70710678118654752f);
+  const f2v au = f2v{fabsf(u.x), fabsf(u.y)};
+  const f2v den = f2fma(f2s(0.3275911f), au, f2s(1.0f));
+  const f2v t = f2v{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f2v p = f2fma(f2s(1.061405429f), t, f2s(-1.453152027f));
+  p = f2fma(p, t, f2s(1.421413741f));
+  p = f2fma(p, t, f2s(-0.284496736f));
+  p = f2fma(p, t, f2s(0.254829592f));
+  p = p * t;
+  const f2v na = -au * au;
+  const f2v e = f2v{__expf(na.x), __expf(na.y)};
+  const f2v tail = f2s(0.5f) * p * e;
+  const f2v one_m = f2s(1.0f) - tail;
+  cdf = f2v{u.x < 0.0f ? tail.x : one_m.x, u.y < 0.0f ? tail.y : one_m.y};
+  pdf = f2s(0.39894228040143268f) * e;
+}
+
+// XOR swizzle of the 16-byte chunks of row k of an unpadded [rows][R] 16-bit LDS image (as the GEMM's
+// row-contiguous tiles): conflict-free for both the k-contiguous fragment reads (ds_read_b128) and
+// the transposing reads (ds_read_b64_tr_b16) of the same image.
+template <int R>
+DFM_INLINE int tr_swz(int k) {
+  if constexpr (R >= 128) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else if constexpr (R == 64) return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  else return 2 * ((k >> 3) & 1);
+}
+// v + v[lane ^ X] for X = 32 / 16 with the gfx950 row-swap permutes (VALU, no LDS round trip)
+template <int X> DFM_INLINE float xor_sum(float v) {
+  const unsigned u = __float_as_uint(v);
+  if constexpr (X == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+}
+
+template <int R> DFM_INLINE int swz_at(int k, int r) { return k * R + ((((r >> 3) ^ tr_swz<R>(k)) << 3) | (r & 7)); }
+
+// Weight images of one chunk in the backward kernel (16-bit: unpadded + swizzled; float32: padded):
+//   w1s [HC][CT] = W1c, read as A[j][c] (h recompute) and transposed as A[c][j] (W1c^T, dxn)
+//   w2s [CT][HC] = W2c, read transposed as A[j][c] (W2c^T, dg)
+template <typename T, int CT> struct BwdW {
+  static constexpr bool H16 = sizeof(T) == 2;
+  static constexpr int P1 = H16 ? CT : CT + 4, P2 = H16 ? HC : HC + 4;  // row pitches
+  static DFM_INLINE int at1(int j, int c) { return H16 ? swz_at<CT>(j, c) : j * P1 + c; }
+  static DFM_INLINE int at2(int c, int j) { return H16 ? swz_at<HC>(c, j) : c * P2 + j; }
+  // A fragment rows r0 .. r0 + 16 of the image [K][R] read transposed: A[r][k] = img[k][r]
+  template <int R>
+  static DFM_INLINE typename FT<T>::frag tr_frag(const T* img, int r0, int k0, int lane) {
+    if constexpr (H16) {
+      const int i = lane & 15, gq = lane >> 4, q = i >> 2, p = i & 3;
+      typedef __attribute__((address_space(3))) short4_t lds_s4;
+      const int k = k0 + 8 * gq + q, r = r0 + 4 * p;
+      short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + swz_at<R>(k, r)));
+      short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + swz_at<R>(k + 4, r)));
+      typedef __attribute__((ext_vector_type(8))) short short8_t;
+      short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      return __builtin_bit_cast(bf16x8_t, v);
+    } else {
+      return img[(k0 + (lane >> 4)) * (R + 4) + r0 + (lane & 15)];
+    }
+  }
+  // A[j][c] = W1c[j][c] (k-contiguous rows of w1s)
+  static DFM_INLINE typename FT<T>::frag w1_frag(const T* w1s, int j0, int k0, int lane) {
+    const int j = j0 + (lane & 15);
+    if constexpr (H16) {
+      return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(w1s + at1(j, k0 + 8 * (lane >> 4))));
+    } else {
+      return w1s[at1(j, k0 + (lane >> 4))];
+    }
+  }
+};
+
+// register-staged prefetch of W1c / W2c / the chunk's parameters into the backward's swizzled images
+template <typename T, int CT, int NT>
+struct BwdPrefetch {
+  using BW = BwdW<T, CT>;
+  static constexpr int V = 16 / sizeof(T);
+  static constexpr int N1 = HC * CT / V, N2 = CT * HC / V;
+  static constexpr int R1 = (N1 + NT - 1) / NT, R2 = (N2 + NT - 1) / NT;
+  static constexpr int RP = (PB + NT - 1) / NT;
+  uint4 w1[R1], w2[R2];
+  float par[RP];
+  DFM_INLINE void load(const T* __restrict__ gw1, const T* __restrict__ gw2, const float* __restrict__ b1,
+                       const float* __restrict__ bpos, const float* __restrict__ wpos, int C, int hid, int c0) {
+#pragma unroll
+    for (int i = 0; i < R1; ++i) {
+      const int v = threadIdx.x + i * NT;
+      const int j = v / (CT / V), c = (v % (CT / V)) * V;
+      w1[i] = (v < N1 && c < C) ? *reinterpret_cast<const uint4*>(gw1 + (long)(c0 + j) * C + c) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < R2; ++i) {
+      const int v = threadIdx.x + i * NT;
+      const int c = v / (HC / V), j = (v % (HC / V)) * V;
+      w2[i] = (v < N2 && c < C) ? *reinterpret_cast<const uint4*>(gw2 + (long)c * hid + c0 + j) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int e = threadIdx.x + i * NT;
+      float v = 0.f;
+      if (e < HC) v = b1[c0 + e];
+      else if (e < 2 * HC) v = bpos[c0 + e - HC];
+      else if (e < PB) {
+        const int t = (e - 2 * HC) / HC, ch = (e - 2 * HC) % HC;
+        v = wpos[(long)(c0 + ch) * 9 + t] + (t == 4 ? 1.0f : 0.0f);
+      }
+      par[i] = v;
+    }
+  }
+  DFM_INLINE void store(T* w1s, T* w2s, float* pb) const {
+#pragma unroll
+    for (int i = 0; i < R1; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= N1) break;
+      const int j = v / (CT / V), c = (v % (CT / V)) * V;
+      *reinterpret_cast<uint4*>(w1s + BW::at1(j, c)) = w1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < R2; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (v >= N2) break;
+      const int c = v / (HC / V), j = (v % (HC / V)) * V;
+      *reinterpret_cast<uint4*>(w2s + BW::at2(c, j)) = w2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int e = threadIdx.x + i * NT;
+      if (e < PB) pb[e] = par[i];
+    }
+  }
+};
+
+template <typename T, int CT, int TH>
+struct BwdGeom {
+  static constexpr int NT = 512, NW = 8;
   static constexpr int HW2 = TW + 2, HW4 = TW + 4;
-  static constexpr int NH1 = (TH + 2) * (TW + 2);
-  static constexpr int NH1P = (NH1 + 15) / 16 * 16;
-  static constexpr int NH2 = (TH + 4) * (TW + 4);
-  static constexpr int NH2P = (NH2 + 15) / 16 * 16;
+  static constexpr int NH1 = (TH + 2) * HW2, NT1 = (NH1 + 15) / 16, NH1P = NT1 * 16;  // tile + 1 halo
+  static constexpr int NH2 = (TH + 4) * HW4, NT2 = (NH2 + 15) / 16, NH2P = NT2 * 16;  // tile + 2 halo
   static constexpr int TP = TH * TW;
-  static constexpr int XP = lpitch<T>(CT);
-  static constexpr int HP = lpitch<T>(HC);
-  static constexpr int SP = CT + 4;
-  static constexpr int G8 = HC / 8;
-  static constexpr int NPAIR = G8 * 10;              // (8-channel group, tap|bias) pairs
-  static constexpr int NSL = NTHR / NPAIR > 3 ? 3 : NTHR / NPAIR;  // pixel slices of the dw-gradient reduction
+  static constexpr int XP = CT + FT<T>::PAD;  // xs / dfs row pitch
+  using BW = BwdW<T, CT>;
+  using P1 = Planes<NH1P, 4>;   // dg -> dhpre: read in the MFMA operand layout ([C])
+  using P2 = Planes<NH2P, 16>;  // h: read per channel pair ([B])
   static constexpr size_t o_df = (size_t)NH2P * XP * sizeof(T);
   static constexpr size_t o_w1 = o_df + (size_t)NH1P * XP * sizeof(T);
-  static constexpr size_t o_w2t = o_w1 + (size_t)HC * XP * sizeof(T);
-  static constexpr size_t o_w1t = o_w2t + (size_t)HC * XP * sizeof(T);
-  static constexpr size_t o_h = o_w1t + (size_t)CT * HP * sizeof(T);
-  static constexpr size_t o_d = o_h + (size_t)(NH2P > TP ? NH2P : TP) * HP * sizeof(T);
-  static constexpr size_t o_r = o_d + (size_t)NH1P * HP * sizeof(T);
-  static constexpr size_t o_p = o_r + (size_t)NSL * NPAIR * 8 * sizeof(float);
-  static constexpr size_t lds_main = o_p + (size_t)11 * HC * sizeof(float);
-  static constexpr size_t lds_stage = (size_t)TP * SP * sizeof(float);
-  static constexpr size_t lds = lds_main > lds_stage ? lds_main : lds_stage;
+  static constexpr size_t o_w2 = o_w1 + (size_t)HC * BW::P1 * sizeof(T);
+  static constexpr size_t o_pb = o_w2 + (size_t)CT * BW::P2 * sizeof(T);
+  static constexpr size_t o_hs = o_pb + (size_t)PB * 4;
+  static constexpr size_t o_ds = o_hs + (size_t)P2::FLOATS * 4;
+  static constexpr size_t o_red = o_ds + (size_t)P1::FLOATS * 4;
+  static constexpr size_t o_gs = o_red + (size_t)NW * (HC / 2) * 10 * 2 * 4;  // per-wave depthwise-gradient sums
+  static constexpr int GP = HC + (sizeof(T) == 2 ? 8 : 4);  // g staging row pitch (elements)
+  static constexpr size_t lds = o_gs + (size_t)TP * GP * sizeof(T);  // g of the tile, written out in [C]
 };
 
-template <typename T, int CT, int TH, int TW, int HC, int NTHR>
-__global__ __launch_bounds__(NTHR, 2) void convffn_bwd_kernel(FfnBwdArgs a) {
-  using G = FfnBwdGeom<T, CT, TH, TW, HC, NTHR>;
-  constexpr int NT = G::NT, NWV = G::NWV, TP = G::TP, XP = G::XP, HP = G::HP, G8 = G::G8;
-  constexpr int PT = TP / 16;
-  constexpr int PTW = (PT + NWV - 1) / NWV;
+template <typename T, int CT, int TH>
+__global__ __launch_bounds__(512) void convffn_bwd_kernel(FfnBwdArgs a) {
+  using G = BwdGeom<T, CT, TH>;
+  using F = FT<T>;
+  using P1 = typename G::P1;
+  using P2 = typename G::P2;
+  using BW = typename G::BW;
+  constexpr int NT = G::NT, NW = G::NW, XP = G::XP;
   constexpr int OT = CT / 16;
-  constexpr int NT2 = G::NH2P / 16;  // fc1 pixel tiles (tile + 2 halo)
-  constexpr int NT1 = G::NH1P / 16;  // dg pixel tiles (tile + 1 halo)
+  constexpr int KC = CT / F::KS;
+  constexpr int K2 = HC / F::KS;
+  constexpr int PTW = 1;                // [C]: waves 0 .. TH-1 own one tile row each
+  static_assert(TH <= NW, "one tile row per wave in [C]");
+  constexpr int NU = G::NT2 + G::NT1;  // [A] units: h tiles, then dg tiles
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* xs = reinterpret_cast<T*>(smem);                 // [NH2P][XP] xn on tile + 2 halo
-  T* dfs = reinterpret_cast<T*>(smem + G::o_df);      // [NH1P][XP] df on tile + 1 halo
-  T* w1s = reinterpret_cast<T*>(smem + G::o_w1);      // [HC][XP] W1 rows of the chunk
-  T* w2ts = reinterpret_cast<T*>(smem + G::o_w2t);    // [HC][XP] W2^T rows of the chunk
-  T* w1ts = reinterpret_cast<T*>(smem + G::o_w1t);    // [CT][HP] W1^T[:, chunk]
-  T* hs = reinterpret_cast<T*>(smem + G::o_h);        // [NH2P][HP] h; later [TP][HP] dh
-  T* ds = reinterpret_cast<T*>(smem + G::o_d);        // [NH1P][HP] dg -> dhpre
-  float* red = reinterpret_cast<float*>(smem + G::o_r);  // [NSL][NPAIR][8]
+  T* xs = reinterpret_cast<T*>(smem);
+  T* dfs = reinterpret_cast<T*>(smem + G::o_df);
+  T* w1s = reinterpret_cast<T*>(smem + G::o_w1);
+  T* w2s = reinterpret_cast<T*>(smem + G::o_w2);
+  float* pb = reinterpret_cast<float*>(smem + G::o_pb);
+  float* hs = reinterpret_cast<float*>(smem + G::o_hs);
+  float* ds = reinterpret_cast<float*>(smem + G::o_ds);
+  float* red = reinterpret_cast<float*>(smem + G::o_red);
+  T* gs = reinterpret_cast<T*>(smem + G::o_gs);
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, tid = threadIdx.x;
-  const int tile = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nt = a.B * a.tiles_y * a.tiles_x;
+  const int tile = xcd_tile(blockIdx.x, nt);
   const int b = tile / (a.tiles_y * a.tiles_x);
   const int ty = (tile / a.tiles_x) % a.tiles_y, tx = tile % a.tiles_x;
   const int y0 = ty * TH, x0 = tx * TW;
-  const int C = a.C, hid = a.hid;
-  const T* xn = (const T*)a.xn;
-  const T* df = (const T*)a.df;
-  const T* w1 = (const T*)a.w1;
-  const T* w2t = (const T*)a.w2t;
-  const T* w1t = (const T*)a.w1t;
-  const int g = tid % G8;
-  auto pix = [&](int yy, int xx) { return (long)(b * a.H + yy) * a.W + xx; };
-  auto inside = [&](int yy, int xx) { return yy >= 0 && yy < a.H && xx >= 0 && xx < a.W; };
+  const int C = a.C, hid = a.hid, H = a.H, W = a.W;
+  const int px = lane & 15, kq = lane >> 4;
+  auto inside = [&](int yy, int xx) { return yy >= 0 && yy < H && xx >= 0 && xx < W; };
+  auto pix = [&](int yy, int xx) { return (long)(b * H + yy) * W + xx; };
 
-  float* pb = reinterpret_cast<float*>(smem + G::o_p);  // [11][HC] b1 | bpos | wpos (tap-major)
-  constexpr int VEC = 16 / sizeof(T);
-  Prefetch2D<T, NT, (HC * CT / VEC + NT - 1) / NT> pw1, pw2t, pw1t;
-  ParamPrefetch<HC, NT> ppar;
-  auto fetch = [&](int c) {
-    pw1.load(w1 + (long)c * C, C, HC, C);
-    pw2t.load(w2t + (long)c * C, C, HC, C);
-    pw1t.load(w1t + c, hid, C, HC);
-    ppar.load(a.b1, a.bpos, a.wpos, c);
-  };
-  auto put = [&]() {
-    pw1.store(w1s, XP, HC, C);
-    pw2t.store(w2ts, XP, HC, C);
-    pw1t.store(w1ts, HP, C, HC);
-    ppar.store(pb);
-  };
-  fetch(0);
-  stage_rows<T, NT>(xs, XP, G::NH2P, C, [&](int q) -> const T* {
-    const int yy = y0 - 2 + q / G::HW4, xx = x0 - 2 + q % G::HW4;
-    return (q < G::NH2 && inside(yy, xx)) ? xn + pix(yy, xx) * a.ldxn : nullptr;
-  });
-  stage_rows<T, NT>(dfs, XP, G::NH1P, C, [&](int q) -> const T* {
-    const int yy = y0 - 1 + q / G::HW2, xx = x0 - 1 + q % G::HW2;
-    return (q < G::NH1 && inside(yy, xx)) ? df + pix(yy, xx) * a.lddf : nullptr;
-  });
-  put();
-
-  float4_t acc[PTW][OT];  // dxn^T[c][p]
+  BwdPrefetch<T, CT, NT> pf;
+  pf.load((const T*)a.w1, (const T*)a.w2, a.b1, a.bpos, a.wpos, C, hid, 0);
+  stage_halo<T, CT, XP, NT>(xs, (const T*)a.xn, a.ldxn, G::NH2, G::NH2P, G::HW4, b, y0 - 2, x0 - 2, H, W, C);
+  stage_halo<T, CT, XP, NT>(dfs, (const T*)a.df, a.lddf, G::NH1, G::NH1P, G::HW2, b, y0 - 1, x0 - 1, H, W, C);
+  pf.store(w1s, w2s, pb);
+  float4_t acc[PTW][OT];  // dxn^T[c][pixel]
 #pragma unroll
   for (int i = 0; i < PTW; ++i)
 #pragma unroll
-    for (int j = 0; j < OT; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < OT; ++o) acc[i][o] = float4_t{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
-  for (int c0 = 0; c0 < hid; c0 += HC) {
-    const bool more = c0 + HC < hid;
-    if (more) fetch(c0 + HC);  // next chunk's operands in flight under this chunk's work
-    // ---- [1] h on tile + 2 halo -> hs ; [2] dg on tile + 1 halo -> ds
-#pragma unroll 1
-    for (int jt = wid; jt < NT2 + NT1; jt += NWV) {
-      float4_t h[HC / 16];
-#pragma unroll
-      for (int it = 0; it < HC / 16; ++it) h[it] = float4_t{0.f, 0.f, 0.f, 0.f};
-      if (jt < NT2) {
-        mma_rows<T, HC / 16>(h, w1s, XP, xs + jt * 16 * XP, XP, C, lane);
-        const int q = jt * 16 + (lane & 15);
-        const int yy = y0 - 2 + q / G::HW4, xx = x0 - 2 + q % G::HW4;
-        const bool val = q < G::NH2 && inside(yy, xx);
-#pragma unroll
-        for (int it = 0; it < HC / 16; ++it) {
-          const int ch = it * 16 + 4 * (lane >> 4);
-          const float4 bb = *reinterpret_cast<const float4*>(pb + ch);
-          const float v[4] = {val ? h[it][0] + bb.x : 0.f, val ? h[it][1] + bb.y : 0.f, val ? h[it][2] + bb.z : 0.f,
-                              val ? h[it][3] + bb.w : 0.f};
-          st4(hs + q * HP + ch, v);
-        }
-      } else {
-        const int j1 = jt - NT2;
-        mma_rows<T, HC / 16>(h, w2ts, XP, dfs + j1 * 16 * XP, XP, C, lane);
-        const int q = j1 * 16 + (lane & 15);
-#pragma unroll
-        for (int it = 0; it < HC / 16; ++it) {
-          const float v[4] = {h[it][0], h[it][1], h[it][2], h[it][3]};
-          st4(ds + q * HP + it * 16 + 4 * (lane >> 4), v);
-        }
-      }
-    }
-    __syncthreads();
-    // ---- [3] hpre = DW3(h) + bpos + h on tile + 1 halo; g = GELU(hpre) (tile pixels -> HBM);
-    //          dhpre = dg * GELU'(hpre) in place (df rows outside the image are zero)
-#pragma unroll 1
-    for (int u = tid; u < G::NH1 * G8; u += NT) {
-      const int q = u / G8;
-      const int qy = q / G::HW2, qx = q % G::HW2;
-      float sv[8], dv[8], gv[8];
-      dw_unit_lds<T, HP, G::HW4, HC, false>(hs + g * 8, qy * G::HW4 + qx, pb + 2 * HC + g * 8, pb + HC + g * 8, sv);
-      ld8<T>(ds + q * HP + g * 8, dv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float cdf, pdf;
-        normal_cdf_pdf(sv[e], cdf, pdf);
-        gv[e] = sv[e] * cdf;
-        dv[e] *= fmaf(sv[e], pdf, cdf);
-      }
-      st8<T>(ds + q * HP + g * 8, dv);
-      const int yy = y0 - 1 + qy, xx = x0 - 1 + qx;
-      if (qy >= 1 && qy <= TH && qx >= 1 && qx <= TW && inside(yy, xx))
-        st8<T>((T*)a.g + pix(yy, xx) * a.ldg + c0 + g * 8, gv);
-    }
-    __syncthreads();
-    // ---- [4] depthwise weight / bias gradient partials: sum_p dhpre[p] * h[p + (dy-1, dx-1)]
+  const int nchunk = hid / HC;
+  const bool stamping = a.stamp != nullptr && blockIdx.x == 0 && tid == 0;
+  auto stamp = [&](int i) {
+    if (stamping) a.stamp[i] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  for (int ci = 0; ci < nchunk; ++ci) {
+    const int c0 = ci * HC;
+    const bool more = ci + 1 < nchunk;
+    stamp(1 + ci * 5);
+    if (more) pf.load((const T*)a.w1, (const T*)a.w2, a.b1, a.bpos, a.wpos, C, hid, c0 + HC);
+    // ---- [A] h^T = W1c xn^T on tile + 2 halo (+ b1, zero outside the image) -> hs; dg^T = W2c^T df^T
+    //          on tile + 1 halo -> ds (df rows outside the image are zero, so is dg)
     {
-      const int pr = tid % G::NPAIR, sl = tid / G::NPAIR;
-      if (sl < G::NSL) {
-        const int gg = pr / 10, t = pr % 10;
-        const int off = t < 9 ? (t / 3) * G::HW4 + t % 3 : G::HW4 + 1;
-        float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int p = sl; p < TP; p += G::NSL) {
-          const int py = p / TW, px = p % TW;
-          float dv[8], hv[8];
-          ld8<T>(ds + ((py + 1) * G::HW2 + px + 1) * HP + gg * 8, dv);
-          if (t < 9) {
-            ld8<T>(hs + ((py + 1) * G::HW4 + px + 1 + off) * HP + gg * 8, hv);
-          } else {
+      typename F::frag aw[2][2][KC];  // [W1c | W2c^T][hidden tile][k-step]
 #pragma unroll
-            for (int e = 0; e < 8; ++e) hv[e] = 1.f;
+      for (int it = 0; it < 2; ++it)
+#pragma unroll
+        for (int ks = 0; ks < KC; ++ks) {
+          aw[0][it][ks] = BW::w1_frag(w1s, it * 16, ks * F::KS, lane);
+          aw[1][it][ks] = BW::template tr_frag<HC>(w2s, it * 16, ks * F::KS, lane);
+        }
+      const int nu = (a.skip & 1) ? 0 : NU;
+      for (int u = wid; u < nu; u += NW) {
+        const bool isH = u < G::NT2;
+        const T* brow = (isH ? xs + (u * 16 + px) * XP : dfs + ((u - G::NT2) * 16 + px) * XP);
+        float4_t h[2] = {float4_t{0.f, 0.f, 0.f, 0.f}, float4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < KC; ++ks) {
+          const typename F::frag xb = F::ld(brow, ks * F::KS, lane);
+#pragma unroll
+          for (int it = 0; it < 2; ++it) h[it] = F::mma(isH ? aw[0][it][ks] : aw[1][it][ks], xb, h[it]);
+        }
+        if (isH) {
+          const int q = u * 16 + px;
+          const int yy = y0 - 2 + q / G::HW4, xx = x0 - 2 + q % G::HW4;
+          const bool ok = q < G::NH2 && inside(yy, xx);
+#pragma unroll
+          for (int it = 0; it < 2; ++it) {
+            const float4 bb = *reinterpret_cast<const float4*>(pb + it * 16 + 4 * kq);
+            const float4 o4 = ok ? make_float4(h[it][0] + bb.x, h[it][1] + bb.y, h[it][2] + bb.z, h[it][3] + bb.w)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(hs + P2::at(q, it * 16 + 4 * kq)) = o4;
+          }
+        } else {
+          const int q = (u - G::NT2) * 16 + px;
+#pragma unroll
+          for (int it = 0; it < 2; ++it)
+            *reinterpret_cast<float4*>(ds + P1::at(q, it * 16 + 4 * kq)) =
+                make_float4(h[it][0], h[it][1], h[it][2], h[it][3]);
+        }
+      }
+    }
+    lds_sync();
+    stamp(2 + ci * 5);
+    // ---- [B] on tile + 1 halo, one channel pair per unit (fixed per thread, its taps in registers):
+    //          hpre = DW3(h) + bpos + h; g = GELU(hpre) (tile pixels -> HBM); dhpre = dg GELU'(hpre)
+    //          in place of dg. The depthwise weight / bias gradient of an interior pixel,
+    //          sum_t dhpre[p] h[p + tap t], reuses the 9 h values just loaded for hpre[p]: per-thread
+    //          sums, then a fixed-order reduction (lanes l ^ 16, l ^ 32, then the 8 waves via LDS).
+    {
+      const int cp = tid & 15, ch = 2 * cp;  // channels ch, ch + 1 of the chunk
+      f2v wt[9];
+      const f2v bias2 = *reinterpret_cast<const f2v*>(pb + HC + ch);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wt[t] = *reinterpret_cast<const f2v*>(pb + 2 * HC + t * HC + ch);
+      f2v dw[10];
+#pragma unroll
+      for (int t = 0; t < 10; ++t) dw[t] = f2s(0.f);
+      const int nq = (a.skip & 2) ? 0 : G::NH1;
+      for (int q = tid >> 4; q < nq; q += NT / 16) {
+        const int qy = q / G::HW2, qx = q % G::HW2;
+        f2v hv[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          hv[t] = *reinterpret_cast<const f2v*>(hs + P2::at((qy + t / 3) * G::HW4 + qx + t % 3, ch));
+        f2v* dp = reinterpret_cast<f2v*>(ds + P1::at(q, ch));
+        f2v dv = *dp;
+        f2v sv = bias2;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) sv = f2fma(wt[t], hv[t], sv);
+        f2v cdf, pdf;
+        normal_cdf_pdf2(sv, cdf, pdf);
+        dv = dv * f2fma(sv, pdf, cdf);
+        *dp = dv;
+        const int yy = y0 - 1 + qy, xx = x0 - 1 + qx;
+        if (qy >= 1 && qy <= TH && qx >= 1 && qx <= TW && inside(yy, xx)) {
+          // g of the interior pixels -> the LDS tile; [C] writes it out with one 16-byte store per lane
+          T* gp = gs + ((qy - 1) * TW + qx - 1) * G::GP + ch;
+          const f2v gv = sv * cdf;
+          if constexpr (sizeof(T) == 2) {
+            const T e2[2] = {Num<T>::from_f(gv.x), Num<T>::from_f(gv.y)};
+            *reinterpret_cast<uint32_t*>(gp) = *reinterpret_cast<const uint32_t*>(e2);
+          } else {
+            *reinterpret_cast<float2*>(gp) = make_float2(gv.x, gv.y);
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s8[e] = fmaf(dv[e], hv[e], s8[e]);
+          for (int t = 0; t < 9; ++t) dw[t] = f2fma(dv, hv[t], dw[t]);
+          dw[9] += dv;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 10; ++t) {  // + lane ^ 32, then + lane ^ 16 (v_permlane{32,16}_swap)
+        dw[t].x = xor_sum<32>(dw[t].x);
+        dw[t].y = xor_sum<32>(dw[t].y);
+        dw[t].x = xor_sum<16>(dw[t].x);
+        dw[t].y = xor_sum<16>(dw[t].y);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 10; ++t) *reinterpret_cast<f2v*>(red + ((wid * 16 + cp) * 10 + t) * 2) = dw[t];
+      }
+    }
+    lds_sync();
+    stamp(3 + ci * 5);
+    // ---- [C] dh = DW3^T(dhpre) + dhpre on the tile rows of this wave, straight into the B fragments
+    //          of dxn^T += W1c^T dh^T; dh -> HBM
+    {
+      typename F::frag a1[OT][K2];
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int ks = 0; ks < K2; ++ks) a1[o][ks] = BW::template tr_frag<CT>(w1s, o * 16, ks * F::KS, lane);
+#pragma unroll
+      for (int i = 0; i < PTW; ++i) {
+        const int pt = wid + i * NW;
+        if (pt >= TH || (a.skip & 4)) break;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {  // tap t reads dhpre at p - (t / 3 - 1, t % 3 - 1)
+          float dv[8], wv[8];
+          ld_lane8<T, G::NH1P>(ds, (pt + 2 - t / 3) * G::HW2 + px + 2 - t % 3, kq, dv);
+          ld_lane8_par<T>(pb + 2 * HC + t * HC, kq, wv);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) s[m] = fmaf(wv[m], dv[m], s[m]);
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) red[(sl * G::NPAIR + pr) * 8 + e] = s8[e];
+        for (int ks = 0; ks < K2; ++ks) {
+          const typename F::frag db = to_frag<T>(s, ks);
+#pragma unroll
+          for (int o = 0; o < OT; ++o) acc[i][o] = F::mma(a1[o][ks], db, acc[i][o]);
+        }
+        const int yy = y0 + pt, xx = x0 + px;
+        if (inside(yy, xx)) {
+          T* dp = (T*)a.dh + pix(yy, xx) * a.lddh + c0;
+          T* gp = (T*)a.g + pix(yy, xx) * a.ldg + c0;
+          const T* gl = gs + (pt * TW + px) * G::GP;
+          if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4*>(dp + 8 * kq) = __builtin_bit_cast(uint4, pack16x8<T>(s));
+            *reinterpret_cast<uint4*>(gp + 8 * kq) = *reinterpret_cast<const uint4*>(gl + 8 * kq);
+          } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) dp[lane_ch<T>(kq, m)] = s[m];
+            *reinterpret_cast<float4*>(gp + 8 * kq) = *reinterpret_cast<const float4*>(gl + 8 * kq);
+            *reinterpret_cast<float4*>(gp + 8 * kq + 4) = *reinterpret_cast<const float4*>(gl + 8 * kq + 4);
+          }
+        }
       }
     }
-    // ---- [5] dh = DW3^T(dhpre) + dhpre on the tile (flipped taps, identity, no bias)
-    {
-      constexpr int NU = (TP * G8 + NT - 1) / NT;
-      float dhv[NU][8];
-#pragma unroll
-      for (int j = 0; j < NU; ++j) {
-        const int p = min((tid + j * NT) / G8, TP - 1);
-        const int pc = (p / TW + 1) * G::HW2 + p % TW + 1;  // the pixel in ds coordinates
-        // dh[p] = dhpre[p] + sum_t w[t] dhpre[p - (t/3 - 1, t%3 - 1)]: the flipped 3x3 around p
-        dw_unit_lds<T, HP, G::HW2, HC, true>(ds + g * 8, pc - G::HW2 - 1, pb + 2 * HC + g * 8, nullptr, dhv[j]);
-      }
-      __syncthreads();  // [4] reads of hs done: dh overwrites it; red complete
-      for (int i = tid; i < G::NPAIR * 8; i += NT) {
-        const int pr = i / 8, e = i % 8, gg = pr / 10, t = pr % 10;
+    // the depthwise-gradient partials of the NW waves, summed in a fixed order: by the waves without a
+    // tile row in [C] when there are enough of them, else after the chunk-end barrier
+    constexpr int R0 = TH * 64 + HC * 10 <= NT ? TH * 64 : 0;
+    auto reduce_red = [&]() {
+      if (tid >= R0 && tid - R0 < HC * 10 && !(a.skip & 8)) {
+        const int r = tid - R0, chn = r / 10, t = r % 10;
+        const int cp = chn >> 1, e = chn & 1;
         float v = 0.f;
 #pragma unroll
-        for (int sl = 0; sl < G::NSL; ++sl) v += red[(sl * G::NPAIR + pr) * 8 + e];
-        a.part[(long)blockIdx.x * hid * 10 + (long)(c0 + gg * 8 + e) * 10 + t] = v;
+        for (int w = 0; w < NW; ++w) v += red[((w * 16 + cp) * 10 + t) * 2 + e];
+        a.part[(long)tile * hid * 10 + (long)(c0 + chn) * 10 + t] = v;
       }
-#pragma unroll
-      for (int j = 0; j < NU; ++j) {
-        const int u = tid + j * NT;
-        if (u >= TP * G8) break;
-        const int p = u / G8;
-        const int yy = y0 + p / TW, xx = x0 + p % TW;
-        st8<T>(hs + p * HP + g * 8, dhv[j]);
-        if (inside(yy, xx)) st8<T>((T*)a.dh + pix(yy, xx) * a.lddh + c0 + g * 8, dhv[j]);
-      }
-    }
-    __syncthreads();
-    // ---- [6] dxn^T[c][p] += W1^T[c][chunk] dh^T
-#pragma unroll
-    for (int i = 0; i < PTW; ++i) {
-      const int pj = wid + i * NWV;
-      if (pj < PT) mma_rows<T, OT>(acc[i], w1ts, HP, hs + pj * 16 * HP, HP, HC, lane);
-    }
-    __syncthreads();  // this chunk's reads of the weight chunks, pb and hs (dh) are done
+    };
+    if (R0 > 0) reduce_red();
+    lds_sync();  // chunk done: hs / ds / weights / pb free
+    stamp(4 + ci * 5);
+    if (R0 == 0) reduce_red();  // red is rewritten only after the next chunk's [A] barrier
     if (more) {
-      put();
-      __syncthreads();
+      pf.store(w1s, w2s, pb);
+      lds_sync();
     }
+    stamp(5 + ci * 5);
   }
-  __syncthreads();
-  float* st = reinterpret_cast<float*>(smem);
+  // ---- dxn: lane holds dxn[pixel px of tile row pt][channels 16 o + 4 kq .. + 4]
 #pragma unroll
   for (int i = 0; i < PTW; ++i) {
-    const int pj = wid + i * NWV;
-    if (pj >= PT) break;
-#pragma unroll
-    for (int ot = 0; ot < OT; ++ot) {
-      const float v[4] = {acc[i][ot][0], acc[i][ot][1], acc[i][ot][2], acc[i][ot][3]};
-      st4(st + (pj * 16 + (lane & 15)) * G::SP + ot * 16 + 4 * (lane >> 4), v);
-    }
-  }
-  __syncthreads();
-  const int CG = C / 8;
-  for (int u = tid; u < TP * CG; u += NT) {
-    const int p = u / CG, c = (u % CG) * 8;
-    const int yy = y0 + p / TW, xx = x0 + p % TW;
+    const int pt = wid + i * NW;
+    if (PTW * NW > TH && pt >= TH) break;
+    const int yy = y0 + pt, xx = x0 + px;
     if (!inside(yy, xx)) continue;
-    st8<T>((T*)a.dxn + pix(yy, xx) * a.lddxn + c, st + p * G::SP + c);
+    T* dp = (T*)a.dxn + pix(yy, xx) * a.lddxn;
+#pragma unroll
+    for (int o = 0; o < OT; ++o) {
+      const int c = o * 16 + 4 * kq;
+      if (c >= C) break;
+      const float v[4] = {acc[i][o][0], acc[i][o][1], acc[i][o][2], acc[i][o][3]};
+      st4g<T>(dp + c, v);
+    }
   }
 }
 
 // ---------------------------------------------------------------- launch configurations
-// (tile, hidden chunk, threads) per channel-width class, sized so two workgroups fit a CU's LDS
-// for bf16 (fp32, the parity path, runs one per CU).
-template <typename T, int CT> struct FwdCfg { static constexpr int TH = 8, TW = CT <= 64 ? 16 : 8, HC = 32, NT = 256; };
-template <typename T, int CT> struct BwdCfg { static constexpr int TH = CT <= 128 ? 8 : 4, TW = 8, HC = 32, NT = 256; };
-// fp32 (the parity path) doubles every LDS image: smaller backward tiles, and C > 128 unsupported
-template <> struct BwdCfg<float, 128> { static constexpr int TH = 4, TW = 4, HC = 32, NT = 256; };
-template <> struct FwdCfg<float, 256> { static constexpr int TH = 1, TW = 1, HC = 32, NT = 256; };  // unused
-template <> struct BwdCfg<float, 256> { static constexpr int TH = 1, TW = 1, HC = 32, NT = 256; };  // unused
-
-constexpr int HC_ALL = 32;  // every configuration walks the hidden dim in chunks of 32
+// forward: 16-bit C <= 64 tiles 8 x 16 with double-buffered weights (two workgroups per CU); C = 128
+// tiles 4 x 16, single-buffered; float32 (the parity path) single-buffered.
+template <typename T, int CT> struct FwdCfg { static constexpr int TH = CT <= 64 ? 8 : 4; static constexpr bool DB = sizeof(T) == 2 && CT <= 64; };
+// backward: one 512-thread workgroup per CU; float32 halves the tile
+template <typename T, int CT> struct BwdCfg { static constexpr int TH = sizeof(T) == 2 ? 8 : 4; };
 
 template <typename T, int CT>
 int launch_fwd(FfnArgs& a, hipStream_t s) {
   using Cf = FwdCfg<T, CT>;
-  using G = FfnGeom<T, CT, Cf::TH, Cf::TW, Cf::HC, Cf::NT>;
+  using G = FwdGeom<T, CT, Cf::TH, Cf::DB>;
   static_assert(G::lds <= 160 * 1024, "LDS");
-  auto kern = convffn_fwd_kernel<T, CT, Cf::TH, Cf::TW, Cf::HC, Cf::NT>;
+  auto kern = convffn_fwd_kernel<T, CT, Cf::TH, Cf::DB>;
   a.tiles_y = cdiv(a.H, Cf::TH);
-  a.tiles_x = cdiv(a.W, Cf::TW);
+  a.tiles_x = cdiv(a.W, TW);
   const long nblk = (long)a.B * a.tiles_y * a.tiles_x;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  DFM_LAUNCH(kern, dim3((unsigned)nblk), dim3(Cf::NT), G::lds, s, a);
+  DFM_LAUNCH(kern, dim3((unsigned)nblk), dim3(G::NT), G::lds, s, a);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
@@ -661,61 +898,49 @@ int launch_fwd(FfnArgs& a, hipStream_t s) {
 template <typename T, int CT>
 int launch_bwd(FfnBwdArgs& a, hipStream_t s) {
   using Cf = BwdCfg<T, CT>;
-  using G = FfnBwdGeom<T, CT, Cf::TH, Cf::TW, Cf::HC, Cf::NT>;
+  using G = BwdGeom<T, CT, Cf::TH>;
   static_assert(G::lds <= 160 * 1024, "LDS");
-  auto kern = convffn_bwd_kernel<T, CT, Cf::TH, Cf::TW, Cf::HC, Cf::NT>;
+  auto kern = convffn_bwd_kernel<T, CT, Cf::TH>;
   a.tiles_y = cdiv(a.H, Cf::TH);
-  a.tiles_x = cdiv(a.W, Cf::TW);
+  a.tiles_x = cdiv(a.W, TW);
   const long nblk = (long)a.B * a.tiles_y * a.tiles_x;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  DFM_LAUNCH(kern, dim3((unsigned)nblk), dim3(Cf::NT), G::lds, s, a);
+  DFM_LAUNCH(kern, dim3((unsigned)nblk), dim3(G::NT), G::lds, s, a);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
 
-template <typename T, int CT>
-long bwd_blocks(int B, int H, int W) {
-  return (long)B * cdiv(H, BwdCfg<T, CT>::TH) * cdiv(W, BwdCfg<T, CT>::TW);
-}
-
 template <typename T>
-long bwd_nblk(int B, int H, int W, int C) {
-  if (C <= 32) return bwd_blocks<T, 32>(B, H, W);
-  if (C <= 64) return bwd_blocks<T, 64>(B, H, W);
-  if (C <= 128) return bwd_blocks<T, 128>(B, H, W);
-  if constexpr (sizeof(T) == 2) return bwd_blocks<T, 256>(B, H, W);
-  return 0;
-}
-
-template <typename T>
-int bwd_dispatch(FfnBwdArgs& a, hipStream_t s) {
-  if (a.C <= 32) return launch_bwd<T, 32>(a, s);
-  if (a.C <= 64) return launch_bwd<T, 64>(a, s);
-  if (a.C <= 128) return launch_bwd<T, 128>(a, s);
-  if constexpr (sizeof(T) == 2) return launch_bwd<T, 256>(a, s);
-  return DFM_ERR_ARG;
+long bwd_nblk(int B, int H, int W) {
+  return (long)B * cdiv(H, BwdCfg<T, 64>::TH) * cdiv(W, TW);
 }
 
 template <typename T>
 int fwd_dispatch(FfnArgs& a, hipStream_t s) {
   if (a.C <= 32) return launch_fwd<T, 32>(a, s);
-  if (a.C <= 64) return launch_fwd<T, 64>(a, s);
-  if (a.C <= 128) return launch_fwd<T, 128>(a, s);
-  if constexpr (sizeof(T) == 2) return launch_fwd<T, 256>(a, s);
-  return DFM_ERR_ARG;
+  return launch_fwd<T, 64>(a, s);
+}
+
+template <typename T>
+int bwd_dispatch(FfnBwdArgs& a, hipStream_t s) {
+  if (a.C <= 32) return launch_bwd<T, 32>(a, s);
+  return launch_bwd<T, 64>(a, s);
 }
 
 bool al16p(const void* p, long ld, int es) { return ((uintptr_t)p % 16 == 0) && ((ld * es) % 16 == 0); }
 
 }  // namespace
 
+// The fused kernels cover the channel widths whose forward and backward tiles fit the LDS together
+// (C <= 64, a multiple of 16: DFormer's stage-0 / stage-1 depth-branch ConvFFNs and Tiny / Large's
+// narrow ones); wider ConvFFNs run on the separate GEMM / depthwise kernels.
 extern "C" int dfm_convffn_supported(int dtype, int C, int hid) {
-  if (dtype != DFM_BF16 && dtype != DFM_F32) return 0;
-  return C >= 8 && C <= (dtype == DFM_BF16 ? 256 : 128) && C % 8 == 0 && hid > 0 && hid % HC_ALL == 0;
+  if (dtype != DFM_BF16 && dtype != DFM_F16 && dtype != DFM_F32) return 0;
+  return C >= 16 && C <= 64 && C % 16 == 0 && hid > 0 && hid % HC == 0;
 }
 
 extern "C" int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn,
@@ -725,7 +950,7 @@ extern "C" int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, c
   DFM_CHECK_ARG(dfm_convffn_supported(dtype, C, hid), "dfm_convffn_fwd: unsupported C=%d hid=%d dtype=%d", C, hid,
                 dtype);
   DFM_CHECK_ARG(xn && x && w1 && b1 && wpos && bpos && w2 && b2 && ls && out && f, "dfm_convffn_fwd: null argument");
-  const int es = dtype == DFM_BF16 ? 2 : 4;
+  const int es = dtype == DFM_F32 ? 4 : 2;
   DFM_CHECK_ARG(al16p(xn, ldxn, es) && al16p(x, ldx, es) && al16p(out, ldout, es) && al16p(f, ldf, es) &&
                     al16p(w1, C, es) && al16p(w2, hid, es) && al16p(b1, 0, 4) && al16p(bpos, 0, 4) &&
                     al16p(wpos, 0, 4),
@@ -738,41 +963,67 @@ extern "C" int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, c
   a.ls = ls; a.rowscale = rowscale; a.out = out; a.ldout = ldout; a.f = f; a.ldf = ldf;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) return fwd_dispatch<bf16_t>(a, s);
+  if (dtype == DFM_F16) return fwd_dispatch<f16_t>(a, s);
   return fwd_dispatch<float>(a, s);
 }
 
 extern "C" size_t dfm_convffn_bwd_workspace(int dtype, int B, int H, int W, int C, int hid) {
-  const long nblk = dtype == DFM_BF16 ? bwd_nblk<bf16_t>(B, H, W, C) : bwd_nblk<float>(B, H, W, C);
+  (void)C;
+  const long nblk = dtype == DFM_F32 ? bwd_nblk<float>(B, H, W) : bwd_nblk<bf16_t>(B, H, W);
   return (size_t)nblk * hid * 10 * sizeof(float);
 }
 
 extern "C" int dfm_convffn_bwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn,
                                const void* df, long lddf, const void* w1, const float* b1, const float* wpos,
-                               const float* bpos, const void* w2t, const void* w1t, void* g, long ldg, void* dh,
-                               long lddh, void* dxn, long lddxn, float* dwpos, float* dbpos, void* workspace,
-                               dfm_stream_t stream) {
+                               const float* bpos, const void* w2, void* g, long ldg, void* dh, long lddh, void* dxn,
+                               long lddxn, float* dwpos, float* dbpos, void* workspace, dfm_stream_t stream) {
   DFM_CHECK_ARG(dfm_convffn_supported(dtype, C, hid), "dfm_convffn_bwd: unsupported C=%d hid=%d dtype=%d", C, hid,
                 dtype);
-  DFM_CHECK_ARG(xn && df && w1 && b1 && wpos && bpos && w2t && w1t && g && dh && dxn && dwpos && dbpos && workspace,
+  DFM_CHECK_ARG(xn && df && w1 && b1 && wpos && bpos && w2 && g && dh && dxn && dwpos && dbpos && workspace,
                 "dfm_convffn_bwd: null argument");
-  const int es = dtype == DFM_BF16 ? 2 : 4;
+  const int es = dtype == DFM_F32 ? 4 : 2;
   DFM_CHECK_ARG(al16p(xn, ldxn, es) && al16p(df, lddf, es) && al16p(g, ldg, es) && al16p(dh, lddh, es) &&
-                    al16p(dxn, lddxn, es) && al16p(w1, C, es) && al16p(w2t, C, es) && al16p(w1t, hid, es) &&
-                    al16p(b1, 0, 4) && al16p(bpos, 0, 4) && al16p(wpos, 0, 4),
+                    al16p(dxn, lddxn, es) && al16p(w1, C, es) && al16p(w2, hid, es) && al16p(b1, 0, 4) &&
+                    al16p(bpos, 0, 4) && al16p(wpos, 0, 4),
                 "dfm_convffn_bwd: rows must be 16-byte aligned");
   if ((long)B * H * W == 0) return DFM_OK;
   FfnBwdArgs a{};
   a.B = B; a.H = H; a.W = W; a.C = C; a.hid = hid;
   a.xn = xn; a.ldxn = ldxn; a.df = df; a.lddf = lddf;
-  a.w1 = w1; a.b1 = b1; a.wpos = wpos; a.bpos = bpos; a.w2t = w2t; a.w1t = w1t;
+  a.w1 = w1; a.b1 = b1; a.wpos = wpos; a.bpos = bpos; a.w2 = w2;
   a.g = g; a.ldg = ldg; a.dh = dh; a.lddh = lddh; a.dxn = dxn; a.lddxn = lddxn;
   a.part = (float*)workspace;
+  static const int skip_env = [] {
+    const char* e = getenv("DFM_FFN_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  a.skip = skip_env;
+  static long long* stamp_buf = [] {
+    long long* p = nullptr;
+    if (getenv("DFM_FFN_STAMP")) (void)hipMalloc(&p, 4096 * sizeof(long long));
+    return p;
+  }();
+  a.stamp = stamp_buf;
   hipStream_t s = (hipStream_t)stream;
-  const int rc = dtype == DFM_BF16 ? bwd_dispatch<bf16_t>(a, s) : bwd_dispatch<float>(a, s);
+  int rc;
+  if (dtype == DFM_BF16) rc = bwd_dispatch<bf16_t>(a, s);
+  else if (dtype == DFM_F16) rc = bwd_dispatch<f16_t>(a, s);
+  else rc = bwd_dispatch<float>(a, s);
   if (rc != DFM_OK) return rc;
   const long nblk = (long)a.B * a.tiles_y * a.tiles_x;
   DFM_LAUNCH(partial_sum_kernel<2>, dim3(cdiv((long)hid * 10, 64)), dim3(1024), 0, s, (int)nblk, (long)hid * 10,
              (const float*)workspace, dwpos, dbpos, 10L, 0);
   DFM_LAUNCH_CHECK();
+  if (stamp_buf) {  // profiling only: print the phase cycles of workgroup 0 (averaged over the chunks)
+    long long h[4096];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, stamp_buf, sizeof(h), hipMemcpyDeviceToHost);
+    const int nc = hid / HC;
+    double ph[4] = {0, 0, 0, 0};
+    for (int c = 0; c < nc; ++c)
+      for (int k = 0; k < 4; ++k) ph[k] += (double)(h[2 + c * 5 + k] - h[1 + c * 5 + k]) / nc;
+    fprintf(stderr, "convffn_bwd stamps (s_memtime ticks / chunk): prologue %lld  A %.0f  B %.0f  C %.0f  "
+            "red+store %.0f  total %lld\n", h[1] - h[0], ph[0], ph[1], ph[2], ph[3], h[nc * 5] - h[0]);
+  }
   return DFM_OK;
 }

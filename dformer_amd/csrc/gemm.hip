@@ -1177,6 +1177,10 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // fitted on the DFormer-B step's GEMM census (tools/gemm_sweep.py --replay, DFM_GEMM_GLDS=0 vs 1):
   // it wins on the forward except wide-N x short-K, and on dgrad from K = 640 up; with a row-
   // contiguous A (wgrad) the register-staged kernel stays ahead.
+  static const int wg_env = [] {  // DFM_GEMM_WG: weight-gradient layout on the LDS-DMA ring (0 off, 3 / 4 stages)
+    const char* e = getenv("DFM_GEMM_WG");
+    return e ? atoi(e) : 0;
+  }();
   if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
     const int kper = (d->K + a.splits - 1) / a.splits;
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 640);
@@ -1184,6 +1188,12 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
       if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
       if (BN == 64) return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
       return glds_ak<64, 128, 4, 2, 2, 3>(a, bk, s);
+    }
+    // weight gradients (both operands row-contiguous, K = pixels): a deep LDS-DMA ring keeps 96-128 KB
+    // of the operand streams in flight per CU, which the latency-bound register pipeline does not
+    if (wg_env && !ak && !bk && a.ala && a.alb && kper >= 4 * GBK && BN == 128) {
+      if (wg_env == 4) return launch_glds<128, 128, 8, 2, false, false, 4, 1>(a, s);
+      return launch_glds<128, 128, 8, 2, false, false, 3, 1>(a, s);
     }
   }
   // Few row tiles (the stage-2/3 GEMMs: M = 19,200 / 4,800 rows) leave CUs idle with 128-row tiles:

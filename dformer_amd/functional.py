@@ -32,8 +32,25 @@ def register_shadow(p, shadow):
     _WCACHE[(id(p), shadow.dtype)] = (_EPOCH[0], shadow, (p.data_ptr(),))
 
 
+def _adjacent_rows(ts):
+    """One [sum of rows, cols] view over 2-D tensors that lie back to back in one storage (the
+    optimizer's flat buffers place q | q_cut | l and proj | proj_e so), or None."""
+    t0 = ts[0]
+    cols = t0.shape[1]
+    off = t0.storage_offset()
+    for t in ts:
+        if (t.dim() != 2 or t.shape[1] != cols or not t.is_contiguous() or t.dtype != t0.dtype or
+                t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() or t.storage_offset() != off):
+            return None
+        off += t.numel()
+    rows = sum(t.shape[0] for t in ts)
+    return t0.new_empty(0).set_(t0.untyped_storage(), t0.storage_offset(), (rows, cols))
+
+
 def wcast(dtype, *params):
-    """Compute-dtype 2-D copy of one parameter (or the row-concatenation of several), cached per epoch."""
+    """Compute-dtype 2-D copy of one parameter (or the row-concatenation of several), cached per epoch.
+    Parameters re-homed by FusedAdamW are views of its flat buffers: the concatenation of adjacent
+    ones is a view of the flat compute-dtype shadow (no per-step copy)."""
     if dtype == torch.float32 and len(params) == 1:
         p = params[0].detach()
         return p if p.dim() == 2 else p.reshape(p.shape[0], -1)
@@ -42,10 +59,15 @@ def wcast(dtype, *params):
     hit = _WCACHE.get(key)
     if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
         return hit[1]
-    src = params[0].detach().reshape(params[0].shape[0], -1) if len(params) == 1 else \
-        torch.cat([p.detach().reshape(p.shape[0], -1) for p in params], 0)
-    src = src.contiguous()
-    w = src if dtype == torch.float32 else K.cast(src, dtype)
+    w = None
+    if len(params) > 1:
+        parts = [wcast(dtype, p) for p in params]
+        w = _adjacent_rows(parts)
+    if w is None:
+        src = params[0].detach().reshape(params[0].shape[0], -1) if len(params) == 1 else \
+            torch.cat([p.detach().reshape(p.shape[0], -1) for p in params], 0)
+        src = src.contiguous()
+        w = src if dtype == torch.float32 else K.cast(src, dtype)
     _WCACHE[key] = (_EPOCH[0], w, ptrs)
     return w
 
@@ -178,33 +200,24 @@ def join_streams(main=None):
 
 
 def _cat1(*vs):
-    """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights."""
+    """Concatenate float32 vectors (bias concat for fused GEMMs); cached like weights (a view when
+    the vectors are adjacent in the optimizer's flat buffer)."""
     key = tuple(id(v) for v in vs) + ("bias",)
     ptrs = tuple(v.data_ptr() for v in vs)
     hit = _WCACHE.get(key)
     if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
         return hit[1]
-    out = torch.cat([v.detach() for v in vs])
+    out = _adjacent_rows([v.detach().view(-1, 1) for v in vs])
+    out = out.view(-1) if out is not None else torch.cat([v.detach() for v in vs])
     _WCACHE[key] = (_EPOCH[0], out, ptrs)
     return out
 
 
-def wcast_t(dtype, p):
-    """Compute-dtype copy of a 2-D weight's transpose (contiguous), cached like wcast."""
-    key = (id(p), dtype, "T")
-    ptrs = (p.data_ptr(),)
-    hit = _WCACHE.get(key)
-    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
-        return hit[1]
-    w = wcast(dtype, p).t().contiguous()
-    _WCACHE[key] = (_EPOCH[0], w, ptrs)
-    return w
-
-
-# DFM_FUSED_FFN=1 runs the ConvFFN on the fused kernels (csrc/convffn.hip). Off by default: measured
-# on MI355X (tools/ffn_ab.py) the fused forward beats the separate kernels at stage 0 (0.48 vs 0.56 ms)
-# but the fused backward is VALU-bound (depthwise + GELU/GELU' recompute on the halo) and slower
-# (s0: 2.4 vs 1.5 ms fwd+bwd), so the separate kernels stay the default until it is not.
+# DFM_FUSED_FFN=1 runs the ConvFFN on the fused kernels (csrc/convffn.hip) wherever they support the
+# width (C <= 64). Off by default: measured on MI355X (tools/ffn_ab.py, DFormer-B bf16 bs 16) the fused
+# forward beats the separate kernels (stage 0: 0.317 vs 0.574 ms) but the fused backward, which
+# recomputes fc1 on a 2-pixel halo and the depthwise / GELU chain per hidden chunk at two waves per
+# SIMD, does not (stage 0 fwd+bwd 1.70 vs 1.51 ms; the whole step 367 vs 381 images/s).
 FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
 
 
@@ -219,11 +232,12 @@ def _ffn_fusable(x, w1, *aligned):
 class ConvFFNFn(torch.autograd.Function):
     """out = x + rowscale * ls * fc2(GELU(DW3x3(h) + h)),  h = fc1(LN(x))   on [P, C] rows.
 
-    fused (default, csrc/convffn.hip): LN, then one kernel for fc1 -> DW3x3 + identity -> GELU ->
-    fc2 -> residual (the [P, rC] hidden activation stays on chip); backward: residual chain rule,
-    one kernel recomputing h / hpre per tile and producing g, dh, dxn and the depthwise gradients,
-    then the fc2 / fc1 weight-gradient GEMMs and the LN backward.
-    unfused: LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
+    fused (C <= 64, csrc/convffn.hip): LN, then one kernel for fc1 -> DW3x3 + identity -> GELU ->
+    fc2 -> residual (the [P, rC] hidden activation stays on chip; only f = the branch output is
+    saved); backward: residual chain rule, one kernel recomputing h / hpre per tile and producing
+    g, dh, dxn and the depthwise gradients, then the fc2 / fc1 weight-gradient GEMMs and the LN
+    backward.
+    unfused (wider C): LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
              GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue)."""
 
     @staticmethod
@@ -283,8 +297,8 @@ class ConvFFNFn(torch.autograd.Function):
         dt = x.dtype
         dout = dout.contiguous()
         df, dls = K.residual_bwd(dout, f, ls, rowscale, H * W)
-        g, dh, dxn, dwpos, dbpos = K.convffn_bwd(xn, df, ctx.shape, wcast(dt, w1), b1, wpos, bpos, wcast_t(dt, w2),
-                                                 wcast_t(dt, w1), dw=gslot(wpos), db=gslot(bpos))
+        g, dh, dxn, dwpos, dbpos = K.convffn_bwd(xn, df, ctx.shape, wcast(dt, w1), b1, wpos, bpos, wcast(dt, w2),
+                                                 dw=gslot(wpos), db=gslot(bpos))
         dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
         dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
         dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
@@ -491,7 +505,8 @@ class AttentionFn(torch.autograd.Function):
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.gelu_bwd(dg, lpre, out=dl)
         # q | q_cut | l
-        dWqcl, dbqcl = K.linear_wgrad(dqcl, xn, bias_grad=True)
+        dWqcl, dbqcl = K.linear_wgrad(dqcl, xn, bias_grad=True, out=gslot_rows(wq, wqc, wl),
+                                      bias_out=gslot_rows(bq, bqc, bl))
         grads["bq"], grads["bqc"], grads["bl"] = dbqcl[:C], dbqcl[C:C + Ch], dbqcl[C + Ch:]
         grads["wq"], grads["wqc"], grads["wl"] = dWqcl[:C], dWqcl[C:C + Ch], dWqcl[C + Ch:]
         Wqcl = wcast(dt, wq, wqc, wl)

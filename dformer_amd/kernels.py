@@ -246,9 +246,10 @@ def convffn_fwd(xn, x, shape, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, out
     return out, f
 
 
-def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2t, w1t, dw=None, db=None):
+def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2, dw=None, db=None):
     """Backward of convffn_fwd given df = dout*ls*rowscale: returns (g, dh, dxn, dwpos, dbpos) with
-    g = GELU(hpre) and dh = dL/dh ([P, hid], for the fc2 / fc1 weight-gradient GEMMs)."""
+    g = GELU(hpre) and dh = dL/dh ([P, hid], for the fc2 / fc1 weight-gradient GEMMs).
+    w1 [hid, C], w2 [C, hid] in the compute dtype (nn.Linear layouts)."""
     B, H, W = shape
     P, C = xn.shape
     hid = w1.shape[0]
@@ -261,8 +262,8 @@ def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2t, w1t, dw=None, db=None):
         db = torch.empty(hid, device=xn.device, dtype=torch.float32)
     ws = _ws(lib.dfm_convffn_bwd_workspace(dtype_code(xn), B, H, W, C, hid), xn.device)
     check(lib.dfm_convffn_bwd(dtype_code(xn), B, H, W, C, hid, ptr(xn), ld(xn), ptr(df), ld(df), ptr(w1), ptr(b1),
-                              ptr(wpos), ptr(bpos), ptr(w2t), ptr(w1t), ptr(g), ld(g), ptr(dh), ld(dh), ptr(dxn),
-                              ld(dxn), ptr(dw), ptr(db), ptr(ws), stream()), "dfm_convffn_bwd")
+                              ptr(wpos), ptr(bpos), ptr(w2), ptr(g), ld(g), ptr(dh), ld(dh), ptr(dxn), ld(dxn),
+                              ptr(dw), ptr(db), ptr(ws), stream()), "dfm_convffn_bwd")
     if ACCOUNT is not None:
         _acct(6.0 * P * C * hid + 36.0 * P * hid, _es(xn) * (P * C * 3 + P * hid * 2) + 3 * _es(xn) * C * hid)
     return g, dh, dxn, dw, db

@@ -51,11 +51,44 @@ class WarmUpPolyLR:
         return self.start_lr * ((1 - float(cur_iter) / self.total_iters) ** self.lr_power)
 
 
+def _chain_order(params, chains):
+    """params reordered so that the members of each chain follow its first member (a chain's flat
+    slots are then adjacent: one view serves the fused GEMM over them, e.g. q | q_cut | l)."""
+    follow = {}
+    members = set()
+    for ch in chains:
+        ch = [p for p in ch if p is not None]
+        if len(ch) > 1:
+            follow[id(ch[0])] = ch[1:]
+            members.update(id(p) for p in ch[1:])
+    out = []
+    for p in params:
+        if id(p) in members:
+            continue
+        out.append(p)
+        out.extend(q for q in follow.get(id(p), []) if any(q is r for r in params))
+    return out
+
+
+def fused_chains(model):
+    """Parameter chains whose flat slots must be adjacent: each Attention's q | q_cut | l weights
+    and biases (one GEMM in the forward, one weight-gradient GEMM in the backward) and proj | proj_e."""
+    chains = []
+    for m in model.modules():
+        if all(hasattr(m, n) for n in ("q", "q_cut", "l", "proj")):
+            chains.append([m.q.weight, m.q_cut.weight, m.l.weight])
+            chains.append([m.q.bias, m.q_cut.bias, m.l.bias])
+            if getattr(m, "proj_e", None) is not None:
+                chains.append([m.proj.weight, m.proj_e.weight])
+                chains.append([m.proj.bias, m.proj_e.bias])
+    return chains
+
+
 class _FlatGroup:
     """Parameters of one optimizer group re-homed into one flat float32 buffer (+ grad, m, v, bf16)."""
 
-    def __init__(self, params, wd, device, shadow_dtype):
-        self.params = [p for p in params if p.requires_grad]
+    def __init__(self, params, wd, device, shadow_dtype, chains=()):
+        self.params = _chain_order([p for p in params if p.requires_grad], chains)
         self.wd = wd
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=device, dtype=torch.float32)
@@ -210,8 +243,9 @@ class FusedAdamW:
         decay, no_decay = group_weight(model)
         self.full_groups = (decay, no_decay)  # reference group lists, incl. frozen params (state_dict indices)
         dev = next(model.parameters()).device
-        self.groups = [_FlatGroup(decay, weight_decay, dev, compute_dtype),
-                       _FlatGroup(no_decay, 0.0, dev, torch.float32)]
+        chains = fused_chains(model)
+        self.groups = [_FlatGroup(decay, weight_decay, dev, compute_dtype, chains),
+                       _FlatGroup(no_decay, 0.0, dev, torch.float32, chains)]
         self.lr, self.betas, self.eps = lr, betas, eps
         self.world = world
         self.step_count = 0

@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 3 (round 2: DFM_F16; copy_dtype on dfm_adamw* / dfm_nmf_update*) */
+int dfm_abi_version(void); /* 4 (round 3: dfm_convffn_bwd takes w2 in its nn.Linear layout) */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -152,9 +152,9 @@ int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const vo
  *   bwd: given df = dL/df (dfm_residual_bwd), recomputes h / hpre per tile and writes g = GELU(hpre)
  *        and dh = dL/dh ([P, hid], the inputs of the fc2 / fc1 weight-gradient GEMMs), dxn = dL/dxn
  *        [P, C] (for dfm_layernorm_bwd) and dwpos [hid][9], dbpos [hid] (overwritten).
- * w1 [hid][C], w2 [C][hid], w2t = w2^T [hid][C], w1t = w1^T [C][hid] in `dtype`; b1, b2, wpos
- * [hid][9], bpos, ls fp32; rowscale fp32 [B] (DropPath) or NULL. Supported shapes:
- * dfm_convffn_supported (8 <= C <= 256, C % 8 == 0, hid a multiple of the hidden chunk). */
+ * w1 [hid][C], w2 [C][hid] in `dtype` (nn.Linear layouts); b1, b2, wpos [hid][9], bpos, ls fp32;
+ * rowscale fp32 [B] (DropPath) or NULL. Supported shapes: dfm_convffn_supported (16 <= C <= 64,
+ * C % 16 == 0, hid % 32 == 0; bf16, f16 and f32). */
 int dfm_convffn_supported(int dtype, int C, int hid);
 int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* x,
                     long ldx, const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
@@ -163,8 +163,8 @@ int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, const void* 
 size_t dfm_convffn_bwd_workspace(int dtype, int B, int H, int W, int C, int hid);
 int dfm_convffn_bwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* df,
                     long lddf, const void* w1, const float* b1, const float* wpos, const float* bpos,
-                    const void* w2t, const void* w1t, void* g, long ldg, void* dh, long lddh, void* dxn,
-                    long lddxn, float* dwpos, float* dbpos, void* workspace, dfm_stream_t stream);
+                    const void* w2, void* g, long ldg, void* dh, long lddh, void* dxn, long lddxn, float* dwpos,
+                    float* dbpos, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)

@@ -11,6 +11,7 @@ Routing around HEAD's crashes: the backbone's `(outs, None)` t
 indexed with [0] before the decode head, and the loss of builder.py:230 is applied
 by hand.
 """
+import contextlib
 import os
 import sys
 import time
@@ -259,11 +260,11 @@ def golden_e2e(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, backw
 
 
 def _fp_rel_err(fa, fb, atol=1e-9):
-    """Same statistic as tests/goldens.py fp_rel_err (sum / abs-sum / l2 / samples)."""
+    """Same statistic as tests/goldens.py fp_rel_err (sum / abs-sum / l2 / relative L2 of the samples)."""
     fa, fb = np.asarray(fa, np.float64), np.asarray(fb, np.float64)
-    scale = max(abs(fb[3:]).max(), atol)
     return max(abs(fa[0] - fb[0]) / max(fb[1], atol), abs(fa[1] - fb[1]) / max(fb[1], atol),
-               abs(fa[2] - fb[2]) / max(fb[2], atol), abs(fa[3:] - fb[3:]).max() / scale)
+               abs(fa[2] - fb[2]) / max(fb[2], atol),
+               np.linalg.norm(fa[3:] - fb[3:]) / max(np.linalg.norm(fb[3:]), atol))
 
 
 def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, dtype=torch.bfloat16,
@@ -283,7 +284,7 @@ def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, 
     if bases is not None:
         model.decode_head.hamburger.ham._build_bases = \
             lambda B_, S, D, R, cuda=False: torch.from_numpy(bases.astype(np.float32))
-    with torch.autocast("cpu", dtype=dtype):
+    with (torch.autocast("cpu", dtype=dtype) if dtype is not None else contextlib.nullcontext()):
         feats = model.encoder_backbone(rgb, dep)[0]
         low = model.decode_head.forward(feats)
         out = F.interpolate(low, size=rgb.shape[-2:], mode="bilinear", align_corners=False)
@@ -410,6 +411,11 @@ def main():
         golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
         golden_bf16_env("e2e_base_small", "DFormer-Base", 2, 64, 80)
         golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37)
+    if want("fp32env"):  # the reference's own float32 error vs fp64: the noise floor of the fp32 gates
+        golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96, dtype=None, prefix="fp32env_")
+        golden_bf16_env("e2e_base_small", "DFormer-Base", 2, 64, 80, dtype=None, prefix="fp32env_")
+        golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37,
+                        dtype=None, prefix="fp32env_")
     if want("f16env"):  # the reference's own torch.autocast(float16) error (train.py --amp, config 5)
         golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37,
                         dtype=torch.float16, prefix="f16env_")

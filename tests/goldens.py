@@ -41,16 +41,20 @@ def rel_err(a, b):
 
 
 def fp_rel_err(fp_a, fp_b, atol=1e-9):
-    """Compare two gen.fingerprint vectors: sum, abs-sum, l2 relative; samples rel-to-max.
+    """Compare two gen.fingerprint vectors: sum, abs-sum, l2 relative; the strided samples as a
+    relative L2 error ||a_s - b_s|| / ||b_s||.
 
-    `atol` floors every denominator so mathematically-zero gradients (e.g. a conv bias feeding a
-    train-mode BatchNorm) compare as equal noise instead of as 100 % relative error."""
+    The samples are NOT compared rel-to-max: a gradient's 1k strided samples can miss its largest
+    entries by orders of magnitude (the image gradient of e2e_tiny_small peaks far above every
+    sample), so max|da_s| / max|b_s| magnified an fp32 summation-order difference of 2e-6 of the
+    tensor's own max into 1e-3..4e-3 (tools/fp32_audit.py measures the full tensors against the
+    fp64 oracle). `atol` floors every denominator so mathematically-zero gradients (e.g. a conv bias
+    feeding a train-mode BatchNorm) compare as equal noise instead of as 100 % relative error."""
     fa, fb = np.asarray(fp_a, np.float64), np.asarray(fp_b, np.float64)
-    scale = max(abs(fb[3:]).max(), atol)
     e_s = abs(fa[0] - fb[0]) / max(fb[1], atol)
     e_a = abs(fa[1] - fb[1]) / max(fb[1], atol)
     e_l = abs(fa[2] - fb[2]) / max(fb[2], atol)
-    e_samp = abs(fa[3:] - fb[3:]).max() / scale
+    e_samp = np.linalg.norm(fa[3:] - fb[3:]) / max(np.linalg.norm(fb[3:]), atol)
     return max(e_s, e_a, e_l, e_samp)
 
 

@@ -6,7 +6,7 @@ import torch
 
 import dformer_ref as R
 import gen
-from goldens import check_param_grads, fp_rel_err, load, rel_err
+from goldens import check_param_grads, fp_rel_err, load, params, rel_err
 
 
 class Cfg(dict):
@@ -61,19 +61,97 @@ def test_segmentor_fp32_vs_reference(name, arch, dec, ncls):
     loss = SegLossFn.apply(rows.contiguous(), b, h, w, lab, 255)
     loss.backward()
     torch.cuda.synchronize()
+    env = load("fp32env_" + name)
     for i, f in enumerate(feats):
-        assert rel_err(f.float().cpu(), g[f"feat{i}"]) < 1e-3, i
-    assert rel_err(low.float().cpu(), g["low"]) < 1e-3
-    assert abs(loss.item() - float(g["loss"])) < 1e-4 * abs(float(g["loss"]))
-    assert fp_rel_err(gen.fingerprint(rgb.grad.cpu().double().numpy()), g["grgb_fp"]) < 1e-3
+        assert rel_err(f.float().cpu(), g[f"feat{i}"]) < 1e-4, i
+    assert rel_err(low.float().cpu(), g["low"]) < 1e-4
+    assert abs(loss.item() - float(g["loss"])) < 1e-5 * abs(float(g["loss"]))
+    e_rgb = fp_rel_err(gen.fingerprint(rgb.grad.cpu().double().numpy()), g["grgb_fp"])
+    assert e_rgb < fp32_gate(env["env/grgb"]), (e_rgb, float(env["env/grgb"]))
     bad = []
     for k, v in g.items():
         if k.startswith("gfp/"):
             p = dict(model.named_parameters())[k[4:]]
             e = fp_rel_err(gen.fingerprint(p.grad.cpu().double().numpy(), 16), v, atol=1e-4)
-            if e > 2e-3:
-                bad.append((k, e))
+            if e > fp32_gate(env["env/" + k]):
+                bad.append((k, e, float(env["env/" + k])))
     assert not bad, bad[:10]
+
+
+# fp32 end-to-end gates, from the reference's OWN float32 error on each golden (tests/golden/
+# fp32env_*.npz: the reference run in float32 vs its float64 golden, oracle/make_goldens.py
+# golden_bf16_env(dtype=None)): 10 x that envelope, floored at 1e-4 — ten times tighter than
+# SURVEY §8c's 1e-3 fp32 gate wherever the envelope allows (it allows it everywhere but for the
+# mathematically-zero gradients of conv biases ahead of a train-mode BatchNorm, whose fingerprints
+# are rounding noise in the reference too). tools/fp32_audit.py / test_segmentor_fp32_vs_oracle_full
+# check the full tensors against the fp64 oracle.
+FP32_ENV_X = 10.0
+FP32_FLOOR = 1e-4
+
+
+def fp32_gate(env):
+    return max(FP32_FLOOR, FP32_ENV_X * float(env))
+
+
+@pytest.mark.gpu
+def test_segmentor_fp32_vs_oracle_full():
+    """Full tensors (not fingerprints) of the fp32 HIP path against the fp64 oracle restatement on
+    e2e_tiny_small: the encoder features and their gradients, the logits and their gradient, the
+    image / depth gradients and every parameter gradient, each rel-to-max <= 1e-4 (measured on
+    MI355X: <= 8.3e-6; the reference's own fp32 error on this case is 1-2e-6)."""
+    errs = fp32_audit("e2e_tiny_small", "DFormer-Tiny", "ham", 40)
+    bad = {k: v for k, v in errs.items() if v > 1e-4}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
+
+
+def fp32_audit(name, arch, dec, ncls):
+    """{quantity: rel-to-max error} of the fp32 HIP path vs the fp64 oracle on a golden case."""
+    g = load(name)
+    B, H, W, _ = [int(v) for v in g["meta"]]
+    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    lab_np = gen.labels(B, H, W, ncls)
+    bases = gen.nmf_bases(B, 512, 64, name=name + "/bases") if dec == "ham" else None
+    model = build(arch, dec, ncls, "cuda")
+    model.train()
+    if dec == "ham":
+        model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(bases).float()
+    rgb = torch.from_numpy(rgb_np).float().cuda().requires_grad_()
+    dep = torch.from_numpy(dep_np).float().cuda().requires_grad_()
+    feats = model.encoder_backbone(rgb, dep)[0]
+    for f in feats:
+        f.retain_grad()
+    low = model.decode_head(feats)
+    low.retain_grad()
+    from dformer_amd.decoders import SegLossFn, _nhwc_rows
+    rows, (b, h, w) = _nhwc_rows(low)
+    loss = SegLossFn.apply(rows.contiguous(), b, h, w, torch.from_numpy(lab_np).cuda(), 255)
+    loss.backward()
+    torch.cuda.synchronize()
+    p = params(R.segmentor_shapes(arch, dec, ncls), torch.float64)
+    rgb64 = torch.from_numpy(rgb_np).double().requires_grad_()
+    dep64 = torch.from_numpy(dep_np).double().requires_grad_()
+    rfeats, rlow, rloss = R.segmentor_forward(p, arch, dec, rgb64, dep64,
+                                              torch.from_numpy(bases).double() if bases is not None else None,
+                                              True, torch.from_numpy(lab_np).long())
+    for f in rfeats:
+        f.retain_grad()
+    rlow.retain_grad()
+    rloss.backward()
+
+    def e(a, b_):
+        return rel_err(a.detach().float().cpu().double(), b_.detach())
+
+    out = {"loss": abs(loss.item() - rloss.item()) / abs(rloss.item()), "low": e(low, rlow),
+           "low.grad": e(low.grad, rlow.grad), "rgb.grad": e(rgb.grad, rgb64.grad),
+           "depth.grad": e(dep.grad, dep64.grad)}
+    for i, (f, rf) in enumerate(zip(feats, rfeats)):
+        out[f"feat{i}"] = e(f, rf)
+        out[f"feat{i}.grad"] = e(f.grad, rf.grad)
+    named = dict(model.named_parameters())
+    for k, v in p.items():
+        if k in named and v.grad is not None and named[k].grad is not None and v.grad.abs().max() > 1e-12:
+            out["grad/" + k] = e(named[k].grad, v.grad)
+    return out
 
 
 @pytest.mark.gpu

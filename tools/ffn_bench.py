@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from dformer_amd import kernels as K  # noqa: E402
 
-STAGES = {0: (16, 120, 160, 64, 8), 1: (16, 60, 80, 128, 8), 2: (16, 30, 40, 256, 4), 3: (16, 120, 160, 32, 8)}
+STAGES = {0: (16, 120, 160, 64, 8), 1: (16, 60, 80, 64, 8), 2: (16, 30, 40, 64, 8), 3: (16, 120, 160, 32, 8)}
 st = int(sys.argv[1]) if len(sys.argv) > 1 else 0
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 B, H, W, C, r = STAGES[st]
@@ -25,7 +25,6 @@ b1, bpos, b2 = (0.1 * torch.randn(n, device=dev) for n in (hid, hid, C))
 wpos = torch.randn(hid, 1, 3, 3, device=dev) / 3
 ls = torch.rand(C, device=dev)
 df = torch.randn(P, C, device=dev).to(dt)
-w2t, w1t = w2.t().contiguous(), w1.t().contiguous()
 
 
 def fwd():
@@ -33,7 +32,7 @@ def fwd():
 
 
 def bwd():
-    return K.convffn_bwd(xn, df, (B, H, W), w1, b1, wpos, bpos, w2t, w1t)
+    return K.convffn_bwd(xn, df, (B, H, W), w1, b1, wpos, bpos, w2)
 
 
 for name, fn in (("fwd", fwd), ("bwd", bwd)):

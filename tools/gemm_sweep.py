@@ -22,6 +22,7 @@ import bench  # noqa: E402
 from dformer_amd import _lib, kernels as K  # noqa: E402
 
 COLD = None  # --cold: a 1 GiB buffer rewritten before every timed launch
+GRAPH = False  # --graph: time launches replayed from a captured graph (device time, no host pacing)
 
 PTR_FIELDS = ("bias", "preact", "mul", "res", "colscale", "rowscale", "colsum")
 
@@ -108,6 +109,27 @@ def replay(d, splits, iters=20):
             ts.append(e0.elapsed_time(e1) * 1e3)
         ts.sort()
         return ts[len(ts) // 2]
+    if GRAPH:  # device time per launch: the launches replayed from a HIP graph (no host pacing)
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            with torch.cuda.graph(g, stream=cs):
+                for _ in range(iters):
+                    _lib.check(_lib.lib.dfm_gemm(d["dtype"], desc, a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                                                 _lib.ptr(ws), _lib.stream()), "dfm_gemm")
+        torch.cuda.current_stream().wait_stream(cs)
+        g.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / iters)
+        return min(ts)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -137,8 +159,12 @@ def main():
     ap.add_argument("--no-splits", action="store_true", help="time only the default split choice")
     ap.add_argument("--cold", action="store_true", help="operands evicted from L2 / Infinity Cache per launch")
     ap.add_argument("--replay", default="", help="replay the shapes of an earlier sweep JSON instead of capturing")
+    ap.add_argument("--graph", action="store_true", help="time graph-replayed launches (device time)")
+    ap.add_argument("--min-count", type=int, default=1, help="replay only shapes called at least this often")
+    ap.add_argument("--wgrad-only", action="store_true", help="only the weight-gradient layout (both row-contiguous)")
     args = ap.parse_args()
-    global COLD
+    global COLD, GRAPH
+    GRAPH = args.graph
     if args.cold:
         COLD = torch.zeros(256 << 20, device="cuda")
     groups = collections.OrderedDict()
@@ -151,6 +177,8 @@ def main():
             groups.setdefault(key(d), [d, 0])[1] += 1
     rows = []
     for _, (d, cnt) in groups.items():
+        if cnt < args.min_count or (args.wgrad_only and (d["a_kcontig"] or d["b_kcontig"])):
+            continue
         nbytes, flops = algo(d)
         r = {"count": cnt, "desc": {k: (bool(v) if k in PTR_FIELDS else v) for k, v in d.items()},
              "bytes": nbytes, "flops": flops, "t_default": replay(d, 0)}
