@@ -262,10 +262,10 @@ def main():
     if not args.no_census:
         table = census(step)
         dom = max(table, key=lambda n: table[n]["measured_ms"])
-    # HIP-graph mode (default at one rank; DFM_GRAPH=1 forces it for multi-rank runs, 0 disables):
+    # HIP-graph mode (default at every world size, RCCL collectives included: tests/test_graph_gpu.py
+    # captures the SyncBN / bucket / loss collectives through a one-rank group; DFM_GRAPH=0 disables):
     # the whole step is captured once and replayed, so ~2.3k kernel launches cost one graph launch
-    graph_env = os.environ.get("DFM_GRAPH")
-    use_graph = not args.eager and (graph_env == "1" or (graph_env is None and world == 1))
+    use_graph = not args.eager and os.environ.get("DFM_GRAPH", "1") != "0"
     use_graph = use_graph and opt.scaler is None  # the fp16 loss scaler reads its overflow flag on the host
     if use_graph:
         step = GraphedTrainStep(model, opt, rgb, dep, lab)

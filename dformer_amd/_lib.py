@@ -69,6 +69,7 @@ _SIGS = {
     "dfm_bn_workspace": (c_size_t, [c_long, c_int]),
     "dfm_bn_stats": (c_int, [c_int, c_long, c_int, P, c_long, P, P, P]),
     "dfm_bn_finalize": (c_int, [c_int, P, c_double, c_float, c_float, P, P, P, P, P]),
+    "dfm_bn_merge": (c_int, [c_int, c_int, P, P, P, P]),
     "dfm_bn_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, P, P, P, P, c_long, c_int, P, c_long, P]),
     "dfm_bn_bwd_stats": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, P]),
     "dfm_bn_bwd_apply": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_double, P, c_long, c_int,

@@ -308,6 +308,26 @@ __global__ void bn_finalize_kernel(int C, const float* __restrict__ st, double c
   if (rv) rv[c] = (1.f - mom) * rv[c] + mom * (float)(var * count / max(count - 1.0, 1.0));
 }
 
+// SyncBN: per-rank shifted sums [S][3][C] (as dfm_bn_stats writes them) -> one triple of the union,
+// re-shifted onto shard 0's K: S1 = sum_s S1_s + n_s d_s, S2 = sum_s S2_s + 2 d_s S1_s + n_s d_s^2 with
+// d_s = K_s - K_0, in fp64 and in shard order (deterministic; for one shard the output is the input).
+__global__ void bn_merge_kernel(int S, int C, const float* __restrict__ parts, const float* __restrict__ counts,
+                                float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double k0 = parts[2 * C + c];
+  double s1 = 0.0, s2 = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const float* p = parts + (long)s * 3 * C;
+    const double n = counts[s], a = p[c], b = p[C + c], d = (double)p[2 * C + c] - k0;
+    s1 += a + n * d;
+    s2 += b + 2.0 * d * a + n * d * d;
+  }
+  out[c] = (float)s1;
+  out[C + c] = (float)s2;
+  out[2 * C + c] = (float)k0;
+}
+
 template <typename T>
 __global__ void bn_apply_kernel(long rows, int C, const T* __restrict__ x, long ldx, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -617,6 +637,15 @@ extern "C" int dfm_bn_finalize(int C, const float* stats, double count, float ep
                                float* rstd, float* rm, float* rv, dfm_stream_t stream) {
   DFM_LAUNCH(bn_finalize_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, C, stats, count, eps,
                      momentum, mean, rstd, rm, rv);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_bn_merge(int shards, int C, const float* parts, const float* counts, float* stats,
+                            dfm_stream_t stream) {
+  DFM_CHECK_ARG(parts && counts && stats && shards > 0 && C > 0, "dfm_bn_merge: bad argument");
+  DFM_LAUNCH(bn_merge_kernel, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, shards, C, parts, counts,
+             stats);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

@@ -6,14 +6,13 @@
 //   computes log-sum-exp and the CE term; block partials are summed in a fixed order.
 // Backward, integer upsampling factor (the DFormer heads: x8 ham, x4 MLP decoder at 480x640):
 //   seg_loss_bwd_tile_kernel + seg_loss_gather_kernel (below): deterministic, no atomics.
-// Backward, other factors: seg_loss_bwd_kernel — per tile of label pixels a separable reduction
-//   in LDS, then one float atomic per (cell, class) per block into a zeroed gradient.
+// Backward, other factors (config 5's 133x183 -> 530x730): seg_loss_bwd_xpass_kernel +
+//   seg_loss_bwd_ypass_kernel, a separable fixed-order contraction: deterministic, no atomics.
 #include <algorithm>
 
 #include "common.h"
 
 namespace {
-constexpr int TY = 4, TX = 64;
 constexpr int MAXC = 64;
 
 DFM_INLINE void src_idx(int dst, int in, int out, int& i0, int& i1, float& l1) {
@@ -122,37 +121,62 @@ __global__ void seg_loss_sum_kernel(int nblk, const float* __restrict__ part, fl
   }
 }
 
-__global__ void zero_kernel(long n, float* __restrict__ p) {
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) p[i] = 0.f;
+
+// ---- backward, any upsampling factor (h <= H, w <= W): separable and deterministic, no atomics.
+// x-pass: a block owns PJ low-res columns of RY label rows; its threads form the scaled
+//   (softmax - onehot) residual of every pixel whose x-taps touch those columns (a span of PX
+//   pixels: the owned columns plus one low-res column either side, recomputed by the neighbouring
+//   block) into LDS, then each (row, column, class) sums its pixels in ascending x:
+//   rx[b][y][j][c] = sum_x wx(x, j) d(b, y, x, c).
+// y-pass: dlogits[b][i][j][c] = sum_y wy(y, i) rx[b][y][j][c], ascending y. Every output element is
+// a fixed-order sum, so the gradient is bitwise reproducible (the integer-factor path below is the
+// faster special case of the same contraction).
+constexpr int XP_NT = 256;
+
+// first pixel index whose source coordinate can reach low-res index j (a conservative lower bound
+// under the src_idx rounding; callers then test each pixel's taps exactly)
+DFM_INLINE int first_pixel(int j, int in, int out) {
+  const float inv = (float)out / (float)in;
+  return max(0, (int)floorf(((float)j + 0.5f) * inv - 0.5f) - 2);
 }
 
-
 template <typename T>
-__global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, int ncls, const T* __restrict__ lg,
-                                                           int H, int W, const long* __restrict__ label, int ignore,
-                                                           const float* __restrict__ loss_out,
-                                                           const float* __restrict__ gscale, float* __restrict__ dlg,
-                                                           int pcmax) {
-  extern __shared__ __attribute__((aligned(16))) float gt[];  // [TY*TX][ncls+1], then rx
-  const int GLD = ncls + 1;
-  const int tiles_x = (W + TX - 1) / TX, tiles_y = (H + TY - 1) / TY;
+__global__ __launch_bounds__(XP_NT) void seg_loss_bwd_xpass_kernel(int B, int h, int w, int ncls,
+                                                                    const T* __restrict__ lg, int H, int W,
+                                                                    const long* __restrict__ label, int ignore,
+                                                                    const float* __restrict__ loss_out,
+                                                                    const float* __restrict__ gscale,
+                                                                    float* __restrict__ rx, int RY, int PJ) {
+  extern __shared__ __attribute__((aligned(16))) float res[];  // [XP_NT][ncls + 1]
+  const int GLD = ncls + 1, PX = XP_NT / RY;
+  const int nj = (w + PJ - 1) / PJ, ny = (H + RY - 1) / RY;
   int bid = blockIdx.x;
-  const int tx = bid % tiles_x; bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int y0 = ty * TY, x0 = tx * TX;
-  const int ny = min(TY, H - y0), nx = min(TX, W - x0);
+  const int jc = bid % nj; bid /= nj;
+  const int yc = bid % ny;
+  const int b = bid / ny;
+  const int j0 = jc * PJ, j1 = min(w, j0 + PJ);  // owned columns [j0, j1)
+  const int xa = first_pixel(j0 - 1, w, W);      // pixels whose taps reach j0 start at src >= j0 - 1
   const float inv = (gscale ? gscale[0] : 1.f) / fmaxf(loss_out[1], 1.f);
   const bool vec = ncls % 8 == 0 && ((uintptr_t)lg & 15) == 0;
-  // phase 1: per-pixel d loss / d upsampled logits
+  __shared__ int tj0[XP_NT], tj1[XP_NT];
+  __shared__ float tw0[XP_NT], tw1[XP_NT];
+  __shared__ int jlo[XP_NT], jhi[XP_NT];
   {
-    const int py = threadIdx.x / TX, px = threadIdx.x % TX;
-    float* row = gt + threadIdx.x * GLD;
-    const int y = y0 + py, x = x0 + px;
+    const int py = threadIdx.x / PX, px = threadIdx.x % PX;
+    const int y = yc * RY + py, x = xa + px;
+    float* row = res + threadIdx.x * GLD;
+    int i0 = -1, i1 = -1;
+    float l1 = 0.f;
+    bool touch = false;
+    if (y < H && x < W) {
+      src_idx(x, w, W, i0, i1, l1);
+      touch = (i0 >= j0 && i0 < j1) || (i1 >= j0 && i1 < j1);
+    }
+    tj0[threadIdx.x] = i0; tj1[threadIdx.x] = i1;
+    tw0[threadIdx.x] = 1.f - l1; tw1[threadIdx.x] = l1;
     long lab = -1;
-    if (py < ny && px < nx) lab = label[((long)b * H + y) * W + x];
-    const bool valid = lab != ignore && lab >= 0 && lab < ncls;
-    if (valid) {
+    if (touch) lab = label[((long)b * H + y) * W + x];
+    if (lab != ignore && lab >= 0 && lab < ncls) {
       float z[MAXC];
       interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
       float m = -INFINITY;
@@ -173,67 +197,66 @@ __global__ __launch_bounds__(256) void seg_loss_bwd_kernel(int B, int h, int w, 
     }
   }
   __syncthreads();
-  // phase 2 (separable): (a) x-reduction of each pixel row onto the patch's low-res columns,
-  // (b) y-reduction onto its low-res rows; every pixel has <= 2 taps per axis.
-  int a0, a1, b0, b1, t0;
-  float tl;
-  src_idx(y0, h, H, a0, t0, tl);
-  src_idx(y0 + ny - 1, h, H, t0, a1, tl);
-  src_idx(x0, w, W, b0, t0, tl);
-  src_idx(x0 + nx - 1, w, W, t0, b1, tl);
-  const int pr = a1 - a0 + 1, pc = b1 - b0 + 1;
-  float* rx = gt + TY * TX * GLD;                      // [TY][pcmax][GLD]
-  __shared__ int xj0[TX], xj1[TX], yi0[TY], yi1[TY];   // taps relative to b0 / a0
-  __shared__ float xw0[TX], xw1[TX], yw0[TY], yw1[TY];
-  __shared__ int jlo[TX + 2], jhi[TX + 2];
-  if (threadIdx.x < nx) {
-    int i0, i1;
-    float l1;
-    src_idx(x0 + threadIdx.x, w, W, i0, i1, l1);
-    xj0[threadIdx.x] = i0 - b0; xj1[threadIdx.x] = i1 - b0;
-    xw0[threadIdx.x] = 1.f - l1; xw1[threadIdx.x] = l1;
-  }
-  if (threadIdx.x >= 64 && threadIdx.x < 64 + ny) {
-    const int py = threadIdx.x - 64;
-    int i0, i1;
-    float l1;
-    src_idx(y0 + py, h, H, i0, i1, l1);
-    yi0[py] = i0 - a0; yi1[py] = i1 - a0;
-    yw0[py] = 1.f - l1; yw1[py] = l1;
-  }
-  __syncthreads();
-  if (threadIdx.x < pc) {  // pixel-column range touching low-res column jj (taps are monotone in px)
-    const int jj = threadIdx.x;
-    int lo = nx, hi = -1;
-    for (int px = 0; px < nx; ++px)
-      if (xj0[px] == jj || xj1[px] == jj) {
+  if (threadIdx.x < j1 - j0) {  // pixel range of owned column j (taps are monotone in x)
+    const int j = j0 + threadIdx.x;
+    int lo = PX, hi = -1;
+    for (int px = 0; px < PX; ++px)
+      if (tj0[px] == j || tj1[px] == j) {
         lo = min(lo, px);
         hi = px;
       }
-    jlo[jj] = lo;
-    jhi[jj] = hi;
+    jlo[threadIdx.x] = lo;
+    jhi[threadIdx.x] = hi;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < ny * pc * ncls; e += 256) {
-    const int c = e % ncls, t = e / ncls, jj = t % pc, py = t / pc;
+  const int pj = j1 - j0;
+  for (int e = threadIdx.x; e < RY * pj * ncls; e += XP_NT) {
+    const int c = e % ncls, t = e / ncls, jj = t % pj, py = t / pj;
+    const int y = yc * RY + py;
+    if (y >= H) continue;
+    const int j = j0 + jj;
     float r = 0.f;
-    const float* grow = gt + (py * TX) * GLD + c;
     for (int px = jlo[jj]; px <= jhi[jj]; ++px) {
-      const float wx = (xj0[px] == jj ? xw0[px] : 0.f) + (xj1[px] == jj ? xw1[px] : 0.f);
-      r = fmaf(wx, grow[px * GLD], r);
+      const int q = py * PX + px;
+      const float wx = (tj0[q] == j ? tw0[q] : 0.f) + (tj1[q] == j ? tw1[q] : 0.f);
+      r = fmaf(wx, res[q * GLD + c], r);
     }
-    rx[(py * pcmax + jj) * GLD + c] = r;
+    rx[(((long)b * H + y) * w + j) * ncls + c] = r;
   }
-  __syncthreads();
-  for (int e = threadIdx.x; e < pr * pc * ncls; e += 256) {
-    const int c = e % ncls, t = e / ncls, jj = t % pc, ii = t / pc;
+}
+
+__global__ void seg_loss_bwd_ypass_kernel(int B, int h, int w, int ncls, int H, const float* __restrict__ rx,
+                                          float* __restrict__ dlg) {
+  const long n = (long)B * h * w * ncls;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const long jc = e % ((long)w * ncls);  // (j, c)
+    const long bi = e / ((long)w * ncls);
+    const int i = bi % h, b = bi / h;
     float acc = 0.f;
-    for (int py = 0; py < ny; ++py) {
-      const float wy = (yi0[py] == ii ? yw0[py] : 0.f) + (yi1[py] == ii ? yw1[py] : 0.f);
-      acc = fmaf(wy, rx[(py * pcmax + jj) * GLD + c], acc);
+    for (int y = first_pixel(i - 1, h, H); y < H; ++y) {
+      int i0, i1;
+      float l1;
+      src_idx(y, h, H, i0, i1, l1);
+      if (i0 > i) break;  // taps are monotone in y
+      const float wy = (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+      if (i0 == i || i1 == i) acc = fmaf(wy, rx[((long)b * H + y) * w * ncls + jc], acc);
     }
-    if (acc != 0.f) atomicAdd(&dlg[(((long)b * h + a0 + ii) * w + b0 + jj) * ncls + c], acc);
+    dlg[e] = acc;
   }
+}
+
+// (rows per x-pass block, owned columns per block) for a W / w ratio: the touched pixel span of PJ
+// columns, (PJ + 1) W / w + 6 pixels (rounding margins included), must fit the PX = 256 / RY lanes
+bool xpass_shape(int w, int W, int& RY, int& PJ) {
+  for (RY = 4; RY >= 1; RY /= 2) {
+    const int PX = XP_NT / RY;
+    PJ = (int)((double)(PX - 6) * w / W) - 1;
+    if (PJ >= 1) {
+      PJ = std::min(PJ, w);
+      return true;
+    }
+  }
+  return false;
 }
 
 // ---- backward for an integer upsampling factor S (H = S h, W = S w, S even, S*S <= 64): the label
@@ -379,10 +402,11 @@ extern "C" size_t dfm_seg_loss_workspace(int B, int H, int W) {
   return (size_t)LOSS_BLOCKS * 2 * sizeof(float);
 }
 
-/* backward workspace of the integer-scale tile path: corner partials of every tile (0 otherwise) */
+/* backward workspace: the integer-scale path's corner partials of every tile, otherwise the x-pass's
+   column-reduced rows rx [B][H][w][ncls] */
 extern "C" size_t dfm_seg_loss_bwd_workspace(int B, int h, int w, int ncls, int H, int W) {
-  if (!tile_scale(h, w, H, W)) return 0;
-  return (size_t)B * (h + 1) * (w + 1) * 4 * ncls * sizeof(float);
+  if (tile_scale(h, w, H, W)) return (size_t)B * (h + 1) * (w + 1) * 4 * ncls * sizeof(float);
+  return (size_t)B * H * w * ncls * sizeof(float);
 }
 
 extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
@@ -426,29 +450,34 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
     return launch_bwd_tiles<float>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, gscale,
                                    (float*)workspace, dlogits, s);
   }
-  // other scales: the general tile kernel (float atomics into a zeroed gradient)
-  DFM_LAUNCH(zero_kernel, dim3(min(4096L, (nl + 255) / 256)), dim3(256), 0, s, nl, dlogits);
-  DFM_LAUNCH_CHECK();
-  const unsigned nblk = B * ((H + TY - 1) / TY) * ((W + TX - 1) / TX);
-  // low-res columns one TX-wide pixel tile can touch (+2 for the taps at both ends)
-  const int pcmax = std::min(TX + 2, (int)(((long)TX * w + W - 1) / W) + 3);
-  const size_t lds = ((size_t)TY * TX + (size_t)TY * pcmax) * (ncls + 1) * sizeof(float);
-  if (lds > 64 * 1024) {  // only small upsampling ratios need more than the default
-    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<bf16_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+  // other scales: separable x-pass into the workspace, then the y-pass
+  DFM_CHECK_ARG(workspace, "dfm_seg_loss_bwd: needs dfm_seg_loss_bwd_workspace bytes of workspace");
+  int RY, PJ;
+  DFM_CHECK_ARG(xpass_shape(w, W, RY, PJ), "dfm_seg_loss_bwd: upsampling ratio W / w above ~120");
+  float* rx = (float*)workspace;
+  const unsigned nblk = (unsigned)((long)B * ((H + RY - 1) / RY) * ((w + PJ - 1) / PJ));
+  const size_t lds = (size_t)XP_NT * (ncls + 1) * sizeof(float);
+  if (lds > 64 * 1024) {
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<bf16_t>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<f16_t>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<float>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipGetLastError();  // a refused attribute must not read as this launch's error
   }
   if (dtype == DFM_BF16)
-    DFM_LAUNCH(seg_loss_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const bf16_t*)logits,
-                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
+    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<bf16_t>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+               (const bf16_t*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
   else if (dtype == DFM_F16)
-    DFM_LAUNCH(seg_loss_bwd_kernel<f16_t>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const f16_t*)logits,
-                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
+    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<f16_t>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+               (const f16_t*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
   else
-    DFM_LAUNCH(seg_loss_bwd_kernel<float>, dim3(nblk), dim3(256), lds, s, B, h, w, ncls, (const float*)logits,
-                       H, W, label, ignore, loss_out, gscale, dlogits, pcmax);
+    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<float>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+               (const float*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
+  DFM_LAUNCH_CHECK();
+  DFM_LAUNCH(seg_loss_bwd_ypass_kernel, dim3((unsigned)std::min(8192L, (nl + 255) / 256)), dim3(256), 0, s, B, h,
+             w, ncls, H, (const float*)rx, dlogits);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

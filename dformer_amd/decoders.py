@@ -16,8 +16,23 @@ from . import kernels as K
 from .functional import gslot, gslot2, wcast
 
 
+# Test-only: with an initialised one-rank process group, take every collective branch (SyncBN
+# all-gather / all-reduce, bucketed gradient all-reduce, loss all-reduce) as if world > 1, so the
+# multi-rank code runs (and is captured into HIP graphs) on a single GPU (tests/test_graph_gpu.py).
+FORCE_COLLECTIVES = False
+
+
+def collectives_on(world=None):
+    """True when the data-parallel collective branches run: world > 1, or FORCE_COLLECTIVES with an
+    initialised process group."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    w = dist.get_world_size() if world is None else world
+    return w > 1 or FORCE_COLLECTIVES
+
+
 def _allreduce(t, sync):
-    if sync and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if sync and collectives_on():
         dist.all_reduce(t)
     return t
 
@@ -26,23 +41,6 @@ def _world(sync):
     if sync and dist.is_available() and dist.is_initialized():
         return dist.get_world_size()
     return 1
-
-
-def merge_bn_stats(parts, counts):
-    """Chan-merge per-shard shifted BN statistics into one (0, M2, mean) triple.
-
-    parts: [S, 3, C] float32 = (sum (x-K_s), sum (x-K_s)^2, K_s) per shard; counts: [S] rows.
-    Returns [3, C] whose finalize gives the statistics of the union of the shards (what
-    SyncBatchNorm's all_gather of (mean, invstd, count) computes, torch/nn/modules/_functions.py)."""
-    n = counts.to(torch.float64).view(-1, 1)
-    s1, s2, k = parts[:, 0].double(), parts[:, 1].double(), parts[:, 2].double()
-    d = s1 / n
-    mean_s = k + d
-    m2_s = s2 - s1 * d
-    N = n.sum()
-    mean = (n * mean_s).sum(0) / N
-    m2 = (m2_s + n * (mean_s - mean) ** 2).sum(0)
-    return torch.stack([torch.zeros_like(mean), m2, mean]).float()
 
 
 # Per-rank row counts of a SyncBN batch, keyed by (local rows, world): data-parallel ranks see the
@@ -54,21 +52,23 @@ _GLOBAL_TOTAL = {}
 def bn_batch_stats(x, bn, sync):
     """Train-mode BatchNorm / SyncBatchNorm statistics of NHWC rows x: (mean, rstd, count), with the
     running statistics updated like torch (momentum, unbiased variance). With SyncBN over a
-    multi-rank group the per-rank shifted sums are all-gathered and Chan-merged."""
+    multi-rank group the per-rank shifted sums are all-gathered into one [world, 3, C] buffer and
+    merged on the device (K.bn_merge; torch SyncBatchNorm all-gathers (mean, invstd, count) the
+    same way, torch/nn/modules/_functions.py)."""
     st = K.bn_stats(x)
     rows = x.shape[0]
     world = _world(sync)
     count = rows
-    if world > 1:
-        gathered = [torch.empty_like(st) for _ in range(world)]
-        dist.all_gather(gathered, st)
+    if sync and collectives_on(world):
+        gathered = torch.empty((world,) + tuple(st.shape), device=st.device, dtype=st.dtype)
+        dist.all_gather_into_tensor(gathered, st)
         counts = _GLOBAL_ROWS.get((rows, world))
         if counts is None:  # first batch of this shape: exchange the per-rank row counts once
             cnt = torch.tensor([float(rows)], device=x.device)
-            parts = [torch.empty_like(cnt) for _ in range(world)]
-            dist.all_gather(parts, cnt)
-            counts = _GLOBAL_ROWS[(rows, world)] = torch.cat(parts)
-        st = merge_bn_stats(torch.stack(gathered), counts)
+            counts = torch.empty(world, device=x.device)
+            dist.all_gather_into_tensor(counts, cnt)
+            _GLOBAL_ROWS[(rows, world)] = counts
+        st = K.bn_merge(gathered, counts)
         total = _GLOBAL_TOTAL.get((rows, world))
         if total is None:  # one host read per batch shape, not one per BN layer per step
             total = _GLOBAL_TOTAL[(rows, world)] = int(counts.sum().item())

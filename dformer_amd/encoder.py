@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .decoders import _allreduce, bn_batch_stats
+from .decoders import _allreduce, bn_batch_stats, collectives_on
 from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, gslot, invalidate_weights, register_side_stream
 
 _EMPTY = {}
@@ -362,8 +362,7 @@ class DFormer(nn.Module):
                  windows=(7, 7, 7, 7), norm_cfg=None, mlp_ratios=(8, 8, 4, 4), num_heads=(2, 4, 10, 16),
                  last_block=(50, 50, 50, 50), drop_path_rate=0.1, init_cfg=None):
         super().__init__()
-        syncbn = bool(norm_cfg) and norm_cfg.get("type") == "SyncBN" and torch.distributed.is_initialized() \
-            and torch.distributed.get_world_size() > 1
+        syncbn = bool(norm_cfg) and norm_cfg.get("type") == "SyncBN" and collectives_on()
         self.depths = depths
         self.dims = dims
         self.mlp_ratios = mlp_ratios

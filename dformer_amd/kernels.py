@@ -486,6 +486,18 @@ def bn_finalize(stats, count, eps, momentum, running_mean=None, running_var=None
     return mean, rstd
 
 
+def bn_merge(parts, counts):
+    """SyncBN: all-gathered per-rank bn_stats triples [S, 3, C] + per-rank rows [S] (float32) -> the
+    union's triple [3, C], shifted by rank 0's K (fixed order; identity for S = 1)."""
+    S, three, C = parts.shape
+    if three != 3 or counts.shape != (S,) or parts.dtype != torch.float32 or counts.dtype != torch.float32:
+        raise ValueError(f"bn_merge: parts {tuple(parts.shape)} {parts.dtype}, counts {tuple(counts.shape)}")
+    parts, counts = parts.contiguous(), counts.contiguous()
+    st = torch.empty(3, C, device=parts.device, dtype=torch.float32)
+    check(lib.dfm_bn_merge(S, C, ptr(parts), ptr(counts), ptr(st), stream()), "dfm_bn_merge")
+    return st
+
+
 def bn_apply(x, mean, rstd, gamma, beta, res=None, act=0, out=None):
     rows, C = x.shape
     if out is None:

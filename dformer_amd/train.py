@@ -16,6 +16,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
+from .decoders import collectives_on
 from .functional import invalidate_weights, join_streams, register_grad_slot, register_shadow
 
 
@@ -162,7 +163,7 @@ class GradBuckets:
         self.pending[bi] -= 1
         if self.pending[bi] == 0:
             self._flush(bi)
-            if self.world > 1:
+            if collectives_on(self.world):
                 # the bucket mixes slots written on the main stream, the depth-branch ConvFFN stream
                 # and the weight-gradient stream, and this hook runs on whichever stream autograd
                 # replays the last AccumulateGrad on: wait for all of them before RCCL reads it
@@ -194,7 +195,7 @@ class GradBuckets:
                         g.grad[off:off + k].zero_()
                         self.unfired.append((g, off, k))
                 self._flush(bi)
-                if self.world > 1:
+                if collectives_on(self.world):
                     join_streams(self.main_stream)
                     self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
@@ -357,7 +358,7 @@ class FusedAdamW:
 
 def all_reduce_mean(t, world):
     """pyt_utils.all_reduce_tensor (SUM then /world), async-free for the scalar loss."""
-    if world > 1:
+    if collectives_on(world):
         t = t.clone()
         dist.all_reduce(t)
         t = t / world

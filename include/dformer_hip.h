@@ -218,13 +218,17 @@ int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, const void* 
  * mmcv ConvModule norm / nn.BatchNorm2d / SyncBatchNorm over NHWC rows (ham_head.py:204-220,
  * MLPDecoder.py:53). stats: float32 [3][C] = (sum (x-K), sum (x-K)^2, K) with the shift K = x[row 0]
  * (no E[x^2]-E[x]^2 cancellation when |mean| >> std); finalize: mean = K + S1/n,
- * var = S2/n - (S1/n)^2. For SyncBN the caller merges per-rank (n, mean, M2) (Chan) into
- * (0, M2, mean). apply: y = act((x - mean) * rstd * gamma + beta) [+ res] ; mean/rstd float32 [C]. */
+ * var = S2/n - (S1/n)^2. For SyncBN (torch SyncBatchNorm's all_gather of per-rank statistics,
+ * torch/nn/modules/_functions.py) the all-gathered per-rank triples [shards][3][C] are merged on the
+ * device by dfm_bn_merge (counts: float32 [shards] rows per rank) into one triple shifted by rank 0's K
+ * (fp64, fixed rank order; exact identity for one shard), which dfm_bn_finalize takes with the total
+ * count. apply: y = act((x - mean) * rstd * gamma + beta) [+ res] ; mean/rstd float32 [C]. */
 size_t dfm_bn_workspace(long rows, int C);
 int dfm_bn_stats(int dtype, long rows, int C, const void* x, long ldx, float* stats, void* workspace,
                  dfm_stream_t stream);
 int dfm_bn_finalize(int C, const float* stats, double count, float eps, float momentum, float* mean,
                     float* rstd, float* running_mean, float* running_var, dfm_stream_t stream);
+int dfm_bn_merge(int shards, int C, const float* parts, const float* counts, float* stats, dfm_stream_t stream);
 int dfm_bn_apply(int dtype, long rows, int C, const void* x, long ldx, const float* mean, const float* rstd,
                  const float* gamma, const float* beta, const void* res, long ldres, int act, void* y,
                  long ldy, dfm_stream_t stream);
@@ -309,9 +313,10 @@ size_t dfm_seg_loss_workspace(int B, int H, int W);
 int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                      const long* label, int ignore, float* lse, float* loss_out, void* workspace,
                      dfm_stream_t stream);
-/* bwd workspace: dfm_seg_loss_bwd_workspace bytes (0 = none needed). With an integer upsampling
- * factor (H = S h, W = S w, S in {2, 4, 8}) the backward is deterministic (fixed-order sums, no
- * atomics); other factors fall back to float atomics. */
+/* bwd workspace: dfm_seg_loss_bwd_workspace bytes (required). Every upsampling factor is
+ * deterministic (fixed-order sums, no atomics): an integer factor (H = S h, W = S w, S in {2, 4, 8})
+ * takes per-tile corner partials + a 4-way gather, any other factor (h <= H, w <= W, W / w up to
+ * ~120) a separable x-pass into rx [B][H][w][ncls] float32 and a y-pass. */
 size_t dfm_seg_loss_bwd_workspace(int B, int h, int w, int ncls, int H, int W);
 int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
                      const long* label, int ignore, const float* lse, const float* loss_out,

@@ -201,10 +201,22 @@ def test_grad_buckets_real_model_world2_gloo():
     assert len({n for *_, n in res}) == 1 and res[0][3] >= 4  # 119 MB fp32 of grads in ~25 MB buckets
 
 
+def _bn_merge_model(parts, counts):
+    """The algorithm of dfm_bn_merge (elementwise.hip bn_merge_kernel), restated in fp64: re-shift every
+    rank's (S1, S2, K) onto rank 0's K and sum in rank order."""
+    k0 = parts[0, 2].double()
+    s1 = torch.zeros_like(k0)
+    s2 = torch.zeros_like(k0)
+    for p, n in zip(parts.double(), counts.double()):
+        d = p[2] - k0
+        s1 = s1 + p[0] + n * d
+        s2 = s2 + p[1] + 2 * d * p[0] + n * d * d
+    return torch.stack([s1, s2, k0]).float()
+
+
 def test_syncbn_merge_matches_full_batch():
-    """SyncBN's Chan merge of per-shard shifted sums (decoders.merge_bn_stats) = full-batch
-    statistics, for uneven shards and |mean| >> std."""
-    from dformer_amd.decoders import merge_bn_stats
+    """SyncBN's merge of per-shard shifted sums (the dfm_bn_merge formula) = full-batch statistics,
+    for uneven shards and |mean| >> std; one shard merges to itself bit for bit."""
     torch.manual_seed(0)
     C = 24
     x = torch.randn(5000, C, dtype=torch.float64) * 0.3 + torch.linspace(-50, 80, C, dtype=torch.float64)
@@ -216,9 +228,11 @@ def test_syncbn_merge_matches_full_batch():
         d = xs - k
         parts.append(torch.stack([d.sum(0), (d * d).sum(0), k]).float())
         counts.append(b - a)
-    st = merge_bn_stats(torch.stack(parts), torch.tensor(counts, dtype=torch.float32)).double()
+    st = _bn_merge_model(torch.stack(parts), torch.tensor(counts, dtype=torch.float32)).double()
     n = x.shape[0]
     mean = st[2] + st[0] / n
     var = st[1] / n - (st[0] / n) ** 2
     assert torch.allclose(mean, x.mean(0), rtol=1e-6, atol=1e-5)
     assert torch.allclose(var, x.var(0, unbiased=False), rtol=1e-4, atol=1e-6)
+    one = _bn_merge_model(parts[0][None], torch.tensor([700.0]))
+    assert torch.equal(one, parts[0])

@@ -78,3 +78,85 @@ def test_graphed_steps_match_eager(decoder):
     torch.cuda.synchronize()
     for b0, gr in zip(before, ob.groups):
         assert torch.equal(b0, gr.flat)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_forced_collectives_one_rank_nccl():
+    """The world > 1 code on the GPU with one rank: a 1-rank RCCL group and decoders.FORCE_COLLECTIVES
+    send every SyncBN statistic through all_gather_into_tensor + the device merge, every BN backward
+    statistic, gradient bucket and the loss through all_reduce. A Tiny + ham step run that way eagerly
+    and as a captured GraphedTrainStep must agree bit for bit, and both with the plain world-1 path
+    (a one-rank sum and a one-shard merge are exact identities). utils/train.py:238-243,
+    utils/engine/engine.py:53-66 (the reference's DDP + SyncBN setup)."""
+    import torch.distributed as dist
+    import bench
+    from dformer_amd import decoders as D
+    from dformer_amd.segmentor import EncoderDecoder
+    from dformer_amd.train import FusedAdamW, GraphedTrainStep, train_step
+    dev = torch.device("cuda", 0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    D.FORCE_COLLECTIVES = True
+    try:
+        cfg = bench.make_cfg("DFormer-Tiny", "ham")
+        cfg["drop_path_rate"] = 0.0
+        models = []
+        for sync in (True, True, False):
+            torch.manual_seed(3)
+            m = EncoderDecoder(cfg=cfg, syncbn=sync)
+            m.decode_head.dropout_ratio = 0.0
+            models.append(m.to(dev).set_compute_dtype(torch.bfloat16))
+        ma, mb, mc = models
+        assert sum(isinstance(x, torch.nn.SyncBatchNorm) for x in ma.modules()) > 0
+        assert not any(isinstance(x, torch.nn.SyncBatchNorm) for x in mc.modules())
+        g = torch.Generator(device=dev)
+        g.manual_seed(11)
+        bases = torch.rand(2, 512, 64, device=dev, generator=g)
+        bases = bases / bases.norm(dim=1, keepdim=True)
+        opts = []
+        for m in models:
+            m.decode_head.hamburger.ham.injected_bases = bases
+            m.return_logits = False
+            m.train()
+            opts.append(FusedAdamW(m, lr=1e-3, weight_decay=cfg.weight_decay, world=1, compute_dtype=torch.bfloat16))
+        oa, ob, oc = opts
+        rgb, dep, lab = bench.synthetic_batch(2, 240, 320, cfg.num_classes, dev, 5)
+        calls = {"all_reduce": 0, "all_gather_into_tensor": 0}
+        real = {k: getattr(dist, k) for k in calls}
+
+        def counting(name):
+            def f(*a, **k):
+                calls[name] += 1
+                return real[name](*a, **k)
+            return f
+        for k in calls:
+            setattr(dist, k, counting(k))
+        try:
+            la = [train_step(ma, oa, rgb, dep, lab).item() for _ in range(5)]
+        finally:
+            for k, f in real.items():
+                setattr(dist, k, f)
+        assert calls["all_reduce"] > 0 and calls["all_gather_into_tensor"] > 0, calls
+        gstep = GraphedTrainStep(mb, ob, rgb, dep, lab, warmup=2)
+        lb = [gstep().item() for _ in range(3)]
+        D.FORCE_COLLECTIVES = False
+        lc = [train_step(mc, oc, rgb, dep, lab).item() for _ in range(5)]
+        assert la[2:] == lb, (la, lb)
+        assert la == lc, (la, lc)
+        for ga, gb, gc in zip(oa.groups, ob.groups, oc.groups):
+            assert torch.equal(ga.flat, gb.flat) and torch.equal(ga.m, gb.m) and torch.equal(ga.v, gb.v)
+            assert torch.equal(ga.flat, gc.flat) and torch.equal(ga.v, gc.v)
+        for (ka, ba), (kc, bc) in zip(ma.state_dict().items(), mc.state_dict().items()):
+            assert ka == kc and torch.equal(ba, bc), ka
+    finally:
+        D.FORCE_COLLECTIVES = False
+        D._GLOBAL_ROWS.clear()
+        D._GLOBAL_TOTAL.clear()
+        dist.destroy_process_group()

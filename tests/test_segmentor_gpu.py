@@ -338,14 +338,15 @@ def test_segmentor_bf16_vs_reference_envelope(name, arch, dec, ncls):
 @pytest.mark.gpu
 def test_syncbn_two_half_batches_equal_full_batch():
     """SyncBN statistics as the DP path forms them: the library's shifted (sum, sumsq, shift) of two
-    half-batches, Chan-merged (decoders.merge_bn_stats), finalize to the full batch's mean / var."""
+    half-batches, merged on the device (K.bn_merge), finalize to the full batch's mean / var; a single
+    shard merges to itself bit for bit (what a one-rank SyncBN group relies on)."""
     from dformer_amd import kernels as K
-    from dformer_amd.decoders import merge_bn_stats
     torch.manual_seed(0)
     x = (torch.randn(60000, 128, device="cuda") * 0.7 + torch.linspace(-20, 40, 128, device="cuda"))
     halves = [x[:26000], x[26000:]]
     parts = torch.stack([K.bn_stats(h) for h in halves])
-    st = merge_bn_stats(parts, torch.tensor([26000.0, 34000.0], device="cuda"))
+    st = K.bn_merge(parts, torch.tensor([26000.0, 34000.0], device="cuda"))
+    assert torch.equal(K.bn_merge(parts[:1], torch.tensor([26000.0], device="cuda")), parts[0])
     rm, rv = torch.zeros(128, device="cuda"), torch.ones(128, device="cuda")
     mean, rstd = K.bn_finalize(st, 60000, 1e-5, 0.1, rm, rv)
     full_mean, full_rstd = K.bn_finalize(K.bn_stats(x), 60000, 1e-5, 0.1)
