@@ -266,7 +266,6 @@ def main():
     # captures the SyncBN / bucket / loss collectives through a one-rank group; DFM_GRAPH=0 disables):
     # the whole step is captured once and replayed, so ~2.3k kernel launches cost one graph launch
     use_graph = not args.eager and os.environ.get("DFM_GRAPH", "1") != "0"
-    use_graph = use_graph and opt.scaler is None  # the fp16 loss scaler reads its overflow flag on the host
     if use_graph:
         step = GraphedTrainStep(model, opt, rgb, dep, lab)
     torch.cuda.synchronize()

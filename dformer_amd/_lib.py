@@ -100,6 +100,8 @@ _SIGS = {
     "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, c_int,
                           P]),
     "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),
+    "dfm_adamw_amp": (c_int, [c_long, P, P, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),
+    "dfm_loss_scale_update": (c_int, [P, P, c_float, c_float, c_int, P]),
     "dfm_convffn_supported": (c_int, [c_int, c_int, c_int]),
     "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
                                 P, P, c_long, P, c_long, P]),

@@ -489,12 +489,18 @@ __global__ void adamw_kernel(long n, float* __restrict__ p, const float* __restr
   }
 }
 // Same update with lr and step read from device memory (hyper = [lr, step]), so a captured HIP
-// graph replays every optimizer step without host-baked scalars.
+// graph replays every optimizer step without host-baked scalars. With the fp16 loss scaler's device
+// state amp = {scale, growth_tracker, applied_steps, skipped} and overflow flag: the step is skipped
+// when flag[0] is set (GradScaler.step), gradients are unscaled by 1/scale and the step count is
+// amp[2] + 1 (torch's AdamW counts applied steps only).
 template <typename TC>
 __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                  float* __restrict__ v, const float* __restrict__ hyper, float b1, float b2,
-                                 float eps, float wd, float gscale, TC* __restrict__ copy) {
-  const float lr = hyper[0], step = hyper[1];
+                                 float eps, float wd, float gscale, TC* __restrict__ copy,
+                                 const float* __restrict__ amp, const int* __restrict__ flag) {
+  if (flag && flag[0]) return;
+  const float lr = hyper[0], step = amp ? amp[2] + 1.f : hyper[1];
+  if (amp) gscale /= amp[0];
   const float bc1 = 1.f - powf(b1, step), bc2_sqrt = sqrtf(1.f - powf(b2, step));
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
@@ -508,6 +514,26 @@ __global__ void adamw_dev_kernel(long n, float* __restrict__ p, const float* __r
     if (copy) copy[i] = Num<TC>::from_f(pi);
   }
 }
+// GradScaler.update (torch/amp/grad_scaler.py _amp_update_scale_) on the device state, after the
+// step's AdamW launches have read it; clears the overflow flag for the next step. One lane.
+__global__ void loss_scale_update_kernel(float* __restrict__ amp, int* __restrict__ flag, float growth,
+                                         float backoff, int interval) {
+  if (threadIdx.x != 0) return;
+  if (flag[0]) {
+    amp[0] *= backoff;
+    amp[1] = 0.f;
+    amp[3] += 1.f;
+  } else {
+    amp[2] += 1.f;
+    amp[1] += 1.f;
+    if (amp[1] >= (float)interval) {
+      amp[0] *= growth;
+      amp[1] = 0.f;
+    }
+  }
+  flag[0] = 0;
+}
+
 // o1 = src * m1, o2 = src * m2 (the two products of one gradient against the two factors of
 // an elementwise product, DFormer.py:134-135: d(q*a) -> dq = d*a, da = d*q): one read of src.
 template <typename T>
@@ -798,10 +824,35 @@ extern "C" int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* 
   if (n == 0) return DFM_OK;
   if (copy_dtype == DFM_F16)
     DFM_LAUNCH(adamw_dev_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
-               beta1, beta2, eps, wd, gscale, (f16_t*)copy);
+               beta1, beta2, eps, wd, gscale, (f16_t*)copy, nullptr, nullptr);
   else
     DFM_LAUNCH(adamw_dev_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
-               beta1, beta2, eps, wd, gscale, (bf16_t*)copy);
+               beta1, beta2, eps, wd, gscale, (bf16_t*)copy, nullptr, nullptr);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_adamw_amp(long n, float* p, const float* g, float* m, float* v, const float* hyper,
+                             const float* amp, const int* flag, float beta1, float beta2, float eps, float wd,
+                             float gscale, void* copy, int copy_dtype, dfm_stream_t stream) {
+  DFM_CHECK_ARG(p && g && m && v && hyper && amp && flag, "dfm_adamw_amp: bad argument");
+  DFM_CHECK_ARG(!copy || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_adamw_amp: bad copy dtype");
+  if (n == 0) return DFM_OK;
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(adamw_dev_kernel<f16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
+               beta1, beta2, eps, wd, gscale, (f16_t*)copy, amp, flag);
+  else
+    DFM_LAUNCH(adamw_dev_kernel<bf16_t>, dim3(ew_grid(n)), dim3(256), 0, (hipStream_t)stream, n, p, g, m, v, hyper,
+               beta1, beta2, eps, wd, gscale, (bf16_t*)copy, amp, flag);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_loss_scale_update(float* amp, int* flag, float growth, float backoff, int interval,
+                                     dfm_stream_t stream) {
+  DFM_CHECK_ARG(amp && flag && interval > 0, "dfm_loss_scale_update: bad argument");
+  DFM_LAUNCH(loss_scale_update_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, amp, flag, growth, backoff,
+             interval);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

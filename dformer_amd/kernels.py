@@ -722,17 +722,27 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
 
 
 # -------------------------------------------------------------------------------------- AdamW
+def loss_scale_update(amp, flag, growth, backoff, interval):
+    check(lib.dfm_loss_scale_update(ptr(amp), ptr(flag), growth, backoff, interval, stream()),
+          "dfm_loss_scale_update")
+
+
 def grad_nonfinite(g, flag):
     """flag (int32 [1], zeroed by the caller) := 1 if any element of g is inf / nan."""
     check(lib.dfm_grad_nonfinite(g.numel(), ptr(g), ptr(flag), stream()), "dfm_grad_nonfinite")
     return flag
 
 
-def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None, hyper=None):
+def adamw(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, bf16_copy=None, hyper=None,
+          amp=None, flag=None):
     """AdamW step; with `hyper` (device float32 [lr, step]) lr and step are read on the device
-    (lr / step arguments ignored) so the launch can live in a replayed HIP graph."""
+    (lr / step arguments ignored) so the launch can live in a replayed HIP graph. With the loss
+    scaler's device state `amp` and overflow `flag` the step is skipped / unscaled on the device."""
     cdt = dtype_code(bf16_copy) if bf16_copy is not None else 0
-    if hyper is not None:
+    if amp is not None:
+        check(lib.dfm_adamw_amp(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(hyper), ptr(amp), ptr(flag), beta1,
+                                beta2, eps, weight_decay, grad_scale, ptr(bf16_copy), cdt, stream()), "dfm_adamw_amp")
+    elif hyper is not None:
         check(lib.dfm_adamw_dev(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(hyper), beta1, beta2, eps,
                                 weight_decay, grad_scale, ptr(bf16_copy), cdt, stream()), "dfm_adamw_dev")
     else:

@@ -207,33 +207,56 @@ class GradBuckets:
 
 class LossScaler:
     """torch.cuda.amp.GradScaler defaults (init 2**16, growth 2.0, backoff 0.5, interval 2000) for
-    the fp16 compute dtype: the loss gradient is seeded with `scale`, the optimizer checks every
-    flat gradient buffer for inf / nan (one kernel per group, one host read per step), skips the
-    update on overflow and unscales by 1/scale otherwise."""
+    the fp16 compute dtype, decided on the device so the fp16 step replays from a captured graph:
+    `state` = float32 {scale, growth_tracker, applied_steps, skipped}. The loss gradient is seeded
+    with a view of state[0]; the optimizer flags inf / nan in every flat gradient buffer
+    (dfm_grad_nonfinite), the AdamW kernels skip the update on overflow and unscale by 1/scale
+    otherwise, and dfm_loss_scale_update applies GradScaler.update and clears the flag. Nothing is
+    read on the host during a step."""
 
     def __init__(self, device, init_scale=2.0 ** 16, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000):
-        self.scale = float(init_scale)
         self.growth_factor, self.backoff_factor, self.growth_interval = growth_factor, backoff_factor, growth_interval
-        self.growth_tracker = 0
+        self.state = torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=device, dtype=torch.float32)
         self.found_inf = torch.zeros(1, device=device, dtype=torch.int32)
-        self.skipped = 0
 
-    def check(self, grads):
-        self.found_inf.zero_()
+    @property
+    def scale(self):
+        return float(self.state[0])
+
+    @property
+    def growth_tracker(self):
+        return int(self.state[1])
+
+    @property
+    def skipped(self):
+        return int(self.state[3])
+
+    def seed(self, loss):
+        """The backward seed scale * d(loss): a view of the device scale, read at replay time."""
+        return self.state[0].view(()).expand_as(loss)
+
+    def flag_nonfinite(self, grads):
         for g in grads:
             K.grad_nonfinite(g, self.found_inf)
-        return bool(self.found_inf.item())
+
+    def update_device(self):
+        K.loss_scale_update(self.state, self.found_inf, self.growth_factor, self.backoff_factor,
+                            self.growth_interval)
 
     def update(self, found_inf):
+        """GradScaler.update on the state from the host (what dfm_loss_scale_update does on the
+        device; used where no device is involved)."""
+        st = self.state
         if found_inf:
-            self.scale *= self.backoff_factor
-            self.growth_tracker = 0
-            self.skipped += 1
+            st[0] *= self.backoff_factor
+            st[1] = 0.0
+            st[3] += 1.0
         else:
-            self.growth_tracker += 1
-            if self.growth_tracker == self.growth_interval:
-                self.scale *= self.growth_factor
-                self.growth_tracker = 0
+            st[2] += 1.0
+            st[1] += 1.0
+            if st[1] >= self.growth_interval:
+                st[0] *= self.growth_factor
+                st[1] = 0.0
 
 
 class FusedAdamW:
@@ -249,6 +272,8 @@ class FusedAdamW:
                        _FlatGroup(no_decay, 0.0, dev, torch.float32, chains)]
         self.lr, self.betas, self.eps = lr, betas, eps
         self.world = world
+        # fp16 compute (BASELINE config 5, the reference's --amp): dynamic loss scaling on the device
+        self.scaler = LossScaler(dev) if compute_dtype == torch.float16 else None
         self.step_count = 0
         # [lr, step] on the device, read by the AdamW kernel: the same arithmetic whether the step
         # runs eagerly (step() refreshes it) or replays from a captured graph (the graph's owner
@@ -262,8 +287,19 @@ class FusedAdamW:
         invalidate_weights()
         for g in self.groups:
             g.register_shadows()
-        # fp16 compute (BASELINE config 5, the reference's --amp): dynamic loss scaling
-        self.scaler = LossScaler(dev) if compute_dtype == torch.float16 else None
+
+    @property
+    def step_count(self):
+        """Applied optimizer steps (torch's AdamW state 'step'). With the fp16 scaler the count lives
+        on the device (an overflowing step is skipped there), so reading it synchronises."""
+        return int(self.scaler.state[2]) if self.scaler is not None else self._steps
+
+    @step_count.setter
+    def step_count(self, v):
+        if self.scaler is not None:
+            self.scaler.state[2] = float(v)
+        else:
+            self._steps = v
 
     def step(self, lr=None):
         join_streams(self.buckets.main_stream)  # every gradient-writing stream is done
@@ -271,25 +307,26 @@ class FusedAdamW:
         for p in self.ungrouped:
             p.grad = None
         gscale = 1.0 / self.world
-        if self.scaler is not None:
-            used = self.scaler.scale  # the scale this step's backward was seeded with
-            inf = self.scaler.check([g.grad for g in self.groups])
-            self.scaler.update(inf)
-            if inf:  # GradScaler.step: the optimizer step is skipped (its step count too)
-                return
-            gscale /= used
-        self.step_count += 1
+        sc = self.scaler
+        if sc is not None:  # GradScaler.unscale_ / step / update, decided on the device
+            sc.flag_nonfinite([g.grad for g in self.groups])
+        else:
+            self._steps += 1
         lr = self.lr if lr is None else lr
         if not self.external_hyper:
             self.hyper[0].fill_(lr)
-            self.hyper[1].fill_(float(self.step_count))
+            if sc is None:
+                self.hyper[1].fill_(float(self._steps))
         # parameters that got no gradient this step: torch.optim.AdamW skips them (no decay, no
         # momentum step), so their value / moments are put back after the flat update
         keep = [(g, off, k, g.flat[off:off + k].clone(), g.m[off:off + k].clone(), g.v[off:off + k].clone())
                 for g, off, k in self.buckets.unfired]
         for g in self.groups:
-            K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, self.step_count,
-                    gscale, g.shadow, hyper=self.hyper)
+            K.adamw(g.flat, g.grad, g.m, g.v, lr, self.betas[0], self.betas[1], self.eps, g.wd, 1, gscale, g.shadow,
+                    hyper=self.hyper, amp=sc.state if sc is not None else None,
+                    flag=sc.found_inf if sc is not None else None)
+        if sc is not None:
+            sc.update_device()
         for g, off, k, p0, m0, v0 in keep:
             g.flat[off:off + k].copy_(p0)
             g.m[off:off + k].copy_(m0)
@@ -377,9 +414,6 @@ class GraphedTrainStep:
     it (true of this package) and no host synchronisation inside the step."""
 
     def __init__(self, model, opt, rgb, depth, label, warmup=2):
-        if opt.scaler is not None:
-            raise ValueError("GraphedTrainStep: the fp16 loss scaler reads its overflow flag on the host "
-                             "(a step may be skipped); run the fp16 step eagerly")
         self.model, self.opt = model, opt
         self.inputs = (rgb, depth, label)
         side = torch.cuda.Stream(device=rgb.device)
@@ -398,14 +432,16 @@ class GraphedTrainStep:
 
     def _set_hyper(self, lr, step):
         self.opt.hyper[0].fill_(self.opt.lr if lr is None else lr)
-        self.opt.hyper[1].fill_(float(step))
+        if step is not None:
+            self.opt.hyper[1].fill_(float(step))
 
     def __call__(self, lr=None):
         """One training step (the first call replays the captured step itself)."""
-        if getattr(self, "_replayed", False):
-            self.opt.step_count += 1
+        amp = self.opt.scaler is not None  # the fp16 step counts its applied steps on the device
+        if getattr(self, "_replayed", False) and not amp:
+            self.opt._steps += 1
         self._replayed = True
-        self._set_hyper(lr, self.opt.step_count)
+        self._set_hyper(lr, None if amp else self.opt._steps)
         self.graph.replay()
         return self.loss
 
@@ -420,8 +456,8 @@ def train_step(model, opt, rgb, depth, label, lr=None):
     loss, _ = model(rgb, depth, label)
     reduce_loss = all_reduce_mean(loss.detach(), opt.world)
     opt.buckets.main_stream = torch.cuda.current_stream() if loss.is_cuda else None
-    if opt.scaler is not None:  # scaler.scale(loss).backward()
-        loss.backward(torch.full_like(loss, opt.scaler.scale))
+    if opt.scaler is not None:  # scaler.scale(loss).backward(), the scale read on the device
+        loss.backward(opt.scaler.seed(loss))
     else:
         loss.backward()
     opt.step(lr)

@@ -337,6 +337,15 @@ int dfm_adamw_dev(long n, float* p, const float* g, float* m, float* v, const fl
 /* fp16 loss scaling (utils/train.py:289, 323-345 torch.cuda.amp.GradScaler): flag[0] = 1 when any
  * gradient element is inf / nan (flag is not cleared: the caller zeroes it per step). */
 int dfm_grad_nonfinite(long n, const float* g, int* flag, dfm_stream_t stream);
+/* The loss scaler decided on the device, so the fp16 step replays from a captured graph: amp[4] =
+ * {scale, growth_tracker, applied_steps, skipped} float32. dfm_adamw_amp is dfm_adamw_dev that
+ * skips the update when flag[0] is set, unscales by 1/amp[0] and uses step amp[2] + 1;
+ * dfm_loss_scale_update (launched after every group's AdamW) applies GradScaler.update — backoff
+ * on overflow, growth after `interval` clean steps — counts the step and clears flag. */
+int dfm_adamw_amp(long n, float* p, const float* g, float* m, float* v, const float* hyper, const float* amp,
+                  const int* flag, float beta1, float beta2, float eps, float weight_decay, float grad_scale,
+                  void* copy, int copy_dtype, dfm_stream_t stream);
+int dfm_loss_scale_update(float* amp, int* flag, float growth, float backoff, int interval, dfm_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -84,12 +84,12 @@ class Cfg(dict):
     __getattr__ = dict.__getitem__
 
 
-def _tiny_fp16_trainer():
+def _tiny_fp16_trainer(dpr=0.1):
     from dformer_amd.segmentor import EncoderDecoder
     from dformer_amd.train import FusedAdamW
     torch.manual_seed(0)
     cfg = Cfg(backbone="DFormer-Tiny", decoder="MLPDecoder", decoder_embed_dim=64, num_classes=13,
-              drop_path_rate=0.1, bn_eps=1e-3, bn_momentum=0.1, background=255)
+              drop_path_rate=dpr, bn_eps=1e-3, bn_momentum=0.1, background=255)
     model = EncoderDecoder(cfg=cfg).cuda().set_compute_dtype(torch.float16)
     model.return_logits = False
     model.train()
@@ -129,3 +129,50 @@ def test_loss_scaler_skips_overflowing_step():
         assert torch.equal(g.flat, f) and torch.equal(g.m, m)
     train_step(model, opt, rgb, dep, lab)
     assert opt.step_count == steps + 1
+
+
+def test_fp16_graphed_step_matches_eager():
+    """The fp16 loss scaler is decided on the device, so the fp16 step captures into a HIP graph:
+    graphed and eager steps agree bit for bit, including a step skipped on overflow (the scale halves
+    and the applied-step count holds, GradScaler semantics, utils/train.py:323-338)."""
+    from dformer_amd.train import GraphedTrainStep, train_step
+    det, bm = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        ma, oa, rgb, dep, lab = _tiny_fp16_trainer(dpr=0.0)  # no RNG: identical math eager / graphed
+        mb, ob, _, _, _ = _tiny_fp16_trainer(dpr=0.0)
+        for m in (ma, mb):
+            m.decode_head.dropout_ratio = 0.0
+        la = [train_step(ma, oa, rgb, dep, lab).item() for _ in range(5)]
+        g = GraphedTrainStep(mb, ob, rgb, dep, lab, warmup=2)
+        lb = [g().item() for _ in range(3)]
+        assert la[2:] == lb, (la, lb)
+        assert oa.step_count == ob.step_count and oa.scaler.scale == ob.scaler.scale
+        for ga, gb in zip(oa.groups, ob.groups):
+            assert torch.equal(ga.flat, gb.flat) and torch.equal(ga.m, gb.m) and torch.equal(ga.v, gb.v)
+        # an overflow inside a replay: the scale is forced so large that the fp16 backward overflows
+        steps, scale = ob.step_count, ob.scaler.scale
+        flat0 = [gr.flat.clone() for gr in ob.groups]
+        ob.scaler.state[0] = 3.0e38
+        g()
+        torch.cuda.synchronize()
+        assert ob.step_count == steps and ob.scaler.scale == 1.5e38 and ob.scaler.skipped >= 1
+        for f, gr in zip(flat0, ob.groups):
+            assert torch.equal(f, gr.flat)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bm
+
+
+def test_loss_scale_update_kernel_schedule():
+    """dfm_loss_scale_update follows GradScaler.update: x0.5 on overflow, x2 after 2000 clean steps,
+    applied steps counted only when clean, the flag cleared every call."""
+    from dformer_amd import kernels as K
+    amp = torch.tensor([65536.0, 0.0, 0.0, 0.0], device="cuda")
+    flag = torch.ones(1, device="cuda", dtype=torch.int32)
+    K.loss_scale_update(amp, flag, 2.0, 0.5, 2000)
+    assert amp.tolist() == [32768.0, 0.0, 0.0, 1.0] and flag.item() == 0
+    for _ in range(1999):
+        K.loss_scale_update(amp, flag, 2.0, 0.5, 2000)
+    assert amp.tolist() == [32768.0, 1999.0, 1999.0, 1.0]
+    K.loss_scale_update(amp, flag, 2.0, 0.5, 2000)
+    assert amp.tolist() == [65536.0, 0.0, 2000.0, 1.0]
