@@ -58,14 +58,21 @@ struct DwTile;
 template <typename T> struct DwTile<T, 3> { static constexpr int TWS = 4, STRIPS = 8; };
 template <typename T> struct DwTile<T, 7> { static constexpr int TWS = 4, STRIPS = 4; };
 
-template <typename T, int K, bool FLIP, int NG>
+// forward tile shape: VAR 0 = DwTile; VAR 1 (7x7) = 8 outputs per thread along the row (the window
+// and the tap weights each read once per kernel row serve twice the FMAs of TWS = 4)
+template <typename T, int K, int VAR>
+struct DwFwdTile {
+  static constexpr int TWS = VAR == 1 ? 8 : DwTile<T, K>::TWS, STRIPS = VAR == 1 ? 2 : DwTile<T, K>::STRIPS;
+};
+
+template <typename T, int K, bool FLIP, int NG, int VAR = 0>
 __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
                                                           const T* __restrict__ x, long ldx,
                                                           const float* __restrict__ w, const float* __restrict__ bias,
                                                           int add_identity, T* __restrict__ y, long ldy,
                                                           int accumulate, T* __restrict__ gout, long ldg) {
   constexpr int CPT = DwCfg<T>::CPT, R = K / 2;
-  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int TWS = DwFwdTile<T, K, VAR>::TWS, STRIPS = DwFwdTile<T, K, VAR>::STRIPS;
   constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
   constexpr int IH = TH + K - 1, IW = TWT + K - 1, CW = NG * CPT;
   extern __shared__ __attribute__((aligned(16))) char dsm[];
@@ -632,13 +639,214 @@ long w7_launch(int B, int H, int W, int C, const void* x, long ldx, const void* 
   return g.nsb;
 }
 
-static bool w7_enabled() {  // DFM_DW_WG7=0 selects the LDS-tiled 7x7 weight gradient (A/B)
-  static const bool on = [] {
-    const char* e = getenv("DFM_DW_WG7");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
+// ---------------------------------------------------------------- LDS-tiled 7x7 weight gradient (v4)
+// The streaming kernel above re-reads every input row once per kernel row (7 blocks) and every
+// input column 2.5x (halo of a 4-wide strip), ~17x the input through L2 per pass. Here a block owns
+// NG channel vectors (CPT channels each) and walks spatial tiles of TH x TW output pixels; per tile
+// the dy tile [TH][TW][NG] and its zero-padded input window [TH+6][TW+6][NG] are staged in LDS once
+// (1.9x the input, 1x dy, from HBM/L2), then thread (g, i, part) accumulates kernel row i of
+// channel vector g — 7 taps x CPT channels — over pixel rows part, part + NP, ...: per pixel one dy
+// vector and one new input vector (the 7-vector window slides along the row in registers) feed
+// 7 * CPT FMAs, so the kernel runs at the VALU rate, not the L2 rate. The input window's row pitch
+// is padded so NG * pitch = 4 (mod 8) vectors: the lanes of one 8-lane LDS phase — NG channel
+// vectors x 2 kernel rows — fall on 8 distinct 16-byte bank groups (dy reads of one pixel are
+// broadcast). At the end the NP parts of a (g, i) meet in LDS in a fixed order and the block writes
+// its partial [blockIdx.x][C][50]; partial_sum_kernel<2> sums the spatial lanes (deterministic).
+constexpr int W7L_NG = 4, W7L_TH = 16, W7L_TW = 14, W7L_NP = 8;   // TW: a multiple of 7 (register ring)
+constexpr int W7L_IH = W7L_TH + 6, W7L_IW = W7L_TW + 7;  // +7: pitch 21 -> NG * pitch = 84 = 4 (mod 8)
+static_assert((W7L_NG * W7L_IW) % 8 == 4, "LDS pitch");
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// one 16-byte vector -> CPT/2 channel pairs (packed-FMA operands; bf16 / f16 widen exactly)
+template <typename T>
+DFM_INLINE void unpack_pairs(uint4 q, f2v* v) {
+  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+  if constexpr (std::is_same<T, bf16_t>::value) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = f2v{__uint_as_float(u[k] << 16), __uint_as_float(u[k] & 0xffff0000u)};
+  } else if constexpr (std::is_same<T, f16_t>::value) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = f2v{h2f((uint16_t)(u[k] & 0xffffu)), h2f((uint16_t)(u[k] >> 16))};
+  } else {
+    v[0] = f2v{__uint_as_float(u[0]), __uint_as_float(u[1])};
+    v[1] = f2v{__uint_as_float(u[2]), __uint_as_float(u[3])};
+  }
 }
+
+template <typename T>
+__global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
+                                                            const T* __restrict__ x, long ldx,
+                                                            const T* __restrict__ dy, long lddy,
+                                                            float* __restrict__ part) {
+  constexpr int CPT = DwCfg<T>::CPT, CP = CPT / 2, NG = W7L_NG, TH = W7L_TH, TW = W7L_TW, NP = W7L_NP;
+  constexpr int IH = W7L_IH, IW = W7L_IW, NX = IH * (TW + 6) * NG, ND = TH * TW * NG;
+  constexpr int NL = (NX + ND + 255) / 256, NACT = NG * 7 * NP, BQ = 256 / NG;
+  __shared__ uint4 xs[IH * IW * NG];
+  __shared__ uint4 ds[ND];
+  const int ncv = C / CPT;
+  const int cv0 = blockIdx.y * NG;  // first channel vector of the slab
+  const long ntiles = (long)B * tiles_h * tiles_w;
+  const int t = threadIdx.x;
+  const int g = t % NG, i = (t / NG) % 7, prt = t / (NG * 7);
+  const bool active = t < NACT;
+  f2v acc[7][CP], bs[CP];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int e = 0; e < CP; ++e) acc[j][e] = f2v{0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < CP; ++e) bs[e] = f2v{0.f, 0.f};
+
+  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tw = (int)(tile % tiles_w), th = (int)((tile / tiles_w) % tiles_h);
+    const long b = tile / ((long)tiles_w * tiles_h);
+    const int h0 = th * TH, w0 = tw * TW;
+    const long img = b * H * W;
+    uint4 buf[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int v = t + l * 256;
+      buf[l] = make_uint4(0, 0, 0, 0);
+      if (v < NX) {
+        const int gg = v % NG, col = (v / NG) % (TW + 6), row = v / (NG * (TW + 6));
+        const int hh = h0 + row - 3, ww = w0 + col - 3, cv = cv0 + gg;
+        if (hh >= 0 && hh < H && ww >= 0 && ww < W && cv < ncv)
+          buf[l] = *reinterpret_cast<const uint4*>(x + (img + (long)hh * W + ww) * ldx + cv * CPT);
+      } else if (v < NX + ND) {
+        const int u = v - NX;
+        const int gg = u % NG, col = (u / NG) % TW, row = u / (NG * TW);
+        const int hh = h0 + row, ww = w0 + col, cv = cv0 + gg;
+        if (hh < H && ww < W && cv < ncv)
+          buf[l] = *reinterpret_cast<const uint4*>(dy + (img + (long)hh * W + ww) * lddy + cv * CPT);
+      }
+    }
+    __syncthreads();  // the previous tile's reads are done
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int v = t + l * 256;
+      if (v < NX) {
+        const int gg = v % NG, col = (v / NG) % (TW + 6), row = v / (NG * (TW + 6));
+        xs[(row * IW + col) * NG + gg] = buf[l];
+      } else if (v < NX + ND) {
+        ds[v - NX] = buf[l];
+      }
+    }
+    __syncthreads();
+    {  // bias gradient: thread (g, q) sums the tile's pixels q, q + BQ, ... of channel vector g
+      for (int pix = t / NG; pix < TH * TW; pix += BQ) {
+        f2v d[CP];
+        unpack_pairs<T>(ds[pix * NG + g], d);
+#pragma unroll
+        for (int e = 0; e < CP; ++e) bs[e] += d[e];
+      }
+    }
+    if (active) {
+#pragma unroll 1
+      for (int r = prt; r < TH; r += NP) {
+        const uint4* xr = xs + ((r + i) * IW) * NG + g;
+        const uint4* dr = ds + (r * TW) * NG + g;
+        f2v xw[7][CP];  // ring: input column q of the row in slot q % 7
+#pragma unroll
+        for (int u = 0; u < 6; ++u) unpack_pairs<T>(xr[u * NG], xw[u]);
+#pragma unroll 1
+        for (int cb = 0; cb < TW; cb += 7) {
+#pragma unroll
+          for (int s7 = 0; s7 < 7; ++s7) {
+            const int c = cb + s7;
+            unpack_pairs<T>(xr[(c + 6) * NG], xw[(s7 + 6) % 7]);
+            f2v d[CP];
+            unpack_pairs<T>(dr[c * NG], d);
+#pragma unroll
+            for (int j = 0; j < 7; ++j)
+#pragma unroll
+              for (int e = 0; e < CP; ++e) acc[j][e] = __builtin_elementwise_fma(d[e], xw[(s7 + j) % 7][e], acc[j][e]);
+          }
+        }
+      }
+    }
+  }
+  // the NP parts of each (g, i) meet in LDS in part order, then part 0 writes the block's partial;
+  // the bias partials of the BQ pixel lanes of each g likewise (lane order)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);
+  constexpr int RS = 7 * CPT + 1;
+  for (int q = 1; q < NP; ++q) {
+    if (active && prt == q) {
+      float* o = red + (g * 7 + i) * RS;
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) {
+          o[j * CPT + 2 * e] = acc[j][e].x;
+          o[j * CPT + 2 * e + 1] = acc[j][e].y;
+        }
+    }
+    __syncthreads();
+    if (active && prt == 0) {
+      const float* o = red + (g * 7 + i) * RS;
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) acc[j][e] += f2v{o[j * CPT + 2 * e], o[j * CPT + 2 * e + 1]};
+    }
+    __syncthreads();
+  }
+  float* bred = red + NG * 7 * RS;  // [BQ][NG][CPT]
+#pragma unroll
+  for (int e = 0; e < CP; ++e) {
+    bred[t * CPT + 2 * e] = bs[e].x;
+    bred[t * CPT + 2 * e + 1] = bs[e].y;
+  }
+  __syncthreads();
+  const long pbase = (long)blockIdx.x * C * 50;
+  if (active && prt == 0 && cv0 + g < ncv) {
+#pragma unroll
+    for (int e = 0; e < CP; ++e) {
+      const int c = (cv0 + g) * CPT + 2 * e;
+      float* o = part + pbase + (long)c * 50;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        o[i * 7 + j] = acc[j][e].x;
+        o[50 + i * 7 + j] = acc[j][e].y;
+      }
+    }
+  }
+  if (t < NG * CPT) {  // bias: thread (g, e) sums the BQ lanes in order
+    const int gg = t / CPT, e = t % CPT;
+    if (cv0 + gg < ncv) {
+      float sum = 0.f;
+      for (int q = 0; q < BQ; ++q) sum += bred[(q * NG + gg) * CPT + e];
+      part[pbase + (long)((cv0 + gg) * CPT + e) * 50 + 49] = sum;
+    }
+  }
+}
+
+template <typename T>
+long w7l_nsb(int B, int H, int W, int C) {
+  const long ntiles = (long)B * cdiv(H, W7L_TH) * cdiv(W, W7L_TW);
+  const long slabs = cdiv(C / DwCfg<T>::CPT, W7L_NG);
+  return std::max(1L, std::min(ntiles, (768 + slabs - 1) / slabs));
+}
+
+template <typename T>
+long w7l_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
+                hipStream_t s) {
+  const long nsb = w7l_nsb<T>(B, H, W, C);
+  const unsigned slabs = cdiv(C / DwCfg<T>::CPT, W7L_NG);
+  DFM_LAUNCH(dw7_lds_wgrad_kernel<T>, dim3((unsigned)nsb, slabs), dim3(256), 0, s, B, H, W, C, cdiv(H, W7L_TH),
+             cdiv(W, W7L_TW), (const T*)x, ldx, (const T*)dy, lddy, part);
+  return nsb;
+}
+
+static int w7_mode() {  // DFM_DW_WG7: 2 (default) LDS-tiled v4, 1 row-streaming, 0 LDS-tiled v3 (A/B)
+  static const int m = [] {
+    const char* e = getenv("DFM_DW_WG7");
+    return e ? atoi(e) : 2;
+  }();
+  return m;
+}
+
 
 // ---------------------------------------------------------------- row-streaming 3x3 forward / input gradient
 // The forward counterpart of the streaming weight gradient: a lane owns one 8-byte channel vector
@@ -810,16 +1018,24 @@ bool dw_aligned(int C, const void* p, long ld) {
   return C % CPT == 0 && ld % CPT == 0 && ((uintptr_t)p % 16) == 0;
 }
 
-template <typename T, int K, bool FLIP, int NG>
+template <typename T, int K, bool FLIP, int NG, int VAR = 0>
 int dw_tile_launch(int B, int H, int W, int C, const void* x, long ldx, const float* w, const float* bias, int id,
                    void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
-  constexpr int CPT = DwCfg<T>::CPT, TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
+  constexpr int CPT = DwCfg<T>::CPT, TWS = DwFwdTile<T, K, VAR>::TWS, STRIPS = DwFwdTile<T, K, VAR>::STRIPS;
   constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
   const int tiles_h = (H + TH - 1) / TH, tiles_w = (W + TWT - 1) / TWT;
   const int G = C / CPT;
   dim3 grid((unsigned)((long)B * tiles_h * tiles_w * cdiv(G, NG)));
   const size_t lds = (size_t)(TH + K - 1) * (TWT + K - 1) * NG * 16 + (size_t)K * K * NG * CPT * sizeof(float);
-  DFM_LAUNCH((dw_tile_fwd_kernel<T, K, FLIP, NG>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
+  if (lds > 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)dw_tile_fwd_kernel<T, K, FLIP, NG, VAR>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
+  DFM_LAUNCH((dw_tile_fwd_kernel<T, K, FLIP, NG, VAR>), grid, dim3(256), lds, s, B, H, W, C, tiles_h, tiles_w,
                      (const T*)x, ldx, w, bias, id, (T*)y, ldy, acc, (T*)gout, ldg);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
@@ -848,6 +1064,12 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
     if (G >= 2) GO(3, 2);
     GO(3, 1);
   }
+  static const int f7 = [] {  // DFM_DW_F7: 7x7 forward tile variant (0: 4 outputs / thread, 1: 8, 2: 8 with NG 4)
+    const char* e = getenv("DFM_DW_F7");
+    return e ? atoi(e) : 0;
+  }();
+  if (f7 == 1 && G >= 8) return dw_tile_launch<T, 7, FLIP, 8, 1>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
+  if (f7 >= 1 && G >= 4) return dw_tile_launch<T, 7, FLIP, 4, 1>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
   if (G >= 8) GO(7, 8);
   if (G >= 4) GO(7, 4);
   if (G >= 2) GO(7, 2);
@@ -957,7 +1179,8 @@ extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, in
                     w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb});
   else if (k == 7)
     nsb = std::max({wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C),
-                    w7_geom<float>(B, H, W, C).nsb, w7_geom<bf16_t>(B, H, W, C).nsb});
+                    w7_geom<float>(B, H, W, C).nsb, w7_geom<bf16_t>(B, H, W, C).nsb, w7l_nsb<float>(B, H, W, C),
+                    w7l_nsb<bf16_t>(B, H, W, C)});
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);
 }
 
@@ -972,21 +1195,24 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   long nsb;
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_enabled() ? w7_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                 : wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
+    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                    : w7_mode() == 1 ? w7_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                     : wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   }
   else if (dtype == DFM_F16) {
     DFM_CHECK_ARG(dw_aligned<f16_t>(C, x, ldx) && dw_aligned<f16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_enabled() ? w7_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                 : wgrad_dispatch<f16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
+    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                    : w7_mode() == 1 ? w7_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                     : wgrad_dispatch<f16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<f16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_enabled() ? w7_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                 : wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
+    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                    : w7_mode() == 1 ? w7_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                                     : wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
           : w3_enabled() ? w3_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
                          : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else {

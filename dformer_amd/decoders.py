@@ -13,7 +13,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import kernels as K
-from .functional import gslot, gslot2, wcast
+from .functional import gslot, gslot2, gslot_rows, wcast
 
 
 # Test-only: with an initialised one-rank process group, take every collective branch (SyncBN
@@ -29,12 +29,6 @@ def collectives_on(world=None):
         return False
     w = dist.get_world_size() if world is None else world
     return w > 1 or FORCE_COLLECTIVES
-
-
-def _allreduce(t, sync):
-    if sync and collectives_on():
-        dist.all_reduce(t)
-    return t
 
 
 def _world(sync):
@@ -79,6 +73,22 @@ def bn_batch_stats(x, bn, sync):
     return mean, rstd, count
 
 
+def bn_grad_stats(x, dy, mean, rstd, bn, sync):
+    """BatchNorm backward statistics st2 = (sum dy, sum dy * xhat) of NHWC rows. Returns (st2 for the
+    input gradient, dgamma, dbeta). The local statistics ARE this rank's beta / gamma gradients
+    (SyncBatchNorm's backward forms grad_weight / grad_bias before its all-reduce,
+    torch/nn/modules/_functions.py; DDP then averages them like every gradient) and are written
+    straight into the flat gradient slots, laid out [beta | gamma] by train.fused_chains; under
+    SyncBN an all-reduced copy feeds the input gradient."""
+    out = gslot_rows(bn.bias, bn.weight) if bn is not None and bn.affine else None
+    st = K.bn_bwd_stats(x, dy, mean, rstd, out=out.view(2, -1) if out is not None else None)
+    stg = st
+    if sync and collectives_on():
+        stg = st.clone()
+        dist.all_reduce(stg)
+    return stg, st[1], st[0]
+
+
 # ============================================================================ building blocks
 class ConvBNActFn(torch.autograd.Function):
     """y = act(BN(x @ W^T) [+ res])  — mmcv ConvModule(1x1 conv, BN, ReLU) (ham_head.py:204-220)."""
@@ -97,7 +107,7 @@ class ConvBNActFn(torch.autograd.Function):
             count = rows
         y = K.bn_apply(y0, mean, rstd, gamma, beta, res=res, act=act)
         ctx.save_for_backward(x, w, y0, y, mean, rstd, gamma)
-        ctx.act, ctx.sync, ctx.count, ctx.has_res = act, sync, count, res is not None
+        ctx.act, ctx.sync, ctx.count, ctx.has_res, ctx.bn = act, sync, count, res is not None, bn
         return y
 
     @staticmethod
@@ -107,12 +117,12 @@ class ConvBNActFn(torch.autograd.Function):
         dy = dy.contiguous()
         if ctx.act == 2:
             dy = K.relu_bwd(dy, y)
-        st2 = _allreduce(K.bn_bwd_stats(y0, dy, mean, rstd), ctx.sync)
+        st2, dgamma, dbeta = bn_grad_stats(y0, dy, mean, rstd, ctx.bn, ctx.sync)
         dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
         dW = K.linear_wgrad(dy0, x, out=gslot2(w))
         dx = K.linear_dgrad(dy0, wcast(x.dtype, w))
         dres = dy if ctx.has_res else None
-        return dx, dres, dW.view_as(w), st2[1].clone(), st2[0].clone(), None, None, None
+        return dx, dres, dW.view_as(w), dgamma, dbeta, None, None, None
 
 
 class LinearActFn(torch.autograd.Function):
@@ -530,7 +540,7 @@ class FuseBNReLUFn(torch.autograd.Function):
             mean, rstd, count = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps), rows
         y = K.bn_apply(y0, mean, rstd, gamma, beta, act=2)
         ctx.save_for_backward(cat, Wc, y0, y, mean, rstd, gamma)
-        ctx.E, ctx.count, ctx.sync, ctx.wshape = E, count, sync, w.shape
+        ctx.E, ctx.count, ctx.sync, ctx.wshape, ctx.bn = E, count, sync, w.shape, bn
         return y
 
     @staticmethod
@@ -539,12 +549,12 @@ class FuseBNReLUFn(torch.autograd.Function):
         cat, Wc, y0, y, mean, rstd, gamma = ctx.saved_tensors
         E = ctx.E
         dy = K.relu_bwd(dy.contiguous(), y)
-        st2 = _allreduce(K.bn_bwd_stats(y0, dy, mean, rstd), ctx.sync)
+        st2, dgamma, dbeta = bn_grad_stats(y0, dy, mean, rstd, ctx.bn, ctx.sync)
         dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
         dWp, db = K.linear_wgrad(dy0, cat, bias_grad=True)  # columns [c1 | c4 | c3 | c2]
         dW = torch.cat([dWp[:, E:], dWp[:, :E]], 1).reshape(ctx.wshape)
         dcat = K.linear_dgrad(dy0, Wc)
-        return dcat, dW, db, st2[1].clone(), st2[0].clone(), None, None, None
+        return dcat, dW, db, dgamma, dbeta, None, None, None
 
 
 # ========================================================================================== loss

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import kernels as K
-from .decoders import _allreduce, bn_batch_stats, collectives_on
+from .decoders import bn_batch_stats, bn_grad_stats, collectives_on
 from .functional import ATTN_PARAM_NAMES, AttentionFn, ConvFFNFn, gslot, invalidate_weights, register_side_stream
 
 _EMPTY = {}
@@ -218,7 +218,7 @@ class BNRowsFn(torch.autograd.Function):
             count = rows
         y = K.bn_apply(xr, mean, rstd, gamma, beta)
         ctx.save_for_backward(xr, mean, rstd, gamma)
-        ctx.sync, ctx.count, ctx.shape = sync, count, (B, C, H, W)
+        ctx.sync, ctx.count, ctx.shape, ctx.bn = sync, count, (B, C, H, W), bn
         ctx.training = bn.training
         return y.view(B, H, W, C).permute(0, 3, 1, 2)
 
@@ -228,12 +228,12 @@ class BNRowsFn(torch.autograd.Function):
         xr, mean, rstd, gamma = ctx.saved_tensors
         B, C, H, W = ctx.shape
         dyr = dy.permute(0, 2, 3, 1).contiguous().view(-1, C)
-        st2 = _allreduce(K.bn_bwd_stats(xr, dyr, mean, rstd), ctx.sync)
+        st2, dgamma, dbeta = bn_grad_stats(xr, dyr, mean, rstd, ctx.bn, ctx.sync)
         if ctx.training:
             dx = K.bn_bwd_apply(xr, dyr, mean, rstd, gamma, st2, ctx.count)
         else:  # running statistics: BN is a fixed per-channel affine
             dx = K.scale_mul(dyr, colscale=rstd * gamma)
-        return dx.view(B, H, W, C).permute(0, 3, 1, 2), st2[1].clone(), st2[0].clone(), None, None
+        return dx.view(B, H, W, C).permute(0, 3, 1, 2), dgamma, dbeta, None, None
 
 
 class ConvS2Fn(torch.autograd.Function):
@@ -268,6 +268,7 @@ class ConvS2Fn(torch.autograd.Function):
         y = K.linear(cols, wp, bias.detach())
         ctx.shape, ctx.cin, ctx.sync, ctx.gelu, ctx.count = (B, H, W), C, sync, gelu, count
         ctx.has_bn = bn is not None
+        ctx.bn = bn
         ctx.training = bn is not None and bn.training
         ctx.x_dtype = x.dtype
         ctx.tag = K.TAG
@@ -291,8 +292,7 @@ class ConvS2Fn(torch.autograd.Function):
             dcols = K.linear_dgrad(dy, wp)
             mean, rstd, gamma, beta = aff
             dz = K.conv3s2_col2im(dcols, ctx.shape, cin, x=xr, bn=aff if ctx.gelu else None, gelu=ctx.gelu)
-            st2 = _allreduce(K.bn_bwd_stats(xr, dz, mean, rstd), ctx.sync)
-            dgamma, dbeta = st2[1].clone(), st2[0].clone()
+            st2, dgamma, dbeta = bn_grad_stats(xr, dz, mean, rstd, ctx.bn, ctx.sync)
             if ctx.needs_input_grad[0]:
                 B, H, W = ctx.shape
                 if ctx.training:

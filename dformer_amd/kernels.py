@@ -510,9 +510,9 @@ def bn_apply(x, mean, rstd, gamma, beta, res=None, act=0, out=None):
     return out
 
 
-def bn_bwd_stats(x, dy, mean, rstd):
+def bn_bwd_stats(x, dy, mean, rstd, out=None):
     rows, C = x.shape
-    st = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    st = torch.empty(2, C, device=x.device, dtype=torch.float32) if out is None else out
     ws = _ws(lib.dfm_bn_workspace(rows, C), x.device)
     check(lib.dfm_bn_bwd_stats(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(mean), ptr(rstd),
                                ptr(st), ptr(ws), stream()), "dfm_bn_bwd_stats")

@@ -73,9 +73,13 @@ def _chain_order(params, chains):
 
 def fused_chains(model):
     """Parameter chains whose flat slots must be adjacent: each Attention's q | q_cut | l weights
-    and biases (one GEMM in the forward, one weight-gradient GEMM in the backward) and proj | proj_e."""
+    and biases (one GEMM in the forward, one weight-gradient GEMM in the backward), proj | proj_e,
+    and every BatchNorm's bias | weight (the BN backward statistics (sum dy, sum dy * xhat) are
+    written straight into them, decoders.bn_grad_stats)."""
     chains = []
     for m in model.modules():
+        if isinstance(m, nn.modules.batchnorm._BatchNorm) and m.affine:
+            chains.append([m.bias, m.weight])
         if all(hasattr(m, n) for n in ("q", "q_cut", "l", "proj")):
             chains.append([m.q.weight, m.q_cut.weight, m.l.weight])
             chains.append([m.q.bias, m.q_cut.bias, m.l.bias])

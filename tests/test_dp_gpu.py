@@ -1,0 +1,118 @@
+"""Two data-parallel ranks on the one GPU of the box (gloo over device tensors; RCCL refuses two ranks
+on one device): the world > 1 code of config 4 — SyncBN statistics all-gathered and merged on the
+device, BN backward statistics all-reduced for the input gradient, bucketed gradient all-reduce, the
+loss all-reduce — against one rank training on the whole batch (utils/train.py:238-243 DDP +
+SyncBatchNorm, utils/engine/engine.py:53-66).
+
+With every label valid both ranks hold the same number of pixels, so DDP's average of the two
+half-batch gradients is exactly the whole-batch gradient and SyncBN over the two ranks is BatchNorm
+over the whole batch: everything must agree to fp32 rounding (the step runs in float32)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BATCH, H, W = 4, 96, 128
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(rank, world):
+    """One train step of DFormer-Tiny + ham on this rank's share of a fixed batch; returns the flat
+    gradients divided by world (the buffers hold the SUM over ranks), the BN running statistics and
+    the all-reduced loss."""
+    import bench
+    from dformer_amd.segmentor import EncoderDecoder
+    from dformer_amd.train import FusedAdamW, train_step
+    dev = torch.device("cuda", 0)
+    cfg = bench.make_cfg("DFormer-Tiny", "ham")
+    cfg["drop_path_rate"] = 0.0
+    torch.manual_seed(3)
+    model = EncoderDecoder(cfg=cfg, syncbn=world > 1)
+    model.decode_head.dropout_ratio = 0.0
+    model = model.to(dev).set_compute_dtype(torch.float32)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    bases = torch.rand(BATCH, 512, 64, device=dev, generator=g)
+    bases = bases / bases.norm(dim=1, keepdim=True)
+    rgb, dep, lab = bench.synthetic_batch(BATCH, H, W, cfg.num_classes, dev, 5)
+    lab[lab == 255] = 0  # equal valid-pixel counts per rank
+    per = BATCH // world
+    sl = slice(rank * per, (rank + 1) * per)
+    model.decode_head.hamburger.ham.injected_bases = bases[sl].contiguous()
+    model.return_logits = False
+    model.train()
+    opt = FusedAdamW(model, lr=0.0, weight_decay=cfg.weight_decay, world=world, compute_dtype=torch.float32)
+    loss = train_step(model, opt, rgb[sl].contiguous(), dep[sl].contiguous(), lab[sl].contiguous())
+    torch.cuda.synchronize()
+    grads = [(gr.grad / world).cpu() for gr in opt.groups]
+    bn_grads = {}
+    for name, m in model.named_modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            for gr in opt.groups:
+                if m.weight in gr.slots:
+                    off, k = gr.slots[m.weight]
+                    bn_grads[name] = (gr.grad[off:off + k] / world).cpu()
+    running = {k: v.cpu() for k, v in model.state_dict().items() if "running" in k}
+    return grads, bn_grads, running, float(loss)
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _run(rank, world), None))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+def test_two_ranks_syncbn_ddp_equal_whole_batch():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    import torch.multiprocessing as mp
+    ref_grads, ref_bn, ref_run, ref_loss = _run(0, 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (out, err)) for r, out, err in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert res[r][1] is None, res[r][1]
+    grads, bn_grads, running, loss = res[0][0]
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
+    for a, b in zip(grads, ref_grads):
+        assert _rel(a, b) < 1e-4, _rel(a, b)
+    # the BN affine gradients are local statistics averaged by DDP, not all-reduced twice
+    assert len(bn_grads) >= 4
+    for k, v in bn_grads.items():
+        assert _rel(v, ref_bn[k]) < 1e-4, (k, _rel(v, ref_bn[k]))
+    for k, v in running.items():
+        if v.dtype.is_floating_point:
+            assert _rel(v, ref_run[k]) < 1e-5, (k, _rel(v, ref_run[k]))
+    # both ranks hold identical all-reduced gradients
+    for a, b in zip(res[1][0][0], grads):
+        assert torch.equal(a, b)

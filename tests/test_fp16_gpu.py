@@ -153,10 +153,10 @@ def test_fp16_graphed_step_matches_eager():
         # an overflow inside a replay: the scale is forced so large that the fp16 backward overflows
         steps, scale = ob.step_count, ob.scaler.scale
         flat0 = [gr.flat.clone() for gr in ob.groups]
-        ob.scaler.state[0] = 3.0e38
+        ob.scaler.state[0] = 2.0 ** 127
         g()
         torch.cuda.synchronize()
-        assert ob.step_count == steps and ob.scaler.scale == 1.5e38 and ob.scaler.skipped >= 1
+        assert ob.step_count == steps and ob.scaler.scale == 2.0 ** 126 and ob.scaler.skipped >= 1
         for f, gr in zip(flat0, ob.groups):
             assert torch.equal(f, gr.flat)
     finally:
