@@ -54,8 +54,11 @@ def bn_batch_stats(x, bn, sync):
     world = _world(sync)
     count = rows
     if sync and collectives_on(world):
-        gathered = torch.empty((world,) + tuple(st.shape), device=st.device, dtype=st.dtype)
+        # gathered along dim 0 as [world * 3, C] (gloo splits the output along its first dim and
+        # requires each piece to have the input's shape; RCCL takes either form)
+        gathered = torch.empty((world * st.shape[0],) + tuple(st.shape[1:]), device=st.device, dtype=st.dtype)
         dist.all_gather_into_tensor(gathered, st)
+        gathered = gathered.view((world,) + tuple(st.shape))
         counts = _GLOBAL_ROWS.get((rows, world))
         if counts is None:  # first batch of this shape: exchange the per-rank row counts once
             cnt = torch.tensor([float(rows)], device=x.device)
