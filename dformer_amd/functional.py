@@ -314,6 +314,22 @@ class ConvFFNFn(torch.autograd.Function):
 # ConvFFN stream, the branch is short and the fork/join events cost what the overlap gains.
 _ATTN_SIDE_ON = os.environ.get("DFM_ATTN_STREAM", "0") == "1"
 _ATTN_SIDE = {}
+# The depth branch of the attention BACKWARD (dual product -> e_back -> DW7x7 -> e_fore gradients,
+# DFormer.py:84-88, 133) is the longer chain (8 launches) and independent of the RGB branch until
+# the q|q_cut|l gradients, so it is issued on a side stream (DFM_ATTN_BWD_STREAM=0: one stream).
+# Measured on MI355X, DFormer-B bf16 bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s.
+_ATTN_BWD_SIDE_ON = os.environ.get("DFM_ATTN_BWD_STREAM", "1") == "1"
+_ATTN_BWD_SIDE = {}
+
+
+def _attn_bwd_side(dev):
+    if not _ATTN_BWD_SIDE_ON:
+        return None
+    st = _ATTN_BWD_SIDE.get(dev)
+    if st is None:
+        st = _ATTN_BWD_SIDE[dev] = torch.cuda.Stream(device=dev)
+        register_side_stream(st)
+    return st
 
 
 def _attn_side(dev):
@@ -457,23 +473,36 @@ class AttentionFn(torch.autograd.Function):
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
-        # depth branch: cxe = cx * xe'
-        dcxe = df[:, fw - Ch:]
-        _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
-        ow, ob = gslot2(web), gslot(beb)
-        grads["web"], grads["beb"] = offload_wgrad((ow, ob), (dxep, e2), lambda: K.linear_wgrad(
-            dxep, e2, out=ow, bias_grad=True, bias_out=ob))
-        de2 = K.linear_dgrad(dxep, wcast(dt, web))
-        ow, ob = gslot(wec), gslot(bec)
-        grads["wec"], grads["bec"] = offload_wgrad((ow, ob), (e1, de2), lambda: K.dwconv_bwd_weight(
-            e1, de2, shape, 7, dw=ow, db=ob))
-        de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
-        ow, ob = gslot2(wef), gslot(bef)
-        grads["wef"], grads["bef"] = offload_wgrad((ow, ob), (de1, xen), lambda: K.linear_wgrad(
-            de1, xen, out=ow, bias_grad=True, bias_out=ob))
-        dxen = K.linear_dgrad(de1, wcast(dt, wef))
+        side = _attn_bwd_side(dev) if x.is_cuda else None
+        main = torch.cuda.current_stream(dev) if side is not None else None
+
+        def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))
+            dcxe = df[:, fw - Ch:]
+            _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
+            ow, ob = gslot2(web), gslot(beb)
+            grads["web"], grads["beb"] = offload_wgrad((ow, ob), (dxep, e2), lambda: K.linear_wgrad(
+                dxep, e2, out=ow, bias_grad=True, bias_out=ob))
+            de2 = K.linear_dgrad(dxep, wcast(dt, web))
+            ow, ob = gslot(wec), gslot(bec)
+            grads["wec"], grads["bec"] = offload_wgrad((ow, ob), (e1, de2), lambda: K.dwconv_bwd_weight(
+                e1, de2, shape, 7, dw=ow, db=ob))
+            de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
+            ow, ob = gslot2(wef), gslot(bef)
+            grads["wef"], grads["bef"] = offload_wgrad((ow, ob), (de1, xen), lambda: K.linear_wgrad(
+                de1, xen, out=ow, bias_grad=True, bias_out=ob))
+            return K.linear_dgrad(de1, wcast(dt, wef)), (dxep, de2, de1)
+
+        if side is not None:  # the depth branch overlaps the RGB branch; joined before q|q_cut|l
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dxen, side_tmp = depth_branch()
+            for t in (df, xep, cx, e2, e1, xen, dqcl):
+                t.record_stream(side)
+        else:
+            dxen, _ = depth_branch()
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
+        dpooled_e = None
         if window:
             kv, pooled, m, o, lse = saved_attn
             dh = C // heads // 2
@@ -487,7 +516,7 @@ class AttentionFn(torch.autograd.Function):
                 dm, pooled, out=ow, bias_grad=True, bias_out=ob))
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
-            K.pool7_bwd(dpooled[:, C:], shape, dx=dxen, accumulate=True)
+            dpooled_e = dpooled[:, C:]
             ow, ob = gslot2(wkv), gslot(bkv)
             grads["wkv"], grads["bkv"] = offload_wgrad((ow, ob), (dkv, g), lambda: K.linear_wgrad(
                 dkv, g, out=ow, bias_grad=True, bias_out=ob))
@@ -504,6 +533,12 @@ class AttentionFn(torch.autograd.Function):
             g, dapre, shape, 7, dw=ow, db=ob))
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.gelu_bwd(dg, lpre, out=dl)
+        if side is not None:  # join the depth branch (dcx columns of dqcl, dxen)
+            main.wait_stream(side)
+            for t in (dxen,) + side_tmp:
+                t.record_stream(main)
+        if dpooled_e is not None:
+            K.pool7_bwd(dpooled_e, shape, dx=dxen, accumulate=True)
         # q | q_cut | l
         dWqcl, dbqcl = K.linear_wgrad(dqcl, xn, bias_grad=True, out=gslot_rows(wq, wqc, wl),
                                       bias_out=gslot_rows(bq, bqc, bl))

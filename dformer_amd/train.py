@@ -426,10 +426,13 @@ class GraphedTrainStep:
             for _ in range(warmup):
                 train_step(model, opt, rgb, depth, label)
         torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         opt.external_hyper = True  # inside the graph AdamW only reads hyper
         try:
-            with torch.cuda.graph(self.graph):
+            # thread-local capture: the process group's watchdog thread keeps querying the events of
+            # earlier (eager) collectives, which under the default global mode invalidates the capture
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.loss = train_step(model, opt, rgb, depth, label)  # host step_count advanced once here
         finally:
             opt.external_hyper = False

@@ -6,7 +6,8 @@ SyncBatchNorm, utils/engine/engine.py:53-66).
 
 With every label valid both ranks hold the same number of pixels, so DDP's average of the two
 half-batch gradients is exactly the whole-batch gradient and SyncBN over the two ranks is BatchNorm
-over the whole batch: everything must agree to fp32 rounding (the step runs in float32)."""
+over the whole batch (the stems' plain BatchNorm2d layers, per-rank in the reference as well, run on
+their running statistics): everything must agree to fp32 rounding (the step runs in float32)."""
 import os
 import socket
 import sys
@@ -53,13 +54,22 @@ def _run(rank, world):
     model.decode_head.hamburger.ham.injected_bases = bases[sl].contiguous()
     model.return_logits = False
     model.train()
+    # the stems' BatchNorm2d layers are per-rank BN in the reference too (DFormer.py:194-211 builds
+    # them as nn.BatchNorm2d whatever norm_cfg says): frozen on running statistics here so the
+    # two-rank step can equal the whole-batch step; every SyncBN layer stays in training mode
+    bb = model.encoder_backbone
+    frozen = [m for stem in (bb.downsample_layers[0], bb.downsample_layers_e[0]) for m in stem
+              if isinstance(m, torch.nn.BatchNorm2d)]
+    assert len(frozen) == 4 and any(isinstance(m, torch.nn.SyncBatchNorm) for m in model.modules()) == (world > 1)
+    for m in frozen:
+        m.eval()
     opt = FusedAdamW(model, lr=0.0, weight_decay=cfg.weight_decay, world=world, compute_dtype=torch.float32)
     loss = train_step(model, opt, rgb[sl].contiguous(), dep[sl].contiguous(), lab[sl].contiguous())
     torch.cuda.synchronize()
     grads = [(gr.grad / world).cpu() for gr in opt.groups]
     bn_grads = {}
     for name, m in model.named_modules():
-        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.training:  # the synchronised layers
             for gr in opt.groups:
                 if m.weight in gr.slots:
                     off, k = gr.slots[m.weight]
@@ -75,7 +85,11 @@ def _worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _run(rank, world), None))
+        grads, bn_grads, running, loss = _run(rank, world)
+        # numpy copies travel by value: a torch CPU tensor would be shared through a file descriptor
+        # that vanishes when this process exits before the parent unpickles it
+        q.put((rank, ([g.numpy() for g in grads], {k: v.numpy() for k, v in bn_grads.items()},
+                      {k: v.numpy() for k, v in running.items()}, loss), None))
     except Exception as e:  # report instead of hanging the parent
         q.put((rank, None, repr(e)))
     finally:
@@ -102,7 +116,9 @@ def test_two_ranks_syncbn_ddp_equal_whole_batch():
         p.join(timeout=60)
     for r in range(2):
         assert res[r][1] is None, res[r][1]
-    grads, bn_grads, running, loss = res[0][0]
+    out = {r: ([torch.from_numpy(g) for g in v[0][0]], {k: torch.from_numpy(t) for k, t in v[0][1].items()},
+               {k: torch.from_numpy(t) for k, t in v[0][2].items()}, v[0][3]) for r, v in res.items()}
+    grads, bn_grads, running, loss = out[0]
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
     for a, b in zip(grads, ref_grads):
         assert _rel(a, b) < 1e-4, _rel(a, b)
@@ -114,5 +130,5 @@ def test_two_ranks_syncbn_ddp_equal_whole_batch():
         if v.dtype.is_floating_point:
             assert _rel(v, ref_run[k]) < 1e-5, (k, _rel(v, ref_run[k]))
     # both ranks hold identical all-reduced gradients
-    for a, b in zip(res[1][0][0], grads):
+    for a, b in zip(out[1][0], grads):
         assert torch.equal(a, b)

@@ -155,6 +155,13 @@ def test_forced_collectives_one_rank_nccl():
             assert torch.equal(ga.flat, gc.flat) and torch.equal(ga.v, gc.v)
         for (ka, ba), (kc, bc) in zip(ma.state_dict().items(), mc.state_dict().items()):
             assert ka == kc and torch.equal(ba, bc), ka
+    except BaseException as e:  # report before the process-group teardown (which may abort on failure)
+        print("forced-collectives failure:", repr(e)[:2000], flush=True)
+        import traceback
+        traceback.print_exc()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        raise
     finally:
         D.FORCE_COLLECTIVES = False
         D._GLOBAL_ROWS.clear()
