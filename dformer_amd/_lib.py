@@ -50,6 +50,8 @@ _SIGS = {
                                     c_int, P]),
     "dfm_dwconv_bwd_weight_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "dfm_dwconv_bwd_weight": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P]),
+    "dfm_dwconv_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
+                               c_int, P, P, P, P]),
     "dfm_colsum_workspace": (c_size_t, [c_long, c_int]),
     "dfm_colsum": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_int, P, P]),
     "dfm_cast": (c_int, [c_int, c_int, c_long, P, P, P]),

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
     const int ow = ow0 + t;
     if (ow >= W) break;
     const long p = img + (long)oh * W + ow;
-    if (add_identity) {
+    if (add_identity & 1) {
       const uint4 q = xs[((row + R) * IW + strip * TWS + t + R) * NG + g];
       float xi[CPT];
       if constexpr (sizeof(T) == 2) {
@@ -177,12 +177,19 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
 #pragma unroll
       for (int e = 0; e < CPT; ++e) acc[t][e] += o[e];
     }
-    stv<T>(yp, acc[t]);
-    if (gout) {
-      float gv[CPT];
+    if (gout) {  // GELU output; y holds the pre-activation or (flag 2) its GELU derivative
+      float gv[CPT], dv[CPT];
 #pragma unroll
-      for (int e = 0; e < CPT; ++e) gv[e] = gelu_f(acc[t][e]);
+      for (int e = 0; e < CPT; ++e) {
+        float cdf, pdf;
+        normal_cdf_pdf(acc[t][e], cdf, pdf);
+        gv[e] = acc[t][e] * cdf;
+        dv[e] = fmaf(acc[t][e], pdf, cdf);
+      }
+      stv<T>(yp, (add_identity & 2) ? dv : acc[t]);
       stv<T>(gout + p * ldg + c0, gv);
+    } else {
+      stv<T>(yp, acc[t]);
     }
   }
 }
@@ -947,7 +954,7 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
 #pragma unroll
             for (int e = 0; e < CPT; ++e) acc[t][e] = fmaf(wv[a * 3 + j][e], xv[e], acc[t][e]);
           }
-          if (q >= 1 && q <= TW && add_identity) {
+          if (q >= 1 && q <= TW && (add_identity & 1)) {
             if (a == 1) {
 #pragma unroll
               for (int e = 0; e < CPT; ++e) acc[q - 1][e] += xv[e];
@@ -967,12 +974,19 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
 #pragma unroll
           for (int e = 0; e < CPT; ++e) acc[t][e] += o[e];
         }
-        w3_store<T>(yp, acc[t]);
-        if (gout) {
-          float gv[CPT];
+        if (gout) {  // GELU output; y holds the pre-activation or (flag 2) its GELU derivative
+          float gv[CPT], dv[CPT];
 #pragma unroll
-          for (int e = 0; e < CPT; ++e) gv[e] = gelu_f(acc[t][e]);
+          for (int e = 0; e < CPT; ++e) {
+            float cdf, pdf;
+            normal_cdf_pdf(acc[t][e], cdf, pdf);
+            gv[e] = acc[t][e] * cdf;
+            dv[e] = fmaf(acc[t][e], pdf, cdf);
+          }
+          w3_store<T>(yp, (add_identity & 2) ? dv : acc[t]);
           w3_store<T>(gout + p * ldg + c0, gv);
+        } else {
+          w3_store<T>(yp, acc[t]);
         }
       }
 #pragma unroll
@@ -994,6 +1008,186 @@ int f3_launch(int B, int H, int W, int C, const void* x, long ldx, const float* 
                      acc, (T*)gout, ldg);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
+}
+
+// ---------------------------------------------------------------- fused 3x3 backward (data + weight)
+// The ConvFFN's depthwise 3x3 + identity backward (DFormer.py:54,62) in ONE pass over dy and x:
+//   dx[h][w] (+)= sum_taps w[2-a][2-j] dy[h+a-1][w+j-1] + dy[h][w]     (identity)
+//   dw[a][j] += dy[h][w] x[h+a-1][w+j-1],  db += dy[h][w]              (per-block partials)
+// The separate kernels read dy twice (input gradient, weight gradient) and x once; here each lane
+// (one 8-byte channel vector, a TW-column strip walking a chunk of RC rows as in the streaming
+// weight gradient) keeps the three dy rows and the three x rows around output row h in registers,
+// loading the next row of each one ahead. dy is read once from HBM (its halo rows / columns from
+// L2), x once, dx written once. All FMAs are packed (v_pk_fma_f32 over channel pairs).
+template <typename T>
+DFM_INLINE void w3_pairs(uint2 q, f2v* v) {
+  if constexpr (std::is_same<T, f16_t>::value) {
+    v[0] = f2v{h2f((uint16_t)(q.x & 0xffffu)), h2f((uint16_t)(q.x >> 16))};
+    v[1] = f2v{h2f((uint16_t)(q.y & 0xffffu)), h2f((uint16_t)(q.y >> 16))};
+  } else if constexpr (sizeof(T) == 2) {
+    v[0] = f2v{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u)};
+    v[1] = f2v{__uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
+  } else {
+    v[0] = f2v{__uint_as_float(q.x), __uint_as_float(q.y)};
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void dw3_stream_bwd_kernel(int B, int H, int W, int C, int RC, int nstrips,
+                                                             int nchunks, int LPU, int UPW,
+                                                             const T* __restrict__ x, long ldx,
+                                                             const T* __restrict__ dy, long lddy,
+                                                             const float* __restrict__ w, int add_identity,
+                                                             T* __restrict__ dx, long lddx, int accumulate,
+                                                             float* __restrict__ part) {
+  constexpr int CPT = W3Cfg<T>::EPL, CP = CPT / 2, TW = W3_TW, NX = TW + 2, NV = 10 * CPT, VCH = 20;
+  __shared__ float red[4][VCH][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lg = lane % LPU, usub = lane / LPU;
+  const int G = C / CPT, cg = blockIdx.y * LPU + lg;
+  const bool valid = usub < UPW && cg < G;
+  const int c0 = cg * CPT;
+  const long units = w3_units(B, nstrips, nchunks);
+
+  f2v wf[9][CP];  // flipped taps (input gradient), centre tap + 1 when add_identity
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+    for (int e = 0; e < CP; ++e) {
+      const float idt = (tap == 4 && add_identity) ? 1.0f : 0.0f;
+      wf[tap][e] = valid ? f2v{w[(long)(c0 + 2 * e) * 9 + 8 - tap] + idt, w[(long)(c0 + 2 * e + 1) * 9 + 8 - tap] + idt}
+                         : f2v{0.f, 0.f};
+    }
+  f2v acc[10][CP];
+#pragma unroll
+  for (int a = 0; a < 10; ++a)
+#pragma unroll
+    for (int e = 0; e < CP; ++e) acc[a][e] = f2v{0.f, 0.f};
+
+  const long stride = (long)gridDim.x * 4 * UPW;
+  for (long u = ((long)blockIdx.x * 4 + wave) * UPW + usub; valid && u < units; u += stride) {
+    const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
+    const long b = u / ((long)nstrips * nchunks);
+    const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
+    const long img = b * H * W;
+    auto load_row = [&](const T* src, long ld, int h, uint2* r) {  // columns w0-1 .. w0+TW, zero outside
+      const bool hok = h >= 0 && h < H;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        const int ww = w0 - 1 + q;
+        r[q] = w3_ld<T>(src + (img + (long)h * W + ww) * ld + c0, hok && ww >= 0 && ww < W);
+      }
+    };
+    uint2 x0[NX], x1[NX], x2[NX], d0[NX], d1[NX], d2[NX];
+    load_row(x, ldx, h0 - 1, x0);
+    load_row(x, ldx, h0, x1);
+    load_row(x, ldx, h0 + 1, x2);
+    load_row(dy, lddy, h0 - 1, d0);
+    load_row(dy, lddy, h0, d1);
+    load_row(dy, lddy, h0 + 1, d2);
+    for (int h = h0; h < h1; ++h) {
+      uint2 xn[NX], dn[NX];
+      load_row(x, ldx, h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
+      load_row(dy, lddy, h + 1 < h1 ? h + 2 : H, dn);
+      f2v o[TW][CP];
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) o[t][e] = f2v{0.f, 0.f};
+      // weight gradient: the centre dy row against the three x rows
+      f2v gc[TW][CP];
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        w3_pairs<T>(d1[t + 1], gc[t]);
+#pragma unroll
+        for (int e = 0; e < CP; ++e) acc[9][e] += gc[t][e];
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const uint2* xr = a == 0 ? x0 : (a == 1 ? x1 : x2);
+        const uint2* dr = a == 0 ? d0 : (a == 1 ? d1 : d2);
+#pragma unroll
+        for (int q = 0; q < NX; ++q) {
+          f2v xv[CP], dv[CP];
+          w3_pairs<T>(xr[q], xv);
+          w3_pairs<T>(dr[q], dv);
+          // input column q feeds output column t with tap j = q - t
+#pragma unroll
+          for (int t = 0; t < TW; ++t) {
+            const int j = q - t;
+            if (j < 0 || j >= 3) continue;
+#pragma unroll
+            for (int e = 0; e < CP; ++e) {
+              acc[a * 3 + j][e] = __builtin_elementwise_fma(gc[t][e], xv[e], acc[a * 3 + j][e]);
+              o[t][e] = __builtin_elementwise_fma(wf[a * 3 + j][e], dv[e], o[t][e]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        const int ww = w0 + t;
+        if (ww >= W) break;
+        T* dp = dx + (img + (long)h * W + ww) * lddx + c0;
+        float ov[CPT];
+#pragma unroll
+        for (int e = 0; e < CP; ++e) {
+          ov[2 * e] = o[t][e].x;
+          ov[2 * e + 1] = o[t][e].y;
+        }
+        if (accumulate) {
+          float pv[CPT];
+          w3_unpack<T>(*reinterpret_cast<const uint2*>(dp), pv);
+#pragma unroll
+          for (int e = 0; e < CPT; ++e) ov[e] += pv[e];
+        }
+        w3_store<T>(dp, ov);
+      }
+#pragma unroll
+      for (int q = 0; q < NX; ++q) {
+        x0[q] = x1[q];
+        x1[q] = x2[q];
+        x2[q] = xn[q];
+        d0[q] = d1[q];
+        d1[q] = d2[q];
+        d2[q] = dn[q];
+      }
+    }
+  }
+
+  // block reduction over the 4 waves and the UPW units of a wave that share a channel vector
+  const long pbase = (long)blockIdx.x * C * 10;
+#pragma unroll
+  for (int vc = 0; vc < NV; vc += VCH) {
+    if (vc) __syncthreads();
+#pragma unroll
+    for (int v = 0; v < VCH; ++v)
+      if (vc + v < NV) {
+        const int V = vc + v, e = V % CPT;
+        const f2v pr = acc[V / CPT][e / 2];
+        red[wave][v][lane] = (e & 1) ? pr.y : pr.x;
+      }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < VCH * LPU; idx += 256) {
+      const int v = idx / LPU, l = idx % LPU, V = vc + v;
+      const int c = (blockIdx.y * LPU + l) * CPT + V % CPT;
+      if (V >= NV || c >= C) continue;
+      float sum = 0.f;
+      for (int wv = 0; wv < 4; ++wv)
+        for (int us = 0; us < UPW; ++us) sum += red[wv][v][us * LPU + l];
+      part[pbase + (long)c * 10 + V / CPT] = sum;
+    }
+  }
+}
+
+template <typename T>
+long b3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, const float* w,
+               int id, void* dx, long lddx, int acc, float* part, hipStream_t s) {
+  const W3Geom g = w3_geom<T>(B, H, W, C);
+  DFM_LAUNCH(dw3_stream_bwd_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C,
+                     g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, w, id,
+                     (T*)dx, lddx, acc, part);
+  return g.nsb;
 }
 
 static bool f3_enabled() {  // DFM_DW_F3=0 keeps the LDS-tiled 3x3 forward / input gradient everywhere (A/B)
@@ -1182,6 +1376,38 @@ extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, in
                     w7_geom<float>(B, H, W, C).nsb, w7_geom<bf16_t>(B, H, W, C).nsb, w7l_nsb<float>(B, H, W, C),
                     w7l_nsb<bf16_t>(B, H, W, C)});
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);
+}
+
+extern "C" int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
+                              const void* dy, long lddy, const float* w, int add_identity, void* dx, long lddx,
+                              int accumulate, float* dw, float* db, void* workspace, dfm_stream_t stream) {
+  DFM_CHECK_ARG(x && dy && w && dx && dw && workspace, "dfm_dwconv_bwd: null argument");
+  DFM_CHECK_ARG(k == 3, "dfm_dwconv_bwd: k=%d unsupported (3x3 only)", k);
+  DFM_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd: bad shape");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)workspace;
+  long nsb;
+  if (dtype == DFM_BF16) {
+    DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy) && dw_aligned<bf16_t>(C, dx, lddx),
+                  "dfm_dwconv_bwd: alignment");
+    nsb = b3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, w, add_identity, dx, lddx, accumulate, part, s);
+  } else if (dtype == DFM_F16) {
+    DFM_CHECK_ARG(dw_aligned<f16_t>(C, x, ldx) && dw_aligned<f16_t>(C, dy, lddy) && dw_aligned<f16_t>(C, dx, lddx),
+                  "dfm_dwconv_bwd: alignment");
+    nsb = b3_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, w, add_identity, dx, lddx, accumulate, part, s);
+  } else if (dtype == DFM_F32) {
+    DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy) && dw_aligned<float>(C, dx, lddx),
+                  "dfm_dwconv_bwd: alignment");
+    nsb = b3_launch<float>(B, H, W, C, x, ldx, dy, lddy, w, add_identity, dx, lddx, accumulate, part, s);
+  } else {
+    dfm_set_error("dfm_dwconv_bwd: bad dtype");
+    return DFM_ERR_DTYPE;
+  }
+  DFM_LAUNCH_CHECK();
+  DFM_LAUNCH(partial_sum_kernel<2>, dim3(cdiv((long)C * 10, 64)), dim3(1024), 0, s, (int)nsb, (long)C * 10,
+                     (const float*)part, dw, db, 10L, 0);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
 }
 
 extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,

@@ -274,9 +274,16 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
   if (a.beta != 0.0f) v += a.beta * (a.c_f32 ? ((const float*)a.C)[ci] : ldf((const TO*)a.C + ci));
   if (a.bias) v += a.bias[n];
   if (n >= a.act_col0) {
-    if (a.preact) stf((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), v);
-    if (a.act == 1) v = gelu_f(v);
-    else if (a.act == 2) v = fmaxf(v, 0.0f);
+    if (a.act == 3) {  // GELU; preact receives its derivative at the pre-activation
+      float cdf, pdf;
+      normal_cdf_pdf(v, cdf, pdf);
+      if (a.preact) stf((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), fmaf(v, pdf, cdf));
+      v *= cdf;
+    } else {
+      if (a.preact) stf((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), v);
+      if (a.act == 1) v = gelu_f(v);
+      else if (a.act == 2) v = fmaxf(v, 0.0f);
+    }
   }
   if (a.mul) {
     const float mv = ldf((const TO*)a.mul + (long)m * a.ldmul + n);
@@ -319,7 +326,17 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v, cons
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
   }
-  if (n >= a.act_col0) {  // act_col0 is a multiple of 8 whenever the vector path is taken
+  if (n >= a.act_col0 && a.act == 3) {  // GELU; preact receives its derivative at the pre-activation
+    float dv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float cdf, pdf;
+      normal_cdf_pdf(v[e], cdf, pdf);
+      dv[e] = fmaf(v[e], pdf, cdf);
+      v[e] *= cdf;
+    }
+    if (a.preact) st8<TO>((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), dv);
+  } else if (n >= a.act_col0) {  // act_col0 is a multiple of 8 whenever the vector path is taken
     if (a.preact) st8<TO>((TO*)a.preact + (long)m * a.ldpre + (n - a.act_col0), v);
     if (a.act == 1) {
 #pragma unroll

@@ -25,7 +25,7 @@ void dfm_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* dfm_last_error(void) { return g_err; }
-extern "C" int dfm_abi_version(void) { return 4; }  // 4: dfm_convffn_bwd takes w2 [C][hid]
+extern "C" int dfm_abi_version(void) { return 5; }  // 5: dfm_dwconv_bwd; GELU' output modes
 
 // ---------------------------------------------------------------- launch tracer
 // dfm_trace_flags is read by DFM_LAUNCH (common.h) before every kernel launch; 0 = tracer off and

@@ -219,6 +219,8 @@ def _cat1(*vs):
 # recomputes fc1 on a 2-pixel halo and the depthwise / GELU chain per hidden chunk at two waves per
 # SIMD, does not (stage 0 fwd+bwd 1.70 vs 1.51 ms; the whole step 367 vs 381 images/s).
 FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
+# DFM_DW_FUSED_BWD=0: the unfused ConvFFN backward runs the DW3x3 input and weight gradients as two kernels
+_DW_FUSED_BWD = os.environ.get("DFM_DW_FUSED_BWD", "1") == "1"
 
 
 def _ffn_fusable(x, w1, *aligned):
@@ -256,10 +258,12 @@ class ConvFFNFn(torch.autograd.Function):
             return out
         h = K.linear(xn, W1, b1)
         g = torch.empty_like(h)
-        hpre = K.dwconv(h, shape, wpos, bpos, 3, add_identity=True, gelu_out=g)
+        # the DW kernel writes GELU'(hpre) instead of hpre (GELU and its derivative share one erf):
+        # the backward's fc2 input gradient then multiplies instead of re-evaluating GELU'
+        gp = K.dwconv(h, shape, wpos, bpos, 3, add_identity=True, gelu_out=g, out_gelu_grad=True)
         f = torch.empty(P, C, device=x.device, dtype=dt)
         out = K.linear(g, W2, b2, preact=f, res=x, colscale=ls, rowscale=rowscale, rows_per_scale=H * W)
-        ctx.save_for_backward(x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
+        ctx.save_for_backward(x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
         return out
 
     @staticmethod
@@ -267,7 +271,7 @@ class ConvFFNFn(torch.autograd.Function):
         K.TAG = ctx.tag + ".bwd"
         if ctx.fused:
             return ConvFFNFn._backward_fused(ctx, dout)
-        x, xn, mu, rs, h, hpre, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
+        x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
         B, H, W = ctx.shape
         dt = x.dtype
         dout = dout.contiguous()
@@ -277,11 +281,14 @@ class ConvFFNFn(torch.autograd.Function):
         o2, ob2 = gslot2(w2), gslot(b2)
         dW2, db2 = offload_wgrad((o2, ob2), (df, g),
                                  lambda: K.linear_wgrad(df, g, out=o2, bias_grad=True, bias_out=ob2))
-        dhpre = K.linear_dgrad(df, W2, gelu_grad_of=hpre)  # GELU backward fused into the epilogue
+        dhpre = K.linear_dgrad(df, W2, mul=gp)  # GELU backward: times the stored GELU'(hpre)
         ow, ob = gslot(wpos), gslot(bpos)
-        dwpos, dbpos = offload_wgrad((ow, ob), (h, dhpre),
-                                     lambda: K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=ow, db=ob))
-        dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
+        if _DW_FUSED_BWD:  # input and weight gradients of DW3x3 + identity in one pass over dhpre, h
+            dh, dwpos, dbpos = K.dwconv_bwd(h, dhpre, ctx.shape, wpos, 3, add_identity=True, dw=ow, db=ob)
+        else:
+            dwpos, dbpos = offload_wgrad((ow, ob), (h, dhpre),
+                                         lambda: K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=ow, db=ob))
+            dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
         o1, ob1 = gslot2(w1), gslot(b1)
         dW1, db1 = offload_wgrad((o1, ob1), (dh, xn),
                                  lambda: K.linear_wgrad(dh, xn, out=o1, bias_grad=True, bias_out=ob1))
@@ -320,14 +327,18 @@ _ATTN_SIDE = {}
 # Measured on MI355X, DFormer-B bf16 bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s.
 _ATTN_BWD_SIDE_ON = os.environ.get("DFM_ATTN_BWD_STREAM", "1") == "1"
 _ATTN_BWD_SIDE = {}
+# DFM_ATTN_BWD_STREAM2=1 (with the above): the pooled-attention part of the RGB branch (bilinear,
+# attention, short_cut_linear and kv gradients) on a second side stream, overlapping the
+# conv-modulation part (q*a, a, DW7x7 gradients); dg = DW7x7^T(...) + dkv Wkv after the join.
+_ATTN_BWD_SIDE2_ON = os.environ.get("DFM_ATTN_BWD_STREAM2", "0") == "1"
 
 
-def _attn_bwd_side(dev):
-    if not _ATTN_BWD_SIDE_ON:
+def _attn_bwd_side(dev, which=1):
+    if not _ATTN_BWD_SIDE_ON or (which == 2 and not _ATTN_BWD_SIDE2_ON):
         return None
-    st = _ATTN_BWD_SIDE.get(dev)
+    st = _ATTN_BWD_SIDE.get((dev, which))
     if st is None:
-        st = _ATTN_BWD_SIDE[dev] = torch.cuda.Stream(device=dev)
+        st = _ATTN_BWD_SIDE[(dev, which)] = torch.cuda.Stream(device=dev)
         register_side_stream(st)
     return st
 
@@ -375,12 +386,13 @@ class AttentionFn(torch.autograd.Function):
         else:
             xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
-        # q | q_cut | l in one GEMM; GELU (and its pre-activation store) only on the l columns
+        # q | q_cut | l in one GEMM; GELU only on the l columns, whose derivative (act 3) is stored
+        # for the backward
         Wqcl = wcast(dt, wq, wqc, wl)
         bqcl = _cat1(bq, bqc, bl)
         qcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         lpre = torch.empty(P, C, device=dev, dtype=dt)
-        K.linear(xn, Wqcl, bqcl, act=1, preact=lpre, act_col0=C + Ch, out=qcl)
+        K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl)
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         xep = torch.empty(P, Ch, device=dev, dtype=dt)
         if side is not None:  # depth branch, part 2: e_back * cx (needs the q|q_cut|l GEMM)
@@ -503,7 +515,10 @@ class AttentionFn(torch.autograd.Function):
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
         dpooled_e = None
-        if window:
+        side2 = _attn_bwd_side(dev, 2) if (window and side is not None) else None
+        dkv = None
+
+        def pooled_branch():  # softmax(q_pool k^T) v over the pooled queries, DFormer.py:119-131
             kv, pooled, m, o, lse = saved_attn
             dh = C // heads // 2
             do = K.bilinear_bwd(df[:, C:C + Ch], (7, 7), (H, W), B)
@@ -516,10 +531,21 @@ class AttentionFn(torch.autograd.Function):
                 dm, pooled, out=ow, bias_grad=True, bias_out=ob))
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
-            dpooled_e = dpooled[:, C:]
             ow, ob = gslot2(wkv), gslot(bkv)
             grads["wkv"], grads["bkv"] = offload_wgrad((ow, ob), (dkv, g), lambda: K.linear_wgrad(
                 dkv, g, out=ow, bias_grad=True, bias_out=ob))
+            return dxn, dpooled, dkv, (do, dm)
+
+        if side2 is not None:  # the pooled-attention branch overlaps the conv-modulation branch
+            side2.wait_stream(main)
+            with torch.cuda.stream(side2):
+                dxn, dpooled, dkv, side2_tmp = pooled_branch()
+            for t in (df, g) + tuple(saved_attn):
+                t.record_stream(side2)
+            dpooled_e = dpooled[:, C:]
+        elif window:
+            dxn, dpooled, dkv, _ = pooled_branch()
+            dpooled_e = dpooled[:, C:]
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
@@ -531,8 +557,13 @@ class AttentionFn(torch.autograd.Function):
         ow, ob = gslot(wconv), gslot(bconv)
         grads["wconv"], grads["bconv"] = offload_wgrad((ow, ob), (g, dapre), lambda: K.dwconv_bwd_weight(
             g, dapre, shape, 7, dw=ow, db=ob))
-        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
-        K.gelu_bwd(dg, lpre, out=dl)
+        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window) and side2 is None)
+        if side2 is not None:  # join the pooled branch: dg += dkv Wkv
+            main.wait_stream(side2)
+            for t in (dxn, dpooled, dkv) + side2_tmp:
+                t.record_stream(main)
+            K.linear_dgrad(dkv, wcast(dt, wkv), out=dg, accumulate=True)
+        K.scale_mul(dg, mul=lpre, out=dl)  # lpre holds GELU'(l pre-activation)
         if side is not None:  # join the depth branch (dcx columns of dqcl, dxen)
             main.wait_stream(side)
             for t in (dxen,) + side_tmp:

@@ -270,13 +270,15 @@ def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2, dw=None, db=None):
 
 
 # ---------------------------------------------------------------------------- depthwise conv
-def dwconv(x, shape, w, bias, k, add_identity=False, out=None, gelu_out=None):
-    """x: [B*H*W, C] view (NHWC rows); w float32 [C,1,k,k] or [C,k,k]. gelu_out: also GELU(y)."""
+def dwconv(x, shape, w, bias, k, add_identity=False, out=None, gelu_out=None, out_gelu_grad=False):
+    """x: [B*H*W, C] view (NHWC rows); w float32 [C,1,k,k] or [C,k,k]. gelu_out: also GELU(y);
+    out_gelu_grad (with gelu_out): `out` receives GELU'(y) instead of y."""
     B, H, W = shape
     C = x.shape[1]
     if out is None:
         out = torch.empty(x.shape[0], C, device=x.device, dtype=x.dtype)
-    check(lib.dfm_dwconv_fwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(w), ptr(bias), int(add_identity),
+    flags = int(bool(add_identity)) | (2 if out_gelu_grad and gelu_out is not None else 0)
+    check(lib.dfm_dwconv_fwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(w), ptr(bias), flags,
                              ptr(out), ld(out), ptr(gelu_out), ld(gelu_out) if gelu_out is not None else 0,
                              stream()), "dfm_dwconv_fwd")
     if ACCOUNT is not None:
@@ -295,6 +297,25 @@ def dwconv_bwd_data(dy, shape, w, k, add_identity=False, dx=None, accumulate=Fal
     if ACCOUNT is not None:
         _acct(2 * k * k * C * dy.shape[0], dy.shape[0] * C * _es(dy) * (2 + bool(accumulate)))
     return dx
+
+
+def dwconv_bwd(x, dy, shape, w, k, add_identity=False, dx=None, accumulate=False, dw=None, db=None):
+    """Input gradient and weight / bias gradient of a 3x3 depthwise conv in one pass (dfm_dwconv_bwd)."""
+    B, H, W = shape
+    C = x.shape[1]
+    if dx is None:
+        dx = torch.empty(dy.shape[0], C, device=dy.device, dtype=dy.dtype)
+        accumulate = False
+    if dw is None:
+        dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
+    if db is None:
+        db = torch.empty(C, device=x.device, dtype=torch.float32)
+    ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
+    check(lib.dfm_dwconv_bwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(w), int(add_identity),
+                             ptr(dx), ld(dx), int(accumulate), ptr(dw), ptr(db), ptr(ws), stream()), "dfm_dwconv_bwd")
+    if ACCOUNT is not None:
+        _acct(4 * k * k * C * x.shape[0], x.shape[0] * C * _es(x) * (3 + bool(accumulate)))
+    return dx, dw, db
 
 
 def dwconv_bwd_weight(x, dy, shape, k, dw=None, db=None):

@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 4 (round 3: dfm_convffn_bwd takes w2 in its nn.Linear layout) */
+int dfm_abi_version(void); /* 5 (round 3: dfm_dwconv_bwd; dwconv flag 2 / GEMM act 3 store GELU') */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -66,7 +66,8 @@ const char* dfm_kernel_name(const void* func);
  *   and their backward (dX = dY W: a_kcontig=1,b_kcontig=0; dW = dY^T X: both 0, split_k).
  * Epilogue, in order (each optional):
  *   v += beta * C_old ; v += bias[n] ; [n >= act_col0: preact[m,n-act_col0] = v ; v = act(v)
- *   (1 gelu, 2 relu)] ;
+ *   (1 gelu, 2 relu, 3 gelu with preact[m,n-act_col0] = gelu'(v) instead of v: the GELU
+ *   backward becomes a plain product)] ;
  *   v *= mul[m,n] ; v = res[m,n] + colscale[n] * rowscale[m / rows_per_scale] * v ;
  *   C[m,n] = v (stored as dtype, or float32 when c_f32).
  * Operands A, B, mul, res, preact are `dtype`; C is dtype or float32 (c_f32).
@@ -127,8 +128,9 @@ int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout,
 
 /* ---------------------------------------------------------------- depthwise conv k x k, NHWC
  * DFormer.py:80-81 (7x7 conv/e_conv, pad 3) and DFormer.py:54,62 (3x3 pos + identity).
- * w: float32 [C][k][k], bias float32 [C] or NULL. add_identity: y += x. gelu_out (optional):
- * GELU(y) as well (the ConvFFN activation, DFormer.py:64).
+ * w: float32 [C][k][k], bias float32 [C] or NULL. add_identity (flags): bit 0: y += x; bit 1 (with
+ * gelu_out): y receives gelu'(y) instead of y. gelu_out (optional): GELU(y) as well (the ConvFFN
+ * activation, DFormer.py:64).
  * bwd_data: dx (+= when accumulate) = conv(dy, flipped w) (+ dy when add_identity).
  * bwd_weight: dw [C][k][k], db [C] (overwritten), workspace from dfm_dwconv_bwd_weight_workspace. */
 int dfm_dwconv_fwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const float* w,
@@ -141,6 +143,11 @@ size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k);
 int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
                           const void* dy, long lddy, float* dw, float* db, void* workspace,
                           dfm_stream_t stream);
+/* bwd_data and bwd_weight of a 3x3 in one pass over dy and x (the ConvFFN's pos conv): dx (+= when
+ * accumulate), dw, db as above; workspace from dfm_dwconv_bwd_weight_workspace (k = 3 only). */
+int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const void* dy,
+                   long lddy, const float* w, int add_identity, void* dx, long lddx, int accumulate, float* dw,
+                   float* db, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- fused ConvFFN
  * DFormer.py:48-67 (MLP: fc1 -> pos = DW3x3 + identity -> GELU -> fc2) inside the Block residual

@@ -264,6 +264,74 @@ def test_dwconv_strided_gelu_accumulate(dt, ks, B, H, W, C):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("ident,acc", [(True, False), (False, True)])
+# planes of every stage geometry incl. odd sizes, partial 64-lane channel slices (520) and strided views
+@pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16), (1, 33, 41, 40),
+                                     (1, 9, 10, 520), (2, 120, 160, 32), (3, 15, 20, 256)])
+def test_dwconv_fused_bwd(dt, ident, acc, B, H, W, C):
+    """dfm_dwconv_bwd (3x3 input + weight gradient in one pass) vs torch fp32, and vs the separate
+    kernels: the weight / bias gradients bit for bit (same partial geometry and summation order)."""
+    k = K()
+    xb = torch.randn(B * H * W, C + 8, device=DEV).to(dt)
+    x = xb[:, :C]
+    w = torch.randn(C, 1, 3, 3, device=DEV) / 3
+    xr = x.float().reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    wr, br = w.clone().requires_grad_(), torch.zeros(C, device=DEV, requires_grad=True)
+    ref = F.conv2d(xr, wr, br, padding=1, groups=C)
+    if ident:
+        ref = ref + xr
+    dyb = torch.randn(B * H * W, C + 16, device=DEV).to(dt)
+    dy = dyb[:, 16:]
+    ref.backward(dy.float().reshape(B, H, W, C).permute(0, 3, 1, 2))
+    base = torch.randn(B * H * W, C, device=DEV).to(dt)
+    dx = base.clone() if acc else None
+    dx, dw, db = k.dwconv_bwd(x, dy, (B, H, W), w, 3, add_identity=ident, dx=dx, accumulate=acc)
+    want = xr.grad + (base.float().reshape(B, H, W, C).permute(0, 3, 1, 2) if acc else 0)
+    assert rel(dx.float().reshape(B, H, W, C).permute(0, 3, 1, 2), want) < TOL[dt]
+    assert rel(dw, wr.grad) < TOL[dt] * 2
+    assert rel(db, br.grad) < TOL[dt]
+    dw2, db2 = k.dwconv_bwd_weight(x, dy, (B, H, W), 3)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 80), (2, 120, 160, 32), (1, 30, 40, 64)])
+def test_dwconv_gelu_grad_out(dt, B, H, W, C):
+    """Flag 2: y receives GELU'(pre) while gelu_out receives GELU(pre) (tile and streaming kernels)."""
+    k = K()
+    x = torch.randn(B * H * W, C, device=DEV).to(dt)
+    w = torch.randn(C, 1, 3, 3, device=DEV) / 3
+    bias = torch.randn(C, device=DEV)
+    pre = k.dwconv(x, (B, H, W), w, bias, 3, True)
+    g1 = torch.empty_like(x)
+    g2 = torch.empty_like(x)
+    gp = k.dwconv(x, (B, H, W), w, bias, 3, True, gelu_out=g1, out_gelu_grad=True)
+    k.dwconv(x, (B, H, W), w, bias, 3, True, gelu_out=g2)
+    assert torch.equal(g1, g2)
+    p = pre.float().requires_grad_()
+    F.gelu(p).sum().backward()
+    assert rel(gp.float(), p.grad) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_act3_gelu_grad_preact(dt):
+    """GEMM act 3: GELU on the columns from act_col0 (as act 1) and preact = GELU'(pre-activation)."""
+    k = K()
+    M, N, Kd, c0 = 700, 96, 64, 40
+    x = torch.randn(M, Kd, device=DEV).to(dt)
+    w = torch.randn(N, Kd, device=DEV).to(dt) / 8
+    b = torch.randn(N, device=DEV)
+    pre1 = torch.empty(M, N - c0, device=DEV, dtype=dt)
+    pre3 = torch.empty(M, N - c0, device=DEV, dtype=dt)
+    y1 = k.linear(x, w, b, act=1, preact=pre1, act_col0=c0)
+    y3 = k.linear(x, w, b, act=3, preact=pre3, act_col0=c0)
+    assert rel(y3.float(), y1.float()) < 1e-6  # the same GELU (contraction may differ in the last bit)
+    p = pre1.float().requires_grad_()
+    F.gelu(p).sum().backward()
+    assert rel(pre3.float(), p.grad) < TOL[dt] * 2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("H,W", [(15, 20), (8, 10), (5, 7), (60, 80), (17, 23)])
 def test_pool7(dt, H, W):
     k = K()
