@@ -38,6 +38,8 @@ _SIGS = {
     "dfm_abi_version": (c_int, []),
     "dfm_gemm_workspace_size": (c_size_t, [ctypes.POINTER(GemmDesc)]),
     "dfm_gemm": (c_int, [c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
+    "dfm_gemm_group_workspace_size": (c_size_t, [c_int, ctypes.POINTER(GemmDesc)]),
+    "dfm_gemm_group": (c_int, [c_int, c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
     "dfm_layernorm_fwd": (c_int, [c_int, c_long, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P]),
     "dfm_layernorm_bwd_workspace": (c_size_t, [c_long, c_int]),
     "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, P, c_long, c_int,

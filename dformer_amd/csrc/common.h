@@ -73,6 +73,16 @@ DFM_INLINE float gelu_grad_f(float x) {
   return fmaf(x, d, c);
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not its global
+// loads or stores (__syncthreads()' fence drains vmcnt, so a register prefetch of the next k-slice or
+// an epilogue's output stores would be waited for at every barrier); the inline asm's memory clobber
+// keeps the compiler from moving LDS accesses across it. Global loads are still waited for before
+// their registers are used (the compiler's per-register vmcnt tracking).
+DFM_INLINE void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 DFM_INLINE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -399,7 +399,7 @@ DFM_INLINE void gemm_epilogue(const GemmArgs& a, float4_t (&acc)[BM / WAVES_M / 
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     constexpr int ITEMS = (HALF * TPR + NT - 1) / NT;
     if (a.splits > 1) {  // fp32 partial tile -> workspace rows padded to ldw (16-byte stores)
 #pragma unroll
@@ -443,14 +443,22 @@ DFM_INLINE void gemm_epilogue(const GemmArgs& a, float4_t (&acc)[BM / WAVES_M / 
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
 // DEPTH 1: one register set (tile t+1 is requested while tile t is multiplied); DEPTH 2: two
 // sets, for long k-loops where one tile of MFMA work cannot cover a global-load round trip.
+// XCD-aware renumbering (bijective for any grid size; blocks id and id + 8 share an XCD): logical
+// block lid of a grid of nblk runs on XCD (lid's run), so consecutive logical blocks share one L2.
+DFM_INLINE int xcd_lid(int id, int nblk) {
+  const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+}
+
+// One output tile (tile, zs = batch * splits + split) of the register-staged MFMA GEMM.
 template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
-__global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
+DFM_INLINE void gemm_tile(const GemmArgs& a, int tile, int zs, char* smem) {
   constexpr int NT = 64 * NW;
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -459,25 +467,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
   using GA = TileGeom<T, BM, BK, AK, NT>;
   using GB = TileGeom<T, BN, BK, BKC, NT>;
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   T* const lds_base = reinterpret_cast<T*>(smem);
 #define LDS_A(i) (lds_base + (i) * GA::ELEMS)
 #define LDS_B(i) (lds_base + 2 * GA::ELEMS + (i) * GB::ELEMS)
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-  const int tiles_m = (a.M + BM - 1) / BM;  // grid.x enumerates M tiles fastest
-  int tile = blockIdx.x, zs = blockIdx.z;
-  if (a.xcd_map) {
-    // XCD-aware renumbering (bijective for any grid size; blocks id and id + 8 share an XCD): the
-    // tiles of one split-K slice — which read the same K range of both operands — run on one XCD,
-    // so the operand slices they share are re-read from that XCD's L2 instead of by all eight.
-    const int nblk = gridDim.x * gridDim.z, id = blockIdx.z * gridDim.x + blockIdx.x;
-    const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
-    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
-    tile = lid % gridDim.x;
-    zs = lid / gridDim.x;
-  }
+  const int tiles_m = (a.M + BM - 1) / BM;  // tiles enumerate M tiles fastest
   // n_fast: consecutive blocks walk the column tiles of one row tile, so a tall A row block (large-M
   // forward / dgrad with several column tiles) is re-read from L2 rather than from HBM
   const int bm = (a.n_fast ? tile / a.tiles_n : tile % tiles_m) * BM;
@@ -558,13 +554,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
     if (nfull >= 1) {
       load_fast(ra0, rb0, 0);
       store_fast(ra0, rb0, 0);
-      __syncthreads();
+      lds_barrier();
       int cur = 0;
       for (int kt = 0; kt + 1 < nfull; ++kt) {
         load_fast(ra0, rb0, kt + 1);
         compute(LDS_A(cur), LDS_B(cur));
         store_fast(ra0, rb0, cur ^ 1);
-        __syncthreads();
+        lds_barrier();
         cur ^= 1;
       }
       compute(LDS_A(cur), LDS_B(cur));
@@ -573,21 +569,21 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
   } else if (nfull == 1) {
     load_fast(ra0, rb0, 0);
     store_fast(ra0, rb0, 0);
-    __syncthreads();
+    lds_barrier();
     compute(LDS_A(0), LDS_B(0));
     done = 1;
   } else if (nfull >= 2) {
     load_fast(ra0, rb0, 0);
     load_fast(ra1, rb1, 1);
     store_fast(ra0, rb0, 0);
-    __syncthreads();
+    lds_barrier();
     // invariant: LDS buffer 0 holds tile kt, set 1 holds tile kt+1 (in flight). Loads past the
     // last whole tile re-read it (in-bounds, L2-hot) so every load is unconditional.
     for (int kt = 0;; kt += 2) {
       load_fast(ra0, rb0, min(kt + 2, nfull - 1));
       compute(LDS_A(0), LDS_B(0));
       store_fast(ra1, rb1, 1);
-      __syncthreads();
+      lds_barrier();
       if (kt + 2 >= nfull) {
         compute(LDS_A(1), LDS_B(1));
         done = kt + 2;
@@ -596,7 +592,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
       load_fast(ra1, rb1, min(kt + 3, nfull - 1));
       compute(LDS_A(1), LDS_B(1));
       store_fast(ra0, rb0, 0);
-      __syncthreads();
+      lds_barrier();
       if (kt + 3 >= nfull) {
         compute(LDS_A(0), LDS_B(0));
         done = kt + 3;
@@ -607,20 +603,73 @@ __global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
   // guarded tail: the partial last slice, or every slice of unaligned operands
   for (int kt = done; kt < nk; ++kt) {
     uint4 rta[GA::NVEC], rtb[GB::NVEC];
-    __syncthreads();
+    lds_barrier();
     const int k0 = kbeg + kt * BK;
     stage_load<T, BM, BK, AK, NT>(rta, A, a.lda, bm, k0, a.M, kend, a.ala);
     stage_load<T, BN, BK, BKC, NT>(rtb, Bp, a.ldb, bn, k0, a.N, kend, a.alb, ones_r);
     stage_store<T, BM, BK, AK, NT>(rta, LDS_A(0));
     stage_store<T, BN, BK, BKC, NT>(rtb, LDS_B(0));
-    __syncthreads();
+    lds_barrier();
     compute(LDS_A(0), LDS_B(0));
   }
-  __syncthreads();  // the epilogue reuses the operand LDS
+  lds_barrier();  // the epilogue reuses the operand LDS
 #undef LDS_A
 #undef LDS_B
 
   gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
+}
+
+// DEPTH 1: one register set (tile t+1 is requested while tile t is multiplied); DEPTH 2: two
+// sets, for long k-loops where one tile of MFMA work cannot cover a global-load round trip.
+template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
+__global__ __launch_bounds__(64 * NW) void gemm_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int tile = blockIdx.x, zs = blockIdx.z;  // grid.x enumerates the output tiles
+  if (a.xcd_map) {
+    // the tiles of one split-K slice — which read the same K range of both operands — run on one
+    // XCD, so the operand slices they share are re-read from that XCD's L2 instead of by all eight
+    const int lid = xcd_lid(blockIdx.z * gridDim.x + blockIdx.x, gridDim.x * gridDim.z);
+    tile = lid % gridDim.x;
+    zs = lid / gridDim.x;
+  }
+  gemm_tile<T, BM, BN, NW, WAVES_M, BK, AK, BKC, DEPTH>(a, tile, zs, smem);
+}
+
+// ---------------------------------------------------------------- grouped GEMM
+// Up to GMAX independent GEMMs of one tile configuration in ONE launch (the weight gradients of a
+// Block's backward, which are independent of each other and of the data-gradient chain): problem q
+// owns the blocks [start[q], start[q+1]) (start a multiple of 8, so the XCD renumbering inside a
+// problem sees the hardware XCD of each block); its tiles x batch x splits run as in gemm_kernel.
+// Sharing the chip between the problems lets each one use fewer split-K slices, and the split-K
+// partials of all problems are combined by ONE grouped reduction launch.
+constexpr int GMAX = 8;
+struct GemmGroup {
+  GemmArgs p[GMAX];
+  int start[GMAX + 1];
+  int n;
+};
+
+static_assert(sizeof(GemmGroup) <= 4096, "the problem table travels as a kernel argument");
+
+DFM_INLINE int group_problem(const GemmGroup& g, int b) {
+  int q = 0;
+#pragma unroll
+  for (int i = 1; i < GMAX; ++i)
+    if (i < g.n && b >= g.start[i]) q = i;
+  return q;
+}
+
+template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
+__global__ __launch_bounds__(64 * NW) void gemm_group_kernel(GemmGroup g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = blockIdx.x;
+  const int q = group_problem(g, b);
+  const GemmArgs& a = g.p[q];  // read in place from the kernel-argument segment (uniform scalar loads)
+  const int ntile = a.tiles_m * a.tiles_n, nblk = ntile * a.batch * a.splits;
+  const int local = b - g.start[q];
+  if (local >= nblk) return;  // padding up to the next multiple of 8
+  const int lid = xcd_lid(local, nblk);
+  gemm_tile<T, BM, BN, NW, WAVES_M, BK, AK, BKC, DEPTH>(a, lid % ntile, lid / ntile, smem);
 }
 
 // M-streaming GEMM for large M x short K (K a multiple of BK, 16-byte aligned operands, no
@@ -701,13 +750,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int ti
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
     store(0);
-    __syncthreads();
+    lds_barrier();
     int cur = 0;
     for (int kt = 0; kt + 1 < nk; ++kt) {
       load(kt + 1);
       compute(LDS_A(cur), LDS_B(cur));
       store(cur ^ 1);
-      __syncthreads();
+      lds_barrier();
       cur ^= 1;
     }
     compute(LDS_A(cur), LDS_B(cur));
@@ -723,7 +772,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int ti
     fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
     fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
     load(0);
-    __syncthreads();  // operand LDS reads done: the epilogue reuses it
+    lds_barrier();  // operand LDS reads done: the epilogue reuses it
     gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm_c, bn_c, 0, 0);
     if (!more) break;
     t = tn;
@@ -736,12 +785,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int ti
 // walk the splits in a fixed order (G = 4 when there are many splits, so short outputs x long
 // split counts still fill the chip), then the G partial sums meet in LDS.
 template <typename T, int G>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a) {
+DFM_INLINE void splitk_reduce_block(const GemmArgs& a, long blk) {
   constexpr int PER = 256 / G;
   __shared__ float red[G][PER];
   const long total = (long)a.batch * a.M * a.ldw;  // padded workspace elements per split
   const int o = threadIdx.x % PER, g = threadIdx.x / PER;
-  const long idx = blockIdx.x * (long)PER + o;
+  const long idx = blk * PER + o;
   float v = 0.f;
   if (idx < total) {
     const float* p = a.ws + idx;
@@ -761,6 +810,20 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a) {
   const long bm = idx / a.ldw;
   const int m = bm % a.M, b = bm / a.M;
   epilogue_store<T>(a, b, m, n, v);
+}
+
+template <typename T, int G>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmArgs a) {
+  splitk_reduce_block<T, G>(a, blockIdx.x);
+}
+
+// grouped combine: problem q (with splits > 1) owns reduction blocks [start[q], start[q+1])
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_group_kernel(GemmGroup g) {
+  const int q = group_problem(g, blockIdx.x);
+  const GemmArgs& a = g.p[q];
+  if (a.splits <= 1) return;
+  splitk_reduce_block<T, 4>(a, blockIdx.x - g.start[q]);
 }
 
 // ---------------------------------------------------------------- LDS-DMA pipelined GEMM (bf16)
@@ -1241,6 +1304,118 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   return launch_depth<T, 128, 128, 8, 2, BKl>(a, ak, bk, s);
 }
 
+// ---- grouped launch (host)
+// The group's split-K choice: every problem gets split-K slices in proportion to its share of the
+// group's work (tiles x K), so the ~512 blocks of the launch (two per CU) each reduce about the
+// same K range (at least 512 elements); d->split_k >= 1 forces a problem's count.
+void group_splits(int n, const DfmGemmDesc* d, int* splits) {
+  double work = 0;
+  for (int q = 0; q < n; ++q) {
+    const int Nw = d[q].N + (d[q].colsum ? 1 : 0);
+    work += (double)cdiv(d[q].M, 128) * cdiv(Nw, 128) * (d[q].batch > 0 ? d[q].batch : 1) * d[q].K;
+  }
+  const double per_blk = std::max(512.0, work / 512.0);
+  for (int q = 0; q < n; ++q) {
+    if (d[q].split_k >= 1) {
+      splits[q] = d[q].split_k;
+      continue;
+    }
+    const double want = d[q].K / per_blk;
+    int p2 = 1;
+    while (2.0 * p2 <= want && p2 < 256) p2 *= 2;
+    splits[q] = p2;
+  }
+}
+
+size_t group_ws_bytes(const DfmGemmDesc* d, int splits) {
+  if (splits <= 1) return 0;
+  const long ldw = (d->N + (d->colsum ? 1 : 0) + 7) & ~7L;
+  return (size_t)splits * (d->batch > 0 ? d->batch : 1) * d->M * ldw * sizeof(float);
+}
+
+template <typename T>
+void fill_args(GemmArgs& a, const DfmGemmDesc* d, const void* A, const void* B, void* C, float* ws, int splits) {
+  constexpr int VEC = Mf<T>::VEC;
+  a = GemmArgs{};
+  a.A = A; a.B = B; a.C = C; a.ws = ws;
+  a.M = d->M; a.N = d->N; a.K = d->K; a.batch = d->batch > 0 ? d->batch : 1;
+  a.Nw = d->N + (d->colsum ? 1 : 0);
+  a.ldw = (a.Nw + 7) & ~7;
+  a.lda = d->lda; a.ldb = d->ldb; a.ldc = d->ldc;
+  a.sa = d->stride_a; a.sb = d->stride_b; a.sc = d->stride_c;
+  a.alpha = d->alpha; a.beta = d->beta; a.c_f32 = d->c_f32;
+  a.bias = d->bias; a.act = d->act; a.preact = d->preact; a.ldpre = d->ldpre;
+  a.mul = d->mul; a.ldmul = d->ldmul; a.res = d->res; a.ldres = d->ldres; a.mul_gelu_grad = d->mul_gelu_grad;
+  a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
+  a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
+  a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
+  a.splits = splits;
+  const double ext_a = ((double)(d->a_kcontig ? d->M : d->K) * d->lda) * sizeof(T);
+  const double ext_b = ((double)(d->b_kcontig ? d->N : d->K) * d->ldb) * sizeof(T);
+  a.ala = (d->lda % VEC == 0) && ((uintptr_t)A % 16 == 0) && (a.batch == 1 || d->stride_a % VEC == 0) &&
+          ext_a < 2147483647.0;
+  a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0) &&
+          ext_b < 2147483647.0;
+  a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
+             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
+}
+
+template <typename T, bool AK, bool BKC>
+int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C, char* ws,
+                 hipStream_t s) {
+  constexpr int BM = 128, BN = 128, NW = 8, WM_ = 2, BK = sizeof(T) == 2 ? 64 : 32, DEPTH = 2;
+  using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
+  using GB = TileGeom<T, BN, BK, BKC, 64 * NW>;
+  const size_t lds_op = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
+  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
+  const size_t lds = std::max(lds_op, (size_t)RP * (BN + 4) * sizeof(float));
+  auto kern = gemm_group_kernel<T, BM, BN, NW, WM_, BK, AK, BKC, DEPTH>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  int splits[GMAX];
+  group_splits(n, d, splits);
+  GemmGroup g;
+  GemmGroup r;  // the same problems with the reduction's block ranges
+  g.n = r.n = n;
+  g.start[0] = r.start[0] = 0;
+  size_t off = 0;
+  bool any_split = false;
+  for (int q = 0; q < n; ++q) {
+    fill_args<T>(g.p[q], &d[q], A[q], B[q], C[q], splits[q] > 1 ? (float*)(ws + off) : nullptr, splits[q]);
+    off += group_ws_bytes(&d[q], splits[q]);
+    g.p[q].xcd_map = 1;
+    g.p[q].tiles_m = cdiv(d[q].M, BM);
+    g.p[q].tiles_n = cdiv(g.p[q].Nw, BN);
+    g.p[q].n_fast = 0;
+    const int nblk = g.p[q].tiles_m * g.p[q].tiles_n * g.p[q].batch * splits[q];
+    g.start[q + 1] = g.start[q] + (nblk + 7) / 8 * 8;
+    r.p[q] = g.p[q];
+    const long total = (long)g.p[q].batch * g.p[q].M * g.p[q].ldw;
+    r.start[q + 1] = r.start[q] + (splits[q] > 1 ? (int)cdiv(total, 64) : 0);
+    any_split = any_split || splits[q] > 1;
+  }
+  DFM_LAUNCH(kern, dim3((unsigned)g.start[n]), dim3(64 * NW), lds, s, g);
+  DFM_LAUNCH_CHECK();
+  if (any_split) {
+    DFM_LAUNCH(splitk_reduce_group_kernel<T>, dim3((unsigned)r.start[n]), dim3(256), 0, s, r);
+    DFM_LAUNCH_CHECK();
+  }
+  return DFM_OK;
+}
+
+template <typename T>
+int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
+                     void* ws, hipStream_t s) {
+  const bool ak = d[0].a_kcontig, bk = d[0].b_kcontig;
+  if (ak && bk) return group_launch<T, true, true>(n, d, A, B, C, (char*)ws, s);
+  if (ak) return group_launch<T, true, false>(n, d, A, B, C, (char*)ws, s);
+  if (bk) return group_launch<T, false, true>(n, d, A, B, C, (char*)ws, s);
+  return group_launch<T, false, false>(n, d, A, B, C, (char*)ws, s);
+}
+
 }  // namespace
 
 extern "C" size_t dfm_gemm_workspace_size(const DfmGemmDesc* d) {
@@ -1264,5 +1439,36 @@ extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const vo
   if (dtype == DFM_F16) return gemm_typed<f16_t>(d, A, B, C, ws, s);
   if (dtype == DFM_F32) return gemm_typed<float>(d, A, B, C, ws, s);
   dfm_set_error("dfm_gemm: unsupported dtype %d", dtype);
+  return DFM_ERR_DTYPE;
+}
+
+extern "C" size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d) {
+  if (n < 1 || n > GMAX || d == nullptr) return 0;
+  int splits[GMAX];
+  group_splits(n, d, splits);
+  size_t total = 0;
+  for (int q = 0; q < n; ++q) total += group_ws_bytes(&d[q], splits[q]);
+  return total;
+}
+
+extern "C" int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
+                              void* const* C, void* ws, dfm_stream_t stream) {
+  DFM_CHECK_ARG(d && A && B && C && n >= 1 && n <= GMAX, "dfm_gemm_group: 1 <= n <= %d problems", GMAX);
+  for (int q = 0; q < n; ++q) {
+    DFM_CHECK_ARG(A[q] && B[q] && C[q], "dfm_gemm_group: null operand (problem %d)", q);
+    DFM_CHECK_ARG(d[q].M > 0 && d[q].N > 0 && d[q].K >= 0, "dfm_gemm_group: bad size (problem %d)", q);
+    DFM_CHECK_ARG(d[q].a_kcontig == d[0].a_kcontig && d[q].b_kcontig == d[0].b_kcontig,
+                  "dfm_gemm_group: problems must share one operand layout");
+    DFM_CHECK_ARG(d[q].a_kcontig ? d[q].lda >= d[q].K : d[q].lda >= d[q].M, "dfm_gemm_group: lda too small");
+    DFM_CHECK_ARG(d[q].b_kcontig ? d[q].ldb >= d[q].K : d[q].ldb >= d[q].N, "dfm_gemm_group: ldb too small");
+    DFM_CHECK_ARG(d[q].ldc >= d[q].N, "dfm_gemm_group: ldc too small");
+    DFM_CHECK_ARG(d[q].colsum == nullptr || d[q].batch <= 1, "dfm_gemm_group: colsum needs batch 1");
+  }
+  DFM_CHECK_ARG(ws != nullptr || dfm_gemm_group_workspace_size(n, d) == 0, "dfm_gemm_group: split-K needs a workspace");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFM_BF16) return gemm_group_typed<bf16_t>(n, d, A, B, C, ws, s);
+  if (dtype == DFM_F16) return gemm_group_typed<f16_t>(n, d, A, B, C, ws, s);
+  if (dtype == DFM_F32) return gemm_group_typed<float>(n, d, A, B, C, ws, s);
+  dfm_set_error("dfm_gemm_group: unsupported dtype %d", dtype);
   return DFM_ERR_DTYPE;
 }

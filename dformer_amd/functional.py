@@ -271,6 +271,11 @@ class ConvFFNFn(torch.autograd.Function):
         K.TAG = ctx.tag + ".bwd"
         if ctx.fused:
             return ConvFFNFn._backward_fused(ctx, dout)
+        with K.wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
+            return ConvFFNFn._backward_unfused(ctx, dout)
+
+    @staticmethod
+    def _backward_unfused(ctx, dout):
         x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
         B, H, W = ctx.shape
         dt = x.dtype
@@ -446,6 +451,11 @@ class AttentionFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx1, dxe1):
         K.TAG = ctx.tag + ".bwd"
+        with K.wgrad_group():  # the Block attention's weight gradients as grouped launches at the end
+            return AttentionFn._backward(ctx, dx1, dxe1)
+
+    @staticmethod
+    def _backward(ctx, dx1, dxe1):
         sv = ctx.saved_tensors
         (x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1, p1e, rowscale,
          rowscale_e) = sv[:20]

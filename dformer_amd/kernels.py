@@ -5,6 +5,7 @@ All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose la
 Activations are float32 or bfloat16; statistics / params / param-grads are float32.
 """
 import ctypes
+import os
 
 import torch
 
@@ -90,10 +91,57 @@ def rows_of(t):
 
 
 # ------------------------------------------------------------------------------------------ GEMM
+# ------------------------------------------------------------------ grouped weight gradients
+# Inside `with wgrad_group():` the weight-gradient GEMMs (linear_wgrad) are not launched one by one:
+# they are queued and issued at the end of the block as grouped launches (dfm_gemm_group, up to 8
+# problems each + one split-K combine), so the independent dW GEMMs of a Block's backward share the
+# chip instead of each splitting K over all of it. Their outputs must not be read before the block
+# ends (they only feed the optimizer). DFM_WGRAD_GROUP=0: immediate launches (A/B timing).
+WGRAD_GROUP = os.environ.get("DFM_WGRAD_GROUP", "1") == "1"
+_WG_PENDING = None
+
+
+class wgrad_group:
+    def __enter__(self):
+        global _WG_PENDING
+        self.prev = _WG_PENDING
+        _WG_PENDING = [] if WGRAD_GROUP else None
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        global _WG_PENDING
+        pending, _WG_PENDING = _WG_PENDING, self.prev
+        if pending and exc_type is None:
+            flush_wgrad(pending)
+        return False
+
+
+def flush_wgrad(pending):
+    """Issue queued GEMMs as grouped launches: problems of one dtype / operand layout, 8 per launch."""
+    classes = {}
+    for item in pending:
+        d, dt = item[0], item[1]
+        classes.setdefault((dt, d.a_kcontig, d.b_kcontig), []).append(item)
+    for (dt, _, _), items in classes.items():
+        for i in range(0, len(items), 8):
+            chunk = items[i:i + 8]
+            n = len(chunk)
+            descs = (_lib.GemmDesc * n)(*[c[0] for c in chunk])
+            pa = (ctypes.c_void_p * n)(*[c[2].data_ptr() for c in chunk])
+            pb = (ctypes.c_void_p * n)(*[c[3].data_ptr() for c in chunk])
+            pc = (ctypes.c_void_p * n)(*[c[4].data_ptr() for c in chunk])
+            dev = chunk[0][2].device
+            ws = _ws(lib.dfm_gemm_group_workspace_size(n, descs), dev)
+            check(lib.dfm_gemm_group(dt, n, descs, ctypes.cast(pa, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p),
+                                     ctypes.cast(pc, ctypes.c_void_p), ptr(ws), stream()), "dfm_gemm_group")
+            if ACCOUNT is not None:
+                _acct(sum(c[5] for c in chunk), sum(c[6] for c in chunk), chunk[0][7])
+
+
 def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
          ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
-         colsum_accumulate=False, mul_gelu_grad=False):
+         colsum_accumulate=False, mul_gelu_grad=False, defer=False):
     dt = dtype_code(a)
     assert b.dtype == a.dtype, (a.dtype, b.dtype)
     c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
@@ -106,16 +154,21 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     if GEMM_TRACE is not None:
         GEMM_TRACE.append({f: getattr(d, f) for f, _ in d._fields_ if not f in ("alpha", "beta")} |
                           {"dtype": dt, "beta": d.beta, "out_f32": out.dtype == torch.float32})
+    es, nb = _es(a), max(batch, 1)
+    byt = es * (M * K * nb + N * K * (nb if stride_b else 1))
+    byt += M * N * nb * (out.element_size() * (2 if beta != 0.0 else 1))
+    byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None))
+    byt += 4 * N * (bias is not None) + 4 * M * (colsum is not None)
+    peak = "bf16" if a.dtype != torch.float32 else "f32"
+    if defer and _WG_PENDING is not None and a.is_cuda:
+        # queued for the block's grouped launch; the tensors stay referenced until it is issued
+        _WG_PENDING.append((d, dt, a, b, out, 2.0 * M * N * K * nb, byt, peak, colsum, bias))
+        return out
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
     if ACCOUNT is not None:
-        es, nb = _es(a), max(batch, 1)
-        byt = es * (M * K * nb + N * K * (nb if stride_b else 1))
-        byt += M * N * nb * (out.element_size() * (2 if beta != 0.0 else 1))
-        byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None))
-        byt += 4 * N * (bias is not None) + 4 * M * (colsum is not None)
-        _acct(2.0 * M * N * K * nb, byt, "bf16" if a.dtype != torch.float32 else "f32")
+        _acct(2.0 * M * N * K * nb, byt, peak)
     return out
 
 
@@ -157,7 +210,7 @@ def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False, bias_out=No
     if bias_grad:
         db = bias_out if bias_out is not None else torch.empty(N, device=dy.device, dtype=torch.float32)
     gemm(dy, x, M=N, N=K, K=M, a_kcontig=False, b_kcontig=False, lda=ld(dy), ldb=ld(x), out=out,
-         ldc=ld(out), beta=1.0 if accumulate else 0.0, colsum=db, colsum_accumulate=accumulate)
+         ldc=ld(out), beta=1.0 if accumulate else 0.0, colsum=db, colsum_accumulate=accumulate, defer=True)
     return (out, db) if bias_grad else out
 
 

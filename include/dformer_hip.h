@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 5 (round 3: dfm_dwconv_bwd; dwconv flag 2 / GEMM act 3 store GELU') */
+int dfm_abi_version(void); /* 6 (round 3: dfm_gemm_group, dfm_dwconv_bwd, GELU' output modes) */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -102,6 +102,13 @@ typedef struct DfmGemmDesc {
 size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);
 int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const void* B, void* C, void* workspace,
              dfm_stream_t stream);
+/* n (1..8) independent GEMMs of one operand layout in ONE launch (+ one split-K combine launch):
+ * the weight gradients of a Block's backward (DFormer.py:76-95 / 53-55 nn.Linear backward), which
+ * share the chip instead of each splitting K across all of it. Same semantics per problem as
+ * dfm_gemm (epilogue, colsum bias gradient); workspace from dfm_gemm_group_workspace_size. */
+size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d);
+int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
+                   void* const* C, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm, channels_last
  * DFormer.py:21-45 (F.layer_norm over the last dim, eps 1e-6). mean/rstd: float32 [rows].

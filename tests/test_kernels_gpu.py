@@ -600,3 +600,41 @@ def test_dual_mul(dt, C):
     o1, o2 = k.dual_mul(src, m1, m2, out1=outb[:, :C], out2=outb[:, C + 8:2 * C + 8])
     assert rel(o1.float(), src.float() * m1.float()) < TOL[dt]
     assert rel(o2.float(), src.float() * m2.float()) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("rows", [19200, 777, 4800])
+def test_wgrad_group(dt, rows):
+    """dfm_gemm_group: the weight gradients queued inside kernels.wgrad_group() (different M / N, bias
+    gradient columns, an accumulating problem, strided operand views) against torch fp32 and against
+    the same GEMMs launched one by one."""
+    k = K()
+    shapes = [(256, 256, True), (640, 256, True), (128, 128, False), (384, 512, True), (64, 96, True),
+              (1024, 256, True), (256, 1024, False), (128, 384, True), (32, 48, True)]
+    dys, xs, refs = [], [], []
+    for n_out, n_in, bias in shapes:
+        dyb = torch.randn(rows, n_out + 8, device=DEV).to(dt)
+        dys.append(dyb[:, 8:])
+        xs.append(torch.randn(rows, n_in, device=DEV).to(dt))
+    base = torch.randn(128, 128, device=DEV)
+    outs = []
+    with k.wgrad_group():
+        for i, (n_out, n_in, bias) in enumerate(shapes):
+            if i == 2:  # accumulate into an existing gradient
+                o = base.clone()
+                k.linear_wgrad(dys[i], xs[i], out=o, accumulate=True)
+                outs.append((o, None))
+            else:
+                outs.append(k.linear_wgrad(dys[i], xs[i], bias_grad=bias) if bias else (k.linear_wgrad(dys[i], xs[i]), None))
+    for i, (n_out, n_in, bias) in enumerate(shapes):
+        ref = dys[i].float().t() @ xs[i].float()
+        if i == 2:
+            ref = ref + base
+        dw, db = outs[i]
+        assert rel(dw, ref) < TOL[dt] * 2, (i, rel(dw, ref))
+        if bias:
+            assert rel(db, dys[i].float().sum(0)) < TOL[dt], i
+        single = k.linear_wgrad(dys[i], xs[i], bias_grad=bias)
+        sw = single[0] if bias else single
+        if i != 2:
+            assert rel(dw, sw) < (1e-5 if dt == torch.float32 else TOL[dt]), i

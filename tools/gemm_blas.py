@@ -7,6 +7,12 @@ prints per-shape microseconds and per-step totals. Tells which shapes the hand-w
 loses on and by how much, i.e. what the tile/pipeline work has left to win.
 
     python tools/gemm_blas.py --sweep gpurun_out/gemm_sweep_r02.json --out gpurun_out/gemm_blas.json
+
+Batched shapes are skipped: in round 3 a run faulted the GPU (illegal address) on the first batched
+bf16 shape of the list (M=4800, N=512, K=896, batch 16, transposed-B view), inside the timed pair of
+this tool's own launches, after 79 shapes had completed; the library kernel of that shape runs in
+every training step (the NMF backward's input gradient), so the torch.matmul / hipBLASLt call on the
+strided batched view is the suspect, not confirmed. Results of that run: profiles/r03_gemm_blas.txt.
 """
 import argparse
 import json
@@ -72,6 +78,8 @@ def main():
     out, tm, tb, td = [], 0.0, 0.0, 0.0
     for r in rows:
         d = r["desc"]
+        if d["batch"] > 1:
+            continue
         t_mine, t_blas, em, eb = run(d)
         cnt = r["count"]
         tm += cnt * t_mine
