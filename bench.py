@@ -149,12 +149,13 @@ def dominant_roofline(table, name, durations_ms):
     peak = MFMA_PEAK_TFS[r["peak"] or "bf16"]
     t_mfma, t_hbm = fl / (peak * 1e12), by / (HBM_PEAK_GBS * 1e9)
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r02_dominant_pmc.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            rec = json.load(f)
-        if rec.get("kernel") == name:
-            traffic = rec.get("traffic_bytes_per_launch")
+    for pmc in (os.path.join(HERE, "profiles", "r03_pmc_dominant.json"), os.path.join(HERE, "profiles", "r02_dominant_pmc.json")):
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                rec = json.load(f)
+            if rec.get("kernel") == name:
+                traffic = rec.get("traffic_bytes_per_launch")
+                break
     if t_mfma >= t_hbm:
         ach = fl / avg_s / 1e12
         out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
@@ -162,6 +163,9 @@ def dominant_roofline(table, name, durations_ms):
         ach = by / avg_s / 1e9
         out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(ach / HBM_PEAK_GBS, 4)}
+    # exact per-launch roofline: sum over the census launches of max(F_i/P, B_i/BW) (launches of one kernel
+    # have different shapes, some HBM-, some MFMA-bound) over the probe's mean launch time
+    out["frac_exact"] = round(r["ideal_ms"] / n_c * 1e-3 / avg_s, 4)
     out.update(traffic=traffic, kernel=name, launches=len(durations_ms), avg_us=round(avg_s * 1e6, 2),
                bytes_per_launch=round(by), flops_per_launch=round(fl),
                census_share=round(r["measured_ms"] / max(sum(t["measured_ms"] for t in table.values()), 1e-9), 4))

@@ -1309,12 +1309,16 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 // group's work (tiles x K), so the ~512 blocks of the launch (two per CU) each reduce about the
 // same K range (at least 512 elements); d->split_k >= 1 forces a problem's count.
 void group_splits(int n, const DfmGemmDesc* d, int* splits) {
+  static const double target = [] {  // DFM_WG_BLOCKS: the grouped launch's block target (A/B timing)
+    const char* e = getenv("DFM_WG_BLOCKS");
+    return e ? std::max(64.0, atof(e)) : 512.0;
+  }();
   double work = 0;
   for (int q = 0; q < n; ++q) {
     const int Nw = d[q].N + (d[q].colsum ? 1 : 0);
     work += (double)cdiv(d[q].M, 128) * cdiv(Nw, 128) * (d[q].batch > 0 ? d[q].batch : 1) * d[q].K;
   }
-  const double per_blk = std::max(512.0, work / 512.0);
+  const double per_blk = std::max(512.0, work / target);
   for (int q = 0; q < n; ++q) {
     if (d[q].split_k >= 1) {
       splits[q] = d[q].split_k;

@@ -170,6 +170,29 @@ def offload_wgrad(outs, inputs, fn):
     return r
 
 
+# DFM_WGRAD_GROUP_STREAM=1: a Block's grouped weight-gradient launches (kernels.wgrad_group) are issued
+# on the weight-gradient stream, forked from the current stream at the end of the Block's backward,
+# so they overlap the next Block's data-gradient chain (joined like the offloaded weight gradients).
+_WG_GROUP_SIDE = os.environ.get("DFM_WGRAD_GROUP_STREAM", "0") == "1"
+
+
+def _flush_wgrad_side(pending):
+    dev = pending[0][2].device
+    ws = _wg_stream(dev)
+    ws.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(ws):
+        K.flush_wgrad(pending)
+    for item in pending:  # operands / outputs stay allocated until the stream is done with them
+        for t in item[2:5] + item[8:10]:
+            if t is not None:
+                t.record_stream(ws)
+
+
+def wgrad_group():
+    """The weight-gradient queue of one Block backward (kernels.wgrad_group)."""
+    return K.wgrad_group(_flush_wgrad_side if _WG_GROUP_SIDE else None)
+
+
 def join_wgrad():
     """The current stream waits for every weight-gradient launch issued so far."""
     for dev, s in _WG_STREAM.items():
@@ -271,7 +294,7 @@ class ConvFFNFn(torch.autograd.Function):
         K.TAG = ctx.tag + ".bwd"
         if ctx.fused:
             return ConvFFNFn._backward_fused(ctx, dout)
-        with K.wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
+        with wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
             return ConvFFNFn._backward_unfused(ctx, dout)
 
     @staticmethod
@@ -451,7 +474,7 @@ class AttentionFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx1, dxe1):
         K.TAG = ctx.tag + ".bwd"
-        with K.wgrad_group():  # the Block attention's weight gradients as grouped launches at the end
+        with wgrad_group():  # the Block attention's weight gradients as grouped launches at the end
             return AttentionFn._backward(ctx, dx1, dxe1)
 
     @staticmethod

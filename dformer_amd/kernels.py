@@ -102,6 +102,12 @@ _WG_PENDING = None
 
 
 class wgrad_group:
+    """Queue the weight-gradient GEMMs issued inside; at exit issue them with `flush` (default
+    flush_wgrad on the current stream)."""
+
+    def __init__(self, flush=None):
+        self.flush = flush
+
     def __enter__(self):
         global _WG_PENDING
         self.prev = _WG_PENDING
@@ -112,7 +118,7 @@ class wgrad_group:
         global _WG_PENDING
         pending, _WG_PENDING = _WG_PENDING, self.prev
         if pending and exc_type is None:
-            flush_wgrad(pending)
+            (self.flush or flush_wgrad)(pending)
         return False
 
 
