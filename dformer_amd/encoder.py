@@ -108,6 +108,9 @@ class Attention(nn.Module):
 
 _SIDE = {}
 _STREAMS = os.environ.get("DFM_STREAMS", "1") != "0"  # DFM_STREAMS=0: one stream (A/B timing)
+# DFM_SIDE_FROM=i: the depth-branch ConvFFN side stream only from stage i on (the stage-0 kernels are
+# thousands of blocks each, HBM-bound on their own)
+_SIDE_FROM = int(os.environ.get("DFM_SIDE_FROM", "0"))
 
 
 def _side_stream(dev):
@@ -176,7 +179,7 @@ class Block(nn.Module):
         # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
         # does its backward: autograd replays a node on its forward's stream), which fills the GPU
         # at the late stages where each kernel alone is latency-bound
-        side = _side_stream(x.device) if x1.is_cuda else None
+        side = _side_stream(x.device) if x1.is_cuda and int(st[1:] if st[1:].isdigit() else 9) >= _SIDE_FROM else None
         if side is not None:
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
@@ -304,11 +307,8 @@ class ConvS2Fn(torch.autograd.Function):
 
 
 # The stem / downsample layers run natively: 3x3 stride-2 convs as gather + MFMA GEMM with their
-# BatchNorms (+ GELU) folded into the gather (ConvS2Fn), the stem's last BN on BNRowsFn.
-# DFM_NATIVE_STEM=0 selects torch's convolutions (MIOpen) with the library's BN kernels for A/B
-# timing; DFM_NATIVE_STEM_BN=0 additionally puts the BatchNorms back on torch.
-_NATIVE_STEM = os.environ.get("DFM_NATIVE_STEM", "1") == "1"
-_NATIVE_STEM_BN = os.environ.get("DFM_NATIVE_STEM_BN", "1") == "1"
+# BatchNorms (+ GELU) folded into the gather (ConvS2Fn), the stem's last BN on BNRowsFn. There is no
+# vendor-convolution path.
 
 
 def _run_downsample_native(seq, x, dt):
@@ -337,20 +337,6 @@ def _run_downsample_native(seq, x, dt):
             x = y.view(B, Ho, Wo, m.out_channels).permute(0, 3, 1, 2)
             pend_bn, pend_gelu = None, False
         i += 1
-    return x
-
-
-def _run_downsample(seq, x, dt=None):
-    """nn.Sequential of the reference's downsample layer (natively, or its BatchNorms on BNRowsFn)."""
-    if _NATIVE_STEM and x.is_cuda and dt is not None:
-        return _run_downsample_native(seq, x, dt)
-    if not _NATIVE_STEM_BN:
-        return seq(x)
-    for m in seq:
-        if isinstance(m, nn.modules.batchnorm._BatchNorm) and x.is_cuda:
-            x = BNRowsFn.apply(x, m.weight, m.bias, m, isinstance(m, nn.SyncBatchNorm))
-        else:
-            x = m(x)
     return x
 
 
@@ -419,13 +405,11 @@ class DFormer(nn.Module):
             b._row_scales = r if b.drop_prob > 0 else None
 
     def _downsample(self, i, x, e):
+        if not x.is_cuda:
+            raise RuntimeError("dformer_amd runs on the HIP library only (tensors must be on the GPU)")
         dt = self.compute_dtype
-        if _NATIVE_STEM and x.is_cuda:
-            return _run_downsample(self.downsample_layers[i], x, dt), _run_downsample(self.downsample_layers_e[i], e, dt)
-        with torch.autocast("cuda", dtype=dt, enabled=dt != torch.float32):
-            x = _run_downsample(self.downsample_layers[i], x)
-            e = _run_downsample(self.downsample_layers_e[i], e)
-        return x, e
+        return (_run_downsample_native(self.downsample_layers[i], x, dt),
+                _run_downsample_native(self.downsample_layers_e[i], e, dt))
 
     def forward(self, x, x_e):
         if x_e is None:
@@ -436,9 +420,6 @@ class DFormer(nn.Module):
             x_e = x_e.unsqueeze(2)
         x_e = x_e[:, 0:1]
         dt = self.compute_dtype
-        if not (_NATIVE_STEM and x.is_cuda):  # the native stem gathers straight from the input tensors
-            x = x.to(dt).contiguous(memory_format=torch.channels_last)
-            x_e = x_e.to(dt).contiguous(memory_format=torch.channels_last)
         self._draw_drop_path(x.shape[0], x.device)
         outs = []
         for i in range(4):

@@ -354,6 +354,13 @@ _ATTN_SIDE = {}
 # the q|q_cut|l gradients, so it is issued on a side stream (DFM_ATTN_BWD_STREAM=0: one stream).
 # Measured on MI355X, DFormer-B bf16 bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s.
 _ATTN_BWD_SIDE_ON = os.environ.get("DFM_ATTN_BWD_STREAM", "1") == "1"
+_ATTN_BWD_SIDE_FROM = int(os.environ.get("DFM_ATTN_BWD_SIDE_FROM", "0"))  # first stage that uses it
+
+
+def _stage_no(tag):
+    """Stage index of a component tag such as 's2.attn' (9 when unknown: side streams stay on)."""
+    t = (tag or "").split(".")[0]
+    return int(t[1:]) if t[:1] == "s" and t[1:].isdigit() else 9
 _ATTN_BWD_SIDE = {}
 # DFM_ATTN_BWD_STREAM2=1 (with the above): the pooled-attention part of the RGB branch (bilinear,
 # attention, short_cut_linear and kv gradients) on a second side stream, overlapping the
@@ -518,7 +525,7 @@ class AttentionFn(torch.autograd.Function):
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
-        side = _attn_bwd_side(dev) if x.is_cuda else None
+        side = _attn_bwd_side(dev) if x.is_cuda and _stage_no(ctx.tag) >= _ATTN_BWD_SIDE_FROM else None
         main = torch.cuda.current_stream(dev) if side is not None else None
 
         def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))

@@ -69,3 +69,16 @@ def test_metrics_formulas_match_reference():
     assert len(f1) == 3 and f1[2] == 0.0
     acc, macc = m.compute_pixel_acc()
     assert abs(acc[0] - 83.33) < 1e-3 and abs(macc - round((5 / 6 + 0.7) / 3 * 100, 2)) < 1e-3
+
+
+def test_warmup_poly_lr():
+    """WarmUpPolyLR (utils/lr_policy.py:22-34): linear warm-up to start_lr, then poly decay."""
+    from dformer_amd.train import WarmUpPolyLR
+    s = WarmUpPolyLR(6e-5, 0.9, 1000, 10)
+    assert s.get_lr(0) == 0.0
+    assert abs(s.get_lr(5) - 3e-5) < 1e-18
+    assert abs(s.get_lr(10) - 6e-5 * (1 - 10 / 1000.0) ** 0.9) < 1e-18
+    assert abs(s.get_lr(500) - 6e-5 * 0.5 ** 0.9) < 1e-18
+    lrs = [s.get_lr(i) for i in range(10, 1000)]
+    assert all(a > b for a, b in zip(lrs, lrs[1:])) and lrs[-1] > 0.0
+    assert s.get_lr(1000) == 0.0

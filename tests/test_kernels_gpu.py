@@ -389,6 +389,11 @@ def test_bilinear_strided(dt, hi, ho, C):
 @pytest.mark.parametrize("B,heads,N,dh",[(2, 2, 300, 32), (1, 4, 1200, 32), (2, 1, 37, 16), (1, 2, 150, 48),
                                          (2, 4, 99, 36), (2, 4, 1564, 36), (2, 8, 391, 36)])
 def test_pooled_attention(dt, B, heads, N, dh):
+    """MFMA pooled attention (bf16 / fp16; fp32 on the scalar kernels) vs torch fp32 on the same rounded
+    inputs. The kernel's own error sources are P and dS rounded to the 16-bit MFMA operand type and the
+    16-bit outputs (bf16: 2^-9 relative, i.e. ~1.1e-3 in norm from the output rounding alone), so the
+    gates sit a few roundings above that instead of at the generic elementwise tolerance."""
+    tol = {torch.float32: 2e-5, torch.bfloat16: 6e-3, torch.float16: 1.5e-3}[dt]
     k = K()
     C2 = heads * dh
     q = torch.randn(B * 49, C2, device=DEV).to(dt)
@@ -399,15 +404,15 @@ def test_pooled_attention(dt, B, heads, N, dh):
     kr = kv.float()[:, :C2].reshape(B, N, heads, dh).permute(0, 2, 1, 3).contiguous().requires_grad_()
     vr = kv.float()[:, C2:].reshape(B, N, heads, dh).permute(0, 2, 1, 3).contiguous().requires_grad_()
     ref = ((qr * scale) @ kr.transpose(-2, -1)).softmax(-1) @ vr
-    assert rel(o.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), ref) < TOL[dt]
+    assert rel(o.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), ref) < tol
     do = torch.randn(B * 49, C2, device=DEV).to(dt)
     ref.backward(do.float().view(B, 49, heads, dh).permute(0, 2, 1, 3))
     dq = torch.empty_like(q)
     dkv = torch.empty_like(kv)
     k.pooled_attn_bwd(q, kv[:, :C2], kv[:, C2:], o, do, lse, B, heads, N, dh, scale, dq, dkv[:, :C2], dkv[:, C2:])
-    assert rel(dq.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), qr.grad) < TOL[dt] * 2
-    assert rel(dkv[:, :C2].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), kr.grad) < TOL[dt] * 2
-    assert rel(dkv[:, C2:].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), vr.grad) < TOL[dt] * 2
+    assert rel(dq.float().view(B, 49, heads, dh).permute(0, 2, 1, 3), qr.grad) < tol * 2
+    assert rel(dkv[:, :C2].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), kr.grad) < tol * 2
+    assert rel(dkv[:, C2:].float().reshape(B, N, heads, dh).permute(0, 2, 1, 3), vr.grad) < tol * 2
 
 
 @pytest.mark.parametrize("dt", DTYPES)
