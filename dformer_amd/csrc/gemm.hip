@@ -1235,7 +1235,11 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
              al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
   const bool ak = d->a_kcontig, bk = d->b_kcontig;
-  const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
+  static const int sk64_env = [] {  // DFM_GEMM_SK64=1: K <= 128 shapes on 64-deep k-slices (A/B timing)
+    const char* e = getenv("DFM_GEMM_SK64");
+    return e ? atoi(e) : 0;
+  }();
+  const bool small_k = (sizeof(T) == 2 ? d->K <= 128 : d->K <= 64) && !(sk64_env && sizeof(T) == 2 && d->K % 64 == 0);
   static const int stream_env = [] {  // DFM_GEMM_STREAM=0 disables the streaming kernel (A/B timing)
     const char* e = getenv("DFM_GEMM_STREAM");
     return e ? atoi(e) : 1;
@@ -1245,7 +1249,9 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
     // DFM_GEMM_STREAM=2 also streams 128-wide column tiles (large-M short-K forward GEMMs with
     // 64 < N, e.g. fc1 / q|q_cut|l at stage 0)
-    a.stream = stream_env != 0 && sizeof(T) == 2 && (BN <= 64 || (stream_env >= 2 && BN == 128)) && ak &&
+    // DFM_GEMM_STREAM=3: 128-wide column tiles stream only on the stage-0 scale shapes (>= 4096 tiles)
+    const bool wide = BN == 128 && (stream_env == 2 || (stream_env == 3 && tiles >= 4096));
+    a.stream = stream_env != 0 && sizeof(T) == 2 && (BN <= 64 || wide) && ak &&
                a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb && d->K % BKsel == 0 &&
                d->K / BKsel <= 8 && tiles >= 1024;
   }
@@ -1393,7 +1399,9 @@ int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* 
     g.p[q].xcd_map = 1;
     g.p[q].tiles_m = cdiv(d[q].M, BM);
     g.p[q].tiles_n = cdiv(g.p[q].Nw, BN);
-    g.p[q].n_fast = 0;
+    // forward / input-gradient problems (k-contiguous A, tall): the column tiles of one row tile run
+    // back to back so the A row block is re-read from L2 (as launch_cfg); weight gradients keep row order
+    g.p[q].n_fast = AK && g.p[q].tiles_n > 1 && d[q].M >= g.p[q].Nw;
     const int nblk = g.p[q].tiles_m * g.p[q].tiles_n * g.p[q].batch * splits[q];
     g.start[q + 1] = g.start[q] + (nblk + 7) / 8 * 8;
     r.p[q] = g.p[q];

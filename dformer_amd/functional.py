@@ -422,26 +422,36 @@ class AttentionFn(torch.autograd.Function):
             xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
         # q | q_cut | l in one GEMM; GELU only on the l columns, whose derivative (act 3) is stored
-        # for the backward
+        # for the backward. Without the side stream, e_fore joins it in one grouped launch.
         Wqcl = wcast(dt, wq, wqc, wl)
         bqcl = _cat1(bq, bqc, bl)
         qcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         lpre = torch.empty(P, C, device=dev, dtype=dt)
-        K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl)
+        with K.gemm_group():
+            K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl, defer=True)
+            if side is None:
+                e1 = K.linear(xen, wcast(dt, wef), bef, defer=True)
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         xep = torch.empty(P, Ch, device=dev, dtype=dt)
         if side is not None:  # depth branch, part 2: e_back * cx (needs the q|q_cut|l GEMM)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
-        # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward)
+        # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward); with kv = Linear(g) and (no
+        # side stream) e_back(DW7(e_fore)) * cx as one grouped launch
         apre = K.dwconv(g, shape, wconv, bconv, 7)
+        if side is None:
+            e2 = K.dwconv(e1, shape, wec, bec, 7)
         a = torch.empty(P, C, device=dev, dtype=dt)
-        K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C])
+        with K.gemm_group():
+            K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C], defer=True)
+            if window:
+                kv = K.linear(g, wcast(dt, wkv), bkv, defer=True)
+            if side is None:
+                K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:], defer=True)
         saved_attn = ()
         if window:
             dh = C // heads // 2
-            kv = K.linear(g, wcast(dt, wkv), bkv)
             pooled = torch.empty(B * 49, C + Ch, device=dev, dtype=dt)
             K.pool7(xn, shape, out=pooled[:, :C])
             if side is not None:
@@ -451,12 +461,8 @@ class AttentionFn(torch.autograd.Function):
             o, lse = K.pooled_attn(m, kv[:, :Ch], kv[:, Ch:], B, heads, P // B, dh, dh ** -0.5)
             K.bilinear(o, (7, 7), (H, W), B, out=f[:, C:C + Ch])
             saved_attn = (kv, pooled, m, o, lse)
-        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
-        if side is None:
-            e1 = K.linear(xen, wcast(dt, wef), bef)
-            e2 = K.dwconv(e1, shape, wec, bec, 7)
-            K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
-        else:  # join; tensors that crossed streams stay alive until both are done with them
+        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe' (grouped above)
+        if side is not None:  # join; tensors that crossed streams stay alive until both are done with them
             main.wait_stream(side)
             for t in (xen, mu2, rs2, e1, e2):
                 t.record_stream(main)
@@ -464,13 +470,15 @@ class AttentionFn(torch.autograd.Function):
                 t.record_stream(side)
         # projections with the Block's residual / layer-scale / DropPath epilogue
         p1 = torch.empty(P, C, device=dev, dtype=dt)
-        x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
-        if drop_depth:
-            xe1, p1e = xe, None
-        else:
-            p1e = torch.empty(P, Ch, device=dev, dtype=dt)
-            xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
-                           rows_per_scale=rps)
+        with K.gemm_group():  # proj and proj_e (each with its own residual epilogue) in one launch
+            x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale,
+                          rows_per_scale=rps, defer=True)
+            if drop_depth:
+                xe1, p1e = xe, None
+            else:
+                p1e = torch.empty(P, Ch, device=dev, dtype=dt)
+                xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
+                               rows_per_scale=rps, defer=True)
         ctx.shape, ctx.heads, ctx.window, ctx.drop_depth = shape, heads, window, drop_depth
         ctx.n_attn = len(saved_attn)
         ctx.save_for_backward(x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1,

@@ -122,6 +122,21 @@ class wgrad_group:
         return False
 
 
+# Independent forward GEMMs of a Block issued as one grouped launch (kernels.linear(..., defer=True)
+# inside `with gemm_group():`); DFM_FWD_GROUP=0: separate launches (A/B timing).
+# Measured on MI355X: 403.6 vs 415.4 images/s — the grouped launch runs the register-staged 128x128
+# kernel, which loses more on these shapes than the saved launches give back, so it stays off.
+FWD_GROUP = os.environ.get("DFM_FWD_GROUP", "0") == "1"
+
+
+class gemm_group(wgrad_group):
+    def __enter__(self):
+        global _WG_PENDING
+        self.prev = _WG_PENDING
+        _WG_PENDING = [] if FWD_GROUP else None
+        return self
+
+
 def flush_wgrad(pending):
     """Issue queued GEMMs as grouped launches: problems of one dtype / operand layout, 8 per launch."""
     classes = {}
@@ -179,8 +194,9 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
 
 
 def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=None, rowscale=None,
-           rows_per_scale=1, out=None, beta=0.0, act_col0=0):
-    """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward)."""
+           rows_per_scale=1, out=None, beta=0.0, act_col0=0, defer=False):
+    """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward). defer=True inside a gemm_group block:
+    queued and issued with the block's other GEMMs as one grouped launch at its end."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -188,7 +204,8 @@ def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=
     return gemm(x, w, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=ld(x), ldb=ld(w), out=out, ldc=ld(out),
                 beta=beta, bias=bias, act=act, preact=preact, ldpre=ld(preact) if preact is not None else 0,
                 mul=mul, ldmul=ld(mul) if mul is not None else 0, res=res, ldres=ld(res) if res is not None else 0,
-                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0)
+                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0,
+                defer=defer)
 
 
 def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None):
