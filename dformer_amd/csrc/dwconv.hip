@@ -17,6 +17,25 @@
 namespace {
 template <typename T> struct DwCfg { static constexpr int CPT = 16 / sizeof(T); };
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// one 16-byte vector -> CPT/2 channel pairs (packed-FMA operands; bf16 / f16 widen exactly)
+template <typename T>
+DFM_INLINE void unpack_pairs(uint4 q, f2v* v) {
+  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+  if constexpr (std::is_same<T, bf16_t>::value) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = f2v{__uint_as_float(u[k] << 16), __uint_as_float(u[k] & 0xffff0000u)};
+  } else if constexpr (std::is_same<T, f16_t>::value) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = f2v{h2f((uint16_t)(u[k] & 0xffffu)), h2f((uint16_t)(u[k] >> 16))};
+  } else {
+    v[0] = f2v{__uint_as_float(u[0]), __uint_as_float(u[1])};
+    v[1] = f2v{__uint_as_float(u[2]), __uint_as_float(u[3])};
+  }
+}
+
+
 template <typename T>
 DFM_INLINE void ldv(const T* p, float* v) {
   if constexpr (sizeof(T) == 2) {
@@ -113,44 +132,45 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
   const int c0 = cbase + g * CPT;
   const int oh = h0 + row, ow0 = w0 + strip * TWS;
   if (c0 >= C || oh >= H || ow0 >= W) return;
-  float acc[TWS][CPT];
+  // channel pairs on packed FMA (v_pk_fma_f32): the same per-element FMA sequence, half the instructions
+  constexpr int CP = CPT / 2;
+  f2v accp[TWS][CP];
 #pragma unroll
-  for (int e = 0; e < CPT; ++e) {
-    const float bv = bias ? bias[c0 + e] : 0.f;
+  for (int e = 0; e < CP; ++e) {
+    const f2v bv = bias ? f2v{bias[c0 + 2 * e], bias[c0 + 2 * e + 1]} : f2v{0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < TWS; ++t) acc[t][e] = bv;
+    for (int t = 0; t < TWS; ++t) accp[t][e] = bv;
   }
 #pragma unroll 1
   for (int i = 0; i < K; ++i) {
-    float win[TWS + K - 1][CPT];
+    f2v win[TWS + K - 1][CP];
     const uint4* xr = xs + ((row + i) * IW + strip * TWS) * NG + g;
 #pragma unroll
-    for (int u = 0; u < TWS + K - 1; ++u) {
-      const uint4 q = xr[u * NG];
-      if constexpr (sizeof(T) == 2) {
-        Raw8<T> r8;
-        r8.w[0] = q;
-        unpack8(r8, win[u]);
-      } else {
-        win[u][0] = __uint_as_float(q.x); win[u][1] = __uint_as_float(q.y);
-        win[u][2] = __uint_as_float(q.z); win[u][3] = __uint_as_float(q.w);
-      }
-    }
+    for (int u = 0; u < TWS + K - 1; ++u) unpack_pairs<T>(xr[u * NG], win[u]);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      float wv[CPT];
+      f2v wv[CP];
       const float4* wp = reinterpret_cast<const float4*>(wl + (i * K + j) * CW + g * CPT);
 #pragma unroll
       for (int q4 = 0; q4 < CPT / 4; ++q4) {
         const float4 f = wp[q4];
-        wv[4 * q4] = f.x; wv[4 * q4 + 1] = f.y; wv[4 * q4 + 2] = f.z; wv[4 * q4 + 3] = f.w;
+        wv[2 * q4] = f2v{f.x, f.y};
+        wv[2 * q4 + 1] = f2v{f.z, f.w};
       }
 #pragma unroll
       for (int t = 0; t < TWS; ++t)
 #pragma unroll
-        for (int e = 0; e < CPT; ++e) acc[t][e] = fmaf(wv[e], win[t + j][e], acc[t][e]);
+        for (int e = 0; e < CP; ++e) accp[t][e] = __builtin_elementwise_fma(wv[e], win[t + j][e], accp[t][e]);
     }
   }
+  float acc[TWS][CPT];
+#pragma unroll
+  for (int t = 0; t < TWS; ++t)
+#pragma unroll
+    for (int e = 0; e < CP; ++e) {
+      acc[t][2 * e] = accp[t][e].x;
+      acc[t][2 * e + 1] = accp[t][e].y;
+    }
 #pragma unroll
   for (int t = 0; t < TWS; ++t) {
     const int ow = ow0 + t;
@@ -401,6 +421,19 @@ DFM_INLINE void w3_unpack(uint2 q, float* v) {
     v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
   } else {
     v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
+  }
+}
+
+template <typename T>
+DFM_INLINE void w3_pairs(uint2 q, f2v* v) {
+  if constexpr (std::is_same<T, f16_t>::value) {
+    v[0] = f2v{h2f((uint16_t)(q.x & 0xffffu)), h2f((uint16_t)(q.x >> 16))};
+    v[1] = f2v{h2f((uint16_t)(q.y & 0xffffu)), h2f((uint16_t)(q.y >> 16))};
+  } else if constexpr (sizeof(T) == 2) {
+    v[0] = f2v{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u)};
+    v[1] = f2v{__uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
+  } else {
+    v[0] = f2v{__uint_as_float(q.x), __uint_as_float(q.y)};
   }
 }
 
@@ -663,24 +696,6 @@ constexpr int W7L_NG = 4, W7L_TH = 16, W7L_TW = 14, W7L_NP = 8;   // TW: a multi
 constexpr int W7L_IH = W7L_TH + 6, W7L_IW = W7L_TW + 7;  // +7: pitch 21 -> NG * pitch = 84 = 4 (mod 8)
 static_assert((W7L_NG * W7L_IW) % 8 == 4, "LDS pitch");
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// one 16-byte vector -> CPT/2 channel pairs (packed-FMA operands; bf16 / f16 widen exactly)
-template <typename T>
-DFM_INLINE void unpack_pairs(uint4 q, f2v* v) {
-  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
-  if constexpr (std::is_same<T, bf16_t>::value) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = f2v{__uint_as_float(u[k] << 16), __uint_as_float(u[k] & 0xffff0000u)};
-  } else if constexpr (std::is_same<T, f16_t>::value) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = f2v{h2f((uint16_t)(u[k] & 0xffffu)), h2f((uint16_t)(u[k] >> 16))};
-  } else {
-    v[0] = f2v{__uint_as_float(u[0]), __uint_as_float(u[1])};
-    v[1] = f2v{__uint_as_float(u[2]), __uint_as_float(u[3])};
-  }
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
                                                             const T* __restrict__ x, long ldx,
@@ -900,19 +915,20 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
                                                              const float* __restrict__ bias, int add_identity,
                                                              T* __restrict__ y, long ldy, int accumulate,
                                                              T* __restrict__ gout, long ldg) {
-  constexpr int CPT = W3Cfg<T>::EPL, TW = W3_TW, NX = TW + 2;
+  constexpr int CPT = W3Cfg<T>::EPL, CP = CPT / 2, TW = W3_TW, NX = TW + 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lg = lane % LPU, usub = lane / LPU;
   const int G = C / CPT, cg = blockIdx.y * LPU + lg;
   if (usub >= UPW || cg >= G) return;
   const int c0 = cg * CPT;
   const long units = w3_units(B, nstrips, nchunks);
-  float wv[9][CPT], bv[CPT];
+  f2v wv[9][CP], bv[CP];  // channel pairs (packed FMA)
 #pragma unroll
-  for (int e = 0; e < CPT; ++e) {
+  for (int e = 0; e < CP; ++e) {
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) wv[tap][e] = w[(long)(c0 + e) * 9 + (FLIP ? 8 - tap : tap)];
-    bv[e] = bias ? bias[c0 + e] : 0.f;
+    for (int tap = 0; tap < 9; ++tap)
+      wv[tap][e] = f2v{w[(long)(c0 + 2 * e) * 9 + (FLIP ? 8 - tap : tap)], w[(long)(c0 + 2 * e + 1) * 9 + (FLIP ? 8 - tap : tap)]};
+    bv[e] = bias ? f2v{bias[c0 + 2 * e], bias[c0 + 2 * e + 1]} : f2v{0.f, 0.f};
   }
   const long stride = (long)gridDim.x * 4 * UPW;
   for (long u = ((long)blockIdx.x * 4 + wave) * UPW + usub; u < units; u += stride) {
@@ -935,33 +951,41 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
     for (int h = h0; h < h1; ++h) {
       uint2 xn[NX];
       load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
-      float acc[TW][CPT];
+      f2v accp[TW][CP];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
 #pragma unroll
-        for (int e = 0; e < CPT; ++e) acc[t][e] = bv[e];
+        for (int e = 0; e < CP; ++e) accp[t][e] = bv[e];
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         const uint2* xr = a == 0 ? x0 : (a == 1 ? x1 : x2);
 #pragma unroll
         for (int q = 0; q < NX; ++q) {
-          float xv[CPT];
-          w3_unpack<T>(xr[q], xv);
+          f2v xv[CP];
+          w3_pairs<T>(xr[q], xv);
 #pragma unroll
           for (int t = 0; t < TW; ++t) {
             const int j = q - t;
             if (j < 0 || j >= 3) continue;
 #pragma unroll
-            for (int e = 0; e < CPT; ++e) acc[t][e] = fmaf(wv[a * 3 + j][e], xv[e], acc[t][e]);
+            for (int e = 0; e < CP; ++e) accp[t][e] = __builtin_elementwise_fma(wv[a * 3 + j][e], xv[e], accp[t][e]);
           }
           if (q >= 1 && q <= TW && (add_identity & 1)) {
             if (a == 1) {
 #pragma unroll
-              for (int e = 0; e < CPT; ++e) acc[q - 1][e] += xv[e];
+              for (int e = 0; e < CP; ++e) accp[q - 1][e] += xv[e];
             }
           }
         }
       }
+      float acc[TW][CPT];
+#pragma unroll
+      for (int t = 0; t < TW; ++t)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) {
+          acc[t][2 * e] = accp[t][e].x;
+          acc[t][2 * e + 1] = accp[t][e].y;
+        }
 #pragma unroll
       for (int t = 0; t < TW; ++t) {
         const int ww = w0 + t;
@@ -1019,19 +1043,6 @@ int f3_launch(int B, int H, int W, int C, const void* x, long ldx, const float* 
 // weight gradient) keeps the three dy rows and the three x rows around output row h in registers,
 // loading the next row of each one ahead. dy is read once from HBM (its halo rows / columns from
 // L2), x once, dx written once. All FMAs are packed (v_pk_fma_f32 over channel pairs).
-template <typename T>
-DFM_INLINE void w3_pairs(uint2 q, f2v* v) {
-  if constexpr (std::is_same<T, f16_t>::value) {
-    v[0] = f2v{h2f((uint16_t)(q.x & 0xffffu)), h2f((uint16_t)(q.x >> 16))};
-    v[1] = f2v{h2f((uint16_t)(q.y & 0xffffu)), h2f((uint16_t)(q.y >> 16))};
-  } else if constexpr (sizeof(T) == 2) {
-    v[0] = f2v{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u)};
-    v[1] = f2v{__uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
-  } else {
-    v[0] = f2v{__uint_as_float(q.x), __uint_as_float(q.y)};
-  }
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void dw3_stream_bwd_kernel(int B, int H, int W, int C, int RC, int nstrips,
                                                              int nchunks, int LPU, int UPW,
