@@ -659,8 +659,11 @@ DFM_INLINE int group_problem(const GemmGroup& g, int b) {
   return q;
 }
 
+// Four waves per SIMD = two blocks per CU (at most 128 VGPRs; the second launch bound is waves per EU):
+// the weight-gradient k-loops are latency-bound with one 8-wave
+// block per CU, and a second resident block doubles the operand bytes in flight.
 template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC, int DEPTH>
-__global__ __launch_bounds__(64 * NW) void gemm_group_kernel(GemmGroup g) {
+__global__ __launch_bounds__(64 * NW, 4) void gemm_group_kernel(GemmGroup g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.x;
   const int q = group_problem(g, b);
@@ -1312,12 +1315,12 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 
 // ---- grouped launch (host)
 // The group's split-K choice: every problem gets split-K slices in proportion to its share of the
-// group's work (tiles x K), so the ~512 blocks of the launch (two per CU) each reduce about the
-// same K range (at least 512 elements); d->split_k >= 1 forces a problem's count.
+// group's work (tiles x K), so the ~1024 blocks of the launch (two resident per CU, two rounds) each
+// reduce about the same K range (at least 512 elements); d->split_k >= 1 forces a problem's count.
 void group_splits(int n, const DfmGemmDesc* d, int* splits) {
   static const double target = [] {  // DFM_WG_BLOCKS: the grouped launch's block target (A/B timing)
     const char* e = getenv("DFM_WG_BLOCKS");
-    return e ? std::max(64.0, atof(e)) : 512.0;
+    return e ? std::max(64.0, atof(e)) : 1024.0;
   }();
   double work = 0;
   for (int q = 0; q < n; ++q) {
