@@ -1273,9 +1273,19 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
     const int kper = (d->K + a.splits - 1) / a.splits;
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 640);
+    // DFM_GLDS_SMALL=n: 64x64 tiles when 64x128 tiles would give fewer than n blocks. Default: always
+    // (measured on the DFormer-B step: 418.1-418.5 images/s with 64x128, 419.4-420.4 below 2048 / 4096
+    // blocks, 421.5 everywhere — the stage-1..3 forward GEMMs are latency-bound and gain from the
+    // doubled block count more than they lose in B-tile reuse)
+    static const int glds_small = [] {
+      const char* e = getenv("DFM_GLDS_SMALL");
+      return e ? atoi(e) : 1 << 30;
+    }();
     if (glds_env && route && !a.stream && a.ala && a.alb && kper >= 2 * GBK) {
       if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
       if (BN == 64) return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
+      // latency-bound shapes (stage 2/3: few row tiles) get twice the blocks from 64-wide column tiles
+      if ((long)cdiv(d->M, 64) * cdiv(a.Nw, 128) * a.batch * a.splits < glds_small) return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
       return glds_ak<64, 128, 4, 2, 2, 3>(a, bk, s);
     }
     // weight gradients (both operands row-contiguous, K = pixels): a deep LDS-DMA ring keeps 96-128 KB

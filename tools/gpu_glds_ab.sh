@@ -1,0 +1,8 @@
+# A/B of the 64x64 LDS-DMA tiles for few-block forward GEMMs (DFM_GLDS_SMALL), with a GEMM test pass
+set -o pipefail
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
+T=${1:-glds}
+DFM_GLDS_SMALL=100000 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_block_gpu.py -x -q -m gpu -k "gemm or linear or block" --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/${T}_k.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -1 gpurun_out/${T}_k.log
+[ $rc -le 1 ] || exit 11
+bash tools/ab_switches.sh ${T} "DFM_GLDS_SMALL=0" "DFM_GLDS_SMALL=512" "DFM_GLDS_SMALL=1024" "DFM_GLDS_SMALL=2048" "DFM_GLDS_SMALL=0" || exit 14
