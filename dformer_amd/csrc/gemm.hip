@@ -1272,7 +1272,14 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   }();
   if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
     const int kper = (d->K + a.splits - 1) / a.splits;
-    const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 640);
+    // DFM_GLDS_DGRAD_K: shortest K of an input gradient on the LDS-DMA ring. With 64x64 tiles the ring
+    // wins from K = 128 up (DFormer-B step, one box: 415.4-416.0 images/s at 640, 416.7-417.9 at 256,
+    // 418.5-419.4 at 128)
+    static const int dgrad_k = [] {
+      const char* e = getenv("DFM_GLDS_DGRAD_K");
+      return e ? atoi(e) : 128;
+    }();
+    const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= dgrad_k);
     // DFM_GLDS_SMALL=n: 64x64 tiles when 64x128 tiles would give fewer than n blocks. Default: always
     // (measured on the DFormer-B step: 418.1-418.5 images/s with 64x128, 419.4-420.4 below 2048 / 4096
     // blocks, 421.5 everywhere — the stage-1..3 forward GEMMs are latency-bound and gain from the
