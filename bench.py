@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
-                    help="compute dtype; fp16 = the reference's --amp (loss scaling, eager launches)")
+                    help="compute dtype; fp16 = the reference's --amp (dynamic loss scaling decided on the device, graph replay)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-census", action="store_true")

@@ -29,7 +29,8 @@ class GemmDesc(ctypes.Structure):
                 ("bias", P), ("act", c_int), ("preact", P), ("ldpre", c_long),
                 ("mul", P), ("ldmul", c_long), ("res", P), ("ldres", c_long),
                 ("colscale", P), ("rowscale", P), ("rows_per_scale", c_long), ("split_k", c_int),
-                ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int), ("mul_gelu_grad", c_int)]
+                ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int), ("mul_gelu_grad", c_int),
+                ("workspace_bytes", ctypes.c_long)]
 
 
 # name -> (restype, argtypes)
@@ -106,12 +107,6 @@ _SIGS = {
     "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),
     "dfm_adamw_amp": (c_int, [c_long, P, P, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),
     "dfm_loss_scale_update": (c_int, [P, P, c_float, c_float, c_int, P]),
-    "dfm_convffn_supported": (c_int, [c_int, c_int, c_int]),
-    "dfm_convffn_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P, P,
-                                P, P, c_long, P, c_long, P]),
-    "dfm_convffn_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
-    "dfm_convffn_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P, P, P,
-                                c_long, P, c_long, P, c_long, P, P, P, P]),
     "dfm_trace_set": (c_int, [c_int, ctypes.c_char_p]),
     "dfm_trace_take": (c_int, [ctypes.POINTER(c_void_p), c_int]),
     "dfm_trace_read": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_float), c_int]),

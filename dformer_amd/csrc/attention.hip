@@ -127,15 +127,6 @@ __global__ void bilinear_bwd_kernel(int B, int Hi, int Wi, int Ho, int Wo, int C
 
 // ------------------------------------------------------------------ 8-channel vector forms
 // (C % 8 == 0, 16-byte aligned rows). Each lane moves 8 channels per 16-byte access.
-// DFM_SCALAR_RESIZE bitmask (A/B checks): 1 bilinear fwd, 2 bilinear bwd, 4 pool fwd, 8 pool bwd
-// take the scalar kernels
-inline int scalar_resize_mask() {
-  static const int m = [] {
-    const char* e = getenv("DFM_SCALAR_RESIZE");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
 inline bool vec_ok(int C, const void* p, long ld) { return C % 8 == 0 && ld % 8 == 0 && (uintptr_t)p % 16 == 0; }
 
 // pool: one block per (image, cell); CV = C/8 lanes per pixel, 256/CV pixels of the bin in
@@ -875,7 +866,7 @@ int dispatch(int dtype, F16 f16, F32 f32) {
 extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, const void* x, long ldx, void* y,
                                       long ldy, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (!(scalar_resize_mask() & 4) && C <= 2048 && vec_ok(C, x, ldx)) {
+  if (C <= 2048 && vec_ok(C, x, ldx)) {
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,
@@ -912,7 +903,7 @@ extern "C" int dfm_adaptive_pool7_fwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, const void* dy, long lddy, void* dx,
                                       long lddx, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (!(scalar_resize_mask() & 8) && vec_ok(C, dy, lddy) && vec_ok(C, dx, lddx)) {
+  if (vec_ok(C, dy, lddy) && vec_ok(C, dx, lddx)) {
     const unsigned gv = grid_for((long)B * H * W * (C / 8));
     return dispatch(
         dtype,
@@ -949,7 +940,7 @@ extern "C" int dfm_adaptive_pool7_bwd(int dtype, int B, int H, int W, int C, con
 extern "C" int dfm_bilinear_fwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo, int C, const void* x, long ldx,
                                 void* y, long ldy, int accumulate, dfm_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (!(scalar_resize_mask() & 1) && vec_ok(C, x, ldx) && vec_ok(C, y, ldy)) {
+  if (vec_ok(C, x, ldx) && vec_ok(C, y, ldy)) {
     const unsigned gv = grid_for((long)B * Ho * Wo * (C / 8));
     return dispatch(
         dtype,
@@ -988,7 +979,7 @@ extern "C" int dfm_bilinear_bwd(int dtype, int B, int Hi, int Wi, int Ho, int Wo
   hipStream_t s = (hipStream_t)stream;
   // taps per axis: ~2 * out/in + 3 must fit the block's LDS lists
   const bool taps_fit = 2 * (Ho / Hi) + 6 <= BL_MAXT && 2 * (Wo / Wi) + 6 <= BL_MAXT && Ho >= Hi && Wo >= Wi;
-  if (!(scalar_resize_mask() & 2) && C <= 2048 && taps_fit && vec_ok(C, dy, lddy) && (uintptr_t)dx % 4 == 0) {
+  if (C <= 2048 && taps_fit && vec_ok(C, dy, lddy) && (uintptr_t)dx % 4 == 0) {
     const size_t lds = (size_t)(256 / (C / 8)) * C * sizeof(float);
     return dispatch(
         dtype,

@@ -214,152 +214,6 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
   }
 }
 
-// ---------------------------------------------------------------- LDS-tiled weight gradient (v3)
-// Block (spatial lane bx, channel block by, kernel-row group bz) walks tiles bx, bx+gridDim.x, ...
-// For each tile the dy tile [TH][TWT][NG] and the TH+KI-1 input rows its KI kernel rows touch
-// ([TH+KI-1][TWT+K-1][NG], zero-padded) are staged in LDS; every thread accumulates KI x K taps
-// x CPT channels over its TWS pixels with a sliding window. At the end the taps are reduced over
-// the threads of one channel group (wave shuffles, then LDS across waves) and written as the
-// block's partial [bx][C][K*K+1] (last column: bias gradient, from bz == 0); a fixed-order
-// second pass sums the partials (deterministic).
-template <typename T, int K>
-struct DwWTile;
-template <typename T> struct DwWTile<T, 3> { static constexpr int KI = 3; };
-template <typename T> struct DwWTile<T, 7> { static constexpr int KI = 1; };
-
-template <typename T, int K, int NG>
-__global__ __launch_bounds__(256) void dw_tile_wgrad_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
-                                                            const T* __restrict__ x, long ldx,
-                                                            const T* __restrict__ dy, long lddy,
-                                                            float* __restrict__ part) {
-  constexpr int CPT = DwCfg<T>::CPT, R = K / 2, KI = DwWTile<T, K>::KI, KK1 = K * K + 1;
-  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
-  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS;
-  constexpr int IH = TH + KI - 1, IW = TWT + K - 1, CW = NG * CPT;
-  constexpr int NTAP = KI * K;
-  extern __shared__ __attribute__((aligned(16))) char dsm[];
-  uint4* xs = reinterpret_cast<uint4*>(dsm);  // [IH][IW][NG]
-  uint4* ds = xs + IH * IW * NG;              // [TH][TWT][NG]
-  float* red = reinterpret_cast<float*>(dsm);  // reused after the tile loop: [4 waves][NTAP+1][CW]
-
-  const int cbase = blockIdx.y * CW;
-  const int i0 = blockIdx.z * KI;
-  const int g = threadIdx.x % NG, strip = (threadIdx.x / NG) % STRIPS, row = threadIdx.x / (NG * STRIPS);
-  const int c0 = cbase + g * CPT;
-  const long ntiles = (long)B * tiles_h * tiles_w;
-
-  float acc[KI][K][CPT];
-  float dbs[CPT];
-#pragma unroll
-  for (int e = 0; e < CPT; ++e) dbs[e] = 0.f;
-#pragma unroll
-  for (int a = 0; a < KI; ++a)
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-#pragma unroll
-      for (int e = 0; e < CPT; ++e) acc[a][j][e] = 0.f;
-
-  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int tw = tile % tiles_w, th = (tile / tiles_w) % tiles_h;
-    const long b = tile / ((long)tiles_w * tiles_h);
-    const int h0 = th * TH, w0 = tw * TWT;
-    const long img = b * H * W;
-    {
-      constexpr int NX = IH * IW * NG, NDY = TH * TWT * NG, NL = (NX + NDY + 255) / 256;
-      uint4 buf[NL];
-#pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        const int v = threadIdx.x + l * 256;
-        buf[l] = make_uint4(0, 0, 0, 0);
-        if (v < NX) {
-          const int gg = v % NG, col = (v / NG) % IW, r = v / (NG * IW);
-          const int hh = h0 + r + i0 - R, ww = w0 + col - R, c = cbase + gg * CPT;
-          if (hh >= 0 && hh < H && ww >= 0 && ww < W && c < C)
-            buf[l] = *reinterpret_cast<const uint4*>(x + (img + (long)hh * W + ww) * ldx + c);
-        } else if (v < NX + NDY) {
-          const int u = v - NX;
-          const int gg = u % NG, col = (u / NG) % TWT, r = u / (NG * TWT);
-          const int hh = h0 + r, ww = w0 + col, c = cbase + gg * CPT;
-          if (hh < H && ww < W && c < C)
-            buf[l] = *reinterpret_cast<const uint4*>(dy + (img + (long)hh * W + ww) * lddy + c);
-        }
-      }
-      __syncthreads();  // the previous tile's LDS reads are done
-#pragma unroll
-      for (int l = 0; l < NL; ++l)
-        if (threadIdx.x + l * 256 < NX + NDY) xs[threadIdx.x + l * 256] = buf[l];
-    }
-    __syncthreads();
-    float gv[TWS][CPT];
-#pragma unroll
-    for (int t = 0; t < TWS; ++t) {
-      const uint4 q = ds[(row * TWT + strip * TWS + t) * NG + g];
-      if constexpr (sizeof(T) == 2) {
-        Raw8<T> r8;
-        r8.w[0] = q;
-        unpack8(r8, gv[t]);
-      } else {
-        gv[t][0] = __uint_as_float(q.x); gv[t][1] = __uint_as_float(q.y);
-        gv[t][2] = __uint_as_float(q.z); gv[t][3] = __uint_as_float(q.w);
-      }
-    }
-    if (i0 == 0) {
-#pragma unroll
-      for (int t = 0; t < TWS; ++t)
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) dbs[e] += gv[t][e];
-    }
-#pragma unroll
-    for (int a = 0; a < KI; ++a) {
-      const uint4* xr = xs + ((row + a) * IW + strip * TWS) * NG + g;
-#pragma unroll
-      for (int u = 0; u < TWS + K - 1; ++u) {
-        const uint4 q = xr[u * NG];
-        float xv[CPT];
-        if constexpr (sizeof(T) == 2) {
-          Raw8<T> r8;
-          r8.w[0] = q;
-          unpack8(r8, xv);
-        } else {
-          xv[0] = __uint_as_float(q.x); xv[1] = __uint_as_float(q.y);
-          xv[2] = __uint_as_float(q.z); xv[3] = __uint_as_float(q.w);
-        }
-        // input column u feeds output t with tap j = u - t
-#pragma unroll
-        for (int t = 0; t < TWS; ++t) {
-          const int j = u - t;
-          if (j < 0 || j >= K) continue;
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) acc[a][j][e] = fmaf(gv[t][e], xv[e], acc[a][j][e]);
-        }
-      }
-    }
-  }
-  __syncthreads();  // LDS is reused for the reduction
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int tap = 0; tap <= NTAP; ++tap) {
-    if (tap == NTAP && i0 != 0) break;
-#pragma unroll
-    for (int e = 0; e < CPT; ++e) {
-      float v = tap < NTAP ? acc[tap / K][tap % K][e] : dbs[e];
-#pragma unroll
-      for (int o = NG; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-      if (lane < NG) red[(wave * (NTAP + 1) + tap) * CW + lane * CPT + e] = v;
-    }
-  }
-  __syncthreads();
-  const long pbase = (long)blockIdx.x * C * KK1;
-  for (int idx = threadIdx.x; idx < (NTAP + 1) * CW; idx += 256) {
-    const int tap = idx / CW, cl = idx % CW, c = cbase + cl;
-    if (c >= C || (tap == NTAP && i0 != 0)) continue;
-    const float v = red[(0 * (NTAP + 1) + tap) * CW + cl] + red[(1 * (NTAP + 1) + tap) * CW + cl] +
-                    red[(2 * (NTAP + 1) + tap) * CW + cl] + red[(3 * (NTAP + 1) + tap) * CW + cl];
-    const int col = tap < NTAP ? (i0 + tap / K) * K + tap % K : K * K;
-    part[pbase + (long)c * KK1 + col] = v;
-  }
-}
-
 // ---------------------------------------------------------------- row-streaming 3x3 weight gradient
 // The tiled kernel above reduces one LDS tile per block visit; on the small-spatial, wide-channel
 // stages (30x40 / 15x20 with 1024-2048 hidden channels) a block sees a single tile and the
@@ -555,130 +409,6 @@ long w3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* 
   return g.nsb;
 }
 
-// ---------------------------------------------------------------- row-streaming 7x7 weight gradient
-// Same lane/strip/chunk walk as the 3x3 kernel, but the 49 taps x 4 channels would not fit in
-// registers, so each block owns one kernel row i (7 taps + the bias from i == 0) and streams the
-// input row h+i-3 next to dy row h. The seven blocks of one spatial block are consecutive in the
-// XCD-remapped order, so they run together on one XCD and their x / dy re-reads hit its L2.
-template <typename T>
-W3Geom w7_geom(int B, int H, int W, int C) {
-  constexpr int CPT = W3Cfg<T>::EPL;
-  W3Geom g;
-  const int G = C / CPT;
-  g.LPU = std::min(64, G);
-  g.UPW = 64 / g.LPU;
-  g.slices = (G + g.LPU - 1) / g.LPU;
-  g.nstrips = (W + W3_TW - 1) / W3_TW;
-  const long target_waves = 4096 / 7;  // per kernel row: ~16 waves per CU over the 7 rows
-  long want = (target_waves * g.UPW + (long)B * g.nstrips * g.slices - 1) / ((long)B * g.nstrips * g.slices);
-  want = std::max(1L, std::min(want, (long)(H + 3) / 4));
-  g.RC = (int)((H + want - 1) / want);
-  g.nchunks = (H + g.RC - 1) / g.RC;
-  g.units = w3_units(B, g.nstrips, g.nchunks);
-  const long waves = (g.units + g.UPW - 1) / g.UPW;
-  g.nsb = std::max(1L, (waves + 3) / 4);
-  return g;
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void dw7_stream_wgrad_kernel(int B, int H, int W, int C, int RC, int nstrips,
-                                                               int nchunks, int LPU, int UPW, int nsb,
-                                                               const T* __restrict__ x, long ldx,
-                                                               const T* __restrict__ dy, long lddy,
-                                                               float* __restrict__ part) {
-  constexpr int CPT = W3Cfg<T>::EPL, TW = W3_TW, K = 7, NX = TW + K - 1, NV = (K + 1) * CPT;
-  __shared__ float red[4][NV][64];
-  const long l = xcd_remap(blockIdx.x, (long)gridDim.x);
-  const int sb = (int)(l / K), i = (int)(l % K);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int lg = lane % LPU, usub = lane / LPU;
-  const int G = C / CPT, cg = blockIdx.y * LPU + lg;
-  const bool valid = usub < UPW && cg < G;
-  const int c0 = cg * CPT;
-  const long units = w3_units(B, nstrips, nchunks);
-
-  float acc[K + 1][CPT];
-#pragma unroll
-  for (int a = 0; a <= K; ++a)
-#pragma unroll
-    for (int e = 0; e < CPT; ++e) acc[a][e] = 0.f;
-
-  const long stride = (long)nsb * 4 * UPW;
-  for (long u = ((long)sb * 4 + wave) * UPW + usub; valid && u < units; u += stride) {
-    const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
-    const long b = u / ((long)nstrips * nchunks);
-    const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
-    const long img = b * H * W;
-    auto load = [&](int h, uint2* xr, uint2* dr) {  // x row h+i-3 and dy row h (zeros past the chunk)
-      const int hx = h + i - K / 2;
-      const bool hok = h < h1 && hx >= 0 && hx < H;
-#pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        const int w = w0 - K / 2 + q;
-        xr[q] = w3_ld<T>(x + (img + (long)hx * W + w) * ldx + c0, hok && w >= 0 && w < W);
-      }
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int w = w0 + t;
-        dr[t] = w3_ld<T>(dy + (img + (long)h * W + w) * lddy + c0, h < h1 && w < W);
-      }
-    };
-    uint2 xc[NX], dc[TW];
-    load(h0, xc, dc);
-    for (int h = h0; h < h1; ++h) {
-      uint2 xn[NX], dn[TW];
-      load(h + 1, xn, dn);
-      float gv[TW][CPT];
-#pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        w3_unpack<T>(dc[t], gv[t]);
-#pragma unroll
-        for (int e = 0; e < CPT; ++e) acc[K][e] += gv[t][e];
-      }
-#pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        float xv[CPT];
-        w3_unpack<T>(xc[q], xv);
-#pragma unroll
-        for (int t = 0; t < TW; ++t) {
-          const int j = q - t;
-          if (j < 0 || j >= K) continue;
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) acc[j][e] = fmaf(gv[t][e], xv[e], acc[j][e]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NX; ++q) xc[q] = xn[q];
-#pragma unroll
-      for (int t = 0; t < TW; ++t) dc[t] = dn[t];
-    }
-  }
-
-#pragma unroll
-  for (int v = 0; v < NV; ++v) red[wave][v][lane] = acc[v / CPT][v % CPT];
-  __syncthreads();
-  const long pbase = (long)sb * C * (K * K + 1);
-  for (int idx = threadIdx.x; idx < NV * LPU; idx += 256) {
-    const int v = idx / LPU, lq = idx % LPU, tap = v / CPT;
-    const int c = (blockIdx.y * LPU + lq) * CPT + v % CPT;
-    if (c >= C || (tap == K && i != 0)) continue;
-    float sum = 0.f;
-    for (int w = 0; w < 4; ++w)
-      for (int us = 0; us < UPW; ++us) sum += red[w][v][us * LPU + lq];
-    part[pbase + (long)c * (K * K + 1) + (tap < K ? i * K + tap : K * K)] = sum;
-  }
-}
-
-template <typename T>
-long w7_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
-               hipStream_t s) {
-  const W3Geom g = w7_geom<T>(B, H, W, C);
-  DFM_LAUNCH(dw7_stream_wgrad_kernel<T>, dim3((unsigned)(g.nsb * 7), (unsigned)g.slices), dim3(256), 0, s,
-                     B, H, W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (int)g.nsb, (const T*)x, ldx,
-                     (const T*)dy, lddy, part);
-  return g.nsb;
-}
-
 // ---------------------------------------------------------------- LDS-tiled 7x7 weight gradient (v4)
 // The streaming kernel above re-reads every input row once per kernel row (7 blocks) and every
 // input column 2.5x (halo of a 4-wide strip), ~17x the input through L2 per pass. Here a block owns
@@ -860,15 +590,6 @@ long w7l_launch(int B, int H, int W, int C, const void* x, long ldx, const void*
              cdiv(W, W7L_TW), (const T*)x, ldx, (const T*)dy, lddy, part);
   return nsb;
 }
-
-static int w7_mode() {  // DFM_DW_WG7: 2 (default) LDS-tiled v4, 1 row-streaming, 0 LDS-tiled v3 (A/B)
-  static const int m = [] {
-    const char* e = getenv("DFM_DW_WG7");
-    return e ? atoi(e) : 2;
-  }();
-  return m;
-}
-
 
 // ---------------------------------------------------------------- row-streaming 3x3 forward / input gradient
 // The forward counterpart of the streaming weight gradient: a lane owns one 8-byte channel vector
@@ -1201,22 +922,6 @@ long b3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* 
   return g.nsb;
 }
 
-static bool f3_enabled() {  // DFM_DW_F3=0 keeps the LDS-tiled 3x3 forward / input gradient everywhere (A/B)
-  static const bool on = [] {
-    const char* e = getenv("DFM_DW_F3");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
-static bool w3_enabled() {  // DFM_DW_WG3=0 selects the LDS-tiled 3x3 weight gradient (A/B)
-  static const bool on = [] {
-    const char* e = getenv("DFM_DW_WG3");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-
 template <typename T>
 bool dw_aligned(int C, const void* p, long ld) {
   constexpr int CPT = DwCfg<T>::CPT;
@@ -1255,26 +960,15 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
   // streaming 3x3 wins on the mid-size stages (60x80 / 30x40 planes: 4-17% faster on DFormer-B);
   // the LDS-tiled kernel stays ahead on the 120x160 and 15x20 planes
   const long plane = (long)H * W;
-  if (k == 3 && f3_enabled() && plane >= 1024 && plane <= 6144) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
+  if (k == 3 && plane >= 1024 && plane <= 6144) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
   const int G = C / DwCfg<T>::CPT;
   // channel groups per block: as many as the tile geometry allows without idling lanes
 #define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)
-  static const int ng3 = [] {  // DFM_DW_NG3=8: 64-channel (one 128-byte line) blocks for 3x3
-    const char* e = getenv("DFM_DW_NG3");
-    return e ? atoi(e) : 4;
-  }();
   if (k == 3) {
-    if (ng3 == 8 && G >= 8) GO(3, 8);
     if (G >= 4) GO(3, 4);
     if (G >= 2) GO(3, 2);
     GO(3, 1);
   }
-  static const int f7 = [] {  // DFM_DW_F7: 7x7 forward tile variant (0: 4 outputs / thread, 1: 8, 2: 8 with NG 4)
-    const char* e = getenv("DFM_DW_F7");
-    return e ? atoi(e) : 0;
-  }();
-  if (f7 == 1 && G >= 8) return dw_tile_launch<T, 7, FLIP, 8, 1>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
-  if (f7 >= 1 && G >= 4) return dw_tile_launch<T, 7, FLIP, 4, 1>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
   if (G >= 8) GO(7, 8);
   if (G >= 4) GO(7, 4);
   if (G >= 2) GO(7, 2);
@@ -1282,71 +976,6 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
 #undef GO
 }
 
-// Weight-gradient launch geometry: ~2048 blocks (spatial lanes x channel blocks x kernel-row
-// groups), each spatial lane walking its share of the tiles.
-template <typename T, int K, int NG>
-void wgrad_geom(int B, int H, int W, int C, int& tiles_h, int& tiles_w, dim3& grid) {
-  constexpr int TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
-  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS, KI = DwWTile<T, K>::KI;
-  tiles_h = (H + TH - 1) / TH;
-  tiles_w = (W + TWT - 1) / TWT;
-  const long ntiles = (long)B * tiles_h * tiles_w;
-  const unsigned chunks = cdiv(C / DwCfg<T>::CPT, NG), zdim = K / KI;
-  long nsb = (2048 + (long)chunks * zdim - 1) / ((long)chunks * zdim);
-  nsb = std::max(1L, std::min(nsb, ntiles));
-  grid = dim3((unsigned)nsb, chunks, zdim);
-}
-
-template <typename T, int K>
-int wgrad_ng(int C) {
-  const int G = C / DwCfg<T>::CPT;
-  if (K == 3) return G >= 4 ? 4 : (G >= 2 ? 2 : 1);
-  return G >= 8 ? 8 : (G >= 4 ? 4 : (G >= 2 ? 2 : 1));
-}
-
-template <typename T, int K, int NG>
-long wgrad_nsb(int B, int H, int W, int C) {
-  int th, tw;
-  dim3 grid;
-  wgrad_geom<T, K, NG>(B, H, W, C, th, tw, grid);
-  return grid.x;
-}
-
-template <typename T, int K>
-long wgrad_nsb_any(int B, int H, int W, int C) {
-  switch (wgrad_ng<T, K>(C)) {
-    case 8: return wgrad_nsb<T, K, 8>(B, H, W, C);
-    case 4: return wgrad_nsb<T, K, 4>(B, H, W, C);
-    case 2: return wgrad_nsb<T, K, 2>(B, H, W, C);
-    default: return wgrad_nsb<T, K, 1>(B, H, W, C);
-  }
-}
-
-template <typename T, int K, int NG>
-long wgrad_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
-                  hipStream_t s) {
-  constexpr int CPT = DwCfg<T>::CPT, TWS = DwTile<T, K>::TWS, STRIPS = DwTile<T, K>::STRIPS;
-  constexpr int TH = 256 / (NG * STRIPS), TWT = TWS * STRIPS, KI = DwWTile<T, K>::KI;
-  int tiles_h, tiles_w;
-  dim3 grid;
-  wgrad_geom<T, K, NG>(B, H, W, C, tiles_h, tiles_w, grid);
-  const size_t lds_tile = ((size_t)(TH + KI - 1) * (TWT + K - 1) * NG + (size_t)TH * TWT * NG) * 16;
-  const size_t lds_red = (size_t)4 * (KI * K + 1) * NG * CPT * sizeof(float);
-  DFM_LAUNCH((dw_tile_wgrad_kernel<T, K, NG>), grid, dim3(256), std::max(lds_tile, lds_red), s, B, H, W, C,
-                     tiles_h, tiles_w, (const T*)x, ldx, (const T*)dy, lddy, part);
-  return grid.x;
-}
-
-template <typename T, int K>
-long wgrad_dispatch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
-                    hipStream_t s) {
-  switch (wgrad_ng<T, K>(C)) {
-    case 8: return wgrad_launch<T, K, 8>(B, H, W, C, x, ldx, dy, lddy, part, s);
-    case 4: return wgrad_launch<T, K, 4>(B, H, W, C, x, ldx, dy, lddy, part, s);
-    case 2: return wgrad_launch<T, K, 2>(B, H, W, C, x, ldx, dy, lddy, part, s);
-    default: return wgrad_launch<T, K, 1>(B, H, W, C, x, ldx, dy, lddy, part, s);
-  }
-}
 }  // namespace
 
 extern "C" int dfm_dwconv_fwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const float* w,
@@ -1380,12 +1009,9 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
 extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k) {
   long nsb = 1;
   if (k == 3)
-    nsb = std::max({wgrad_nsb_any<float, 3>(B, H, W, C), wgrad_nsb_any<bf16_t, 3>(B, H, W, C),
-                    w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb});
+    nsb = std::max(w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb);
   else if (k == 7)
-    nsb = std::max({wgrad_nsb_any<float, 7>(B, H, W, C), wgrad_nsb_any<bf16_t, 7>(B, H, W, C),
-                    w7_geom<float>(B, H, W, C).nsb, w7_geom<bf16_t>(B, H, W, C).nsb, w7l_nsb<float>(B, H, W, C),
-                    w7l_nsb<bf16_t>(B, H, W, C)});
+    nsb = std::max(w7l_nsb<float>(B, H, W, C), w7l_nsb<bf16_t>(B, H, W, C));
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);
 }
 
@@ -1432,26 +1058,17 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
   long nsb;
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                    : w7_mode() == 1 ? w7_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                     : wgrad_dispatch<bf16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
-          : w3_enabled() ? w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                         : wgrad_dispatch<bf16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    nsb = k == 7 ? w7l_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                 : w3_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, part, s);
   }
   else if (dtype == DFM_F16) {
     DFM_CHECK_ARG(dw_aligned<f16_t>(C, x, ldx) && dw_aligned<f16_t>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                    : w7_mode() == 1 ? w7_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                     : wgrad_dispatch<f16_t, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
-          : w3_enabled() ? w3_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                         : wgrad_dispatch<f16_t, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    nsb = k == 7 ? w7l_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                 : w3_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else if (dtype == DFM_F32) {
     DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy), "dwconv wgrad: alignment");
-    nsb = k == 7 ? (w7_mode() == 2 ? w7l_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                    : w7_mode() == 1 ? w7_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                                     : wgrad_dispatch<float, 7>(B, H, W, C, x, ldx, dy, lddy, part, s))
-          : w3_enabled() ? w3_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
-                         : wgrad_dispatch<float, 3>(B, H, W, C, x, ldx, dy, lddy, part, s);
+    nsb = k == 7 ? w7l_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s)
+                 : w3_launch<float>(B, H, W, C, x, ldx, dy, lddy, part, s);
   } else {
     dfm_set_error("dfm_dwconv_bwd_weight: bad dtype");
     return DFM_ERR_DTYPE;

@@ -156,14 +156,10 @@ int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, c
   const int nblk = red_blocks(rows);
   constexpr int V = 16 / sizeof(T);
   const int G = C / V;
-  // The vectorized narrow-row reduction is the default (DFM_COLRED_VEC=0 selects the scalar kernel
-  // for A/B timing). BN statistics are sums shifted by the first row, so the variance no longer
-  // cancels (E[x²] - E[x]² moved the fp32 input-gradient golden past 1e-3 in round 1).
-  static const bool vec_on = [] {
-    const char* e = getenv("DFM_COLRED_VEC");
-    return !e || atoi(e) != 0;
-  }();
-  const bool vec = vec_on && C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
+  // The vectorized narrow-row reduction wherever the row layout allows it. BN statistics are sums
+  // shifted by the first row, so the variance does not cancel (E[x²] - E[x]² moved the fp32
+  // input-gradient golden past 1e-3 in round 1).
+  const bool vec = C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
                    (!y || (ldy % V == 0 && ((uintptr_t)y & 15) == 0));
   if (vec)
     DFM_LAUNCH((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,

@@ -9,7 +9,6 @@ statistics on the library's shifted-sum BN kernels, then one gather that folds t
 the stem's GELU) into the convolution operand and one MFMA GEMM (csrc/conv.hip), reading the raw
 input image and the previous stage's NHWC rows in place (no NCHW<->NHWC permute copies).
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -107,15 +106,11 @@ class Attention(nn.Module):
 
 
 _SIDE = {}
-_STREAMS = os.environ.get("DFM_STREAMS", "1") != "0"  # DFM_STREAMS=0: one stream (A/B timing)
-# DFM_SIDE_FROM=i: the depth-branch ConvFFN side stream only from stage i on (the stage-0 kernels are
-# thousands of blocks each, HBM-bound on their own)
-_SIDE_FROM = int(os.environ.get("DFM_SIDE_FROM", "0"))
 
 
 def _side_stream(dev):
-    if not _STREAMS:
-        return None
+    """The depth-branch ConvFFN (mlp_e2) stream: independent of the RGB branch's ConvFFN within a
+    Block, so the two overlap (the stage-2/3 kernels alone leave most CUs idle)."""
     s = _SIDE.get(dev)
     if s is None:
         s = _SIDE[dev] = torch.cuda.Stream(device=dev)
@@ -179,7 +174,7 @@ class Block(nn.Module):
         # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
         # does its backward: autograd replays a node on its forward's stream), which fills the GPU
         # at the late stages where each kernel alone is latency-bound
-        side = _side_stream(x.device) if x1.is_cuda and int(st[1:] if st[1:].isdigit() else 9) >= _SIDE_FROM else None
+        side = _side_stream(x.device) if x1.is_cuda else None
         if side is not None:
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)

@@ -9,7 +9,6 @@ Reference semantics (file:line in Originofamonia/DFormer):
   ConvFFNFn     MLP.forward + Block residual/layer-scale/DropPath   DFormer.py:48-67, 173-179
   AttentionFn   Attention.forward + Block residuals                 DFormer.py:70-145, 168-179
 """
-import os
 import weakref
 
 import torch
@@ -134,69 +133,9 @@ def gslot_rows(*ps):
     return ss[0][0][ss[0][1]:off].view(rows, *cols) if cols else ss[0][0][ss[0][1]:off]
 
 
-# ---------------------------------------------------------------- weight-gradient stream
-# The weight gradients (split-K wgrad GEMMs, depthwise dW) are off the backward's critical path:
-# nothing consumes them before the optimizer. When they land in flat-gradient slots (persistent
-# buffers, FusedAdamW built) they are issued on a second stream that forks from the current one at
-# each call, so they overlap the data-gradient chain of the following layers (the stage-2/3 kernels
-# alone are latency-bound and leave most CUs idle). FusedAdamW.step and GradBuckets' all-reduces
-# join the stream (join_wgrad). Off by default (DFM_WGRAD_STREAM=1 enables it): measured on MI355X
-# the overlap LOSES — 369.8 vs 381.1 images/s on the DFormer-B step — the split-K wgrad grids
-# (hundreds of blocks) crowd out the latency-bound data-gradient chain instead of filling its gaps.
-_WG_ON = os.environ.get("DFM_WGRAD_STREAM", "0") == "1"
-_WG_STREAM = {}
-
-
-def _wg_stream(dev):
-    s = _WG_STREAM.get(dev)
-    if s is None:
-        s = _WG_STREAM[dev] = torch.cuda.Stream(device=dev)
-    return s
-
-
-def offload_wgrad(outs, inputs, fn):
-    """fn() — weight-gradient launches writing only into `outs` — on the weight-gradient stream when
-    every out is a flat-gradient slot; `inputs` (the tensors fn reads) are recorded on that stream
-    so the allocator does not hand their memory out before it is done."""
-    if not _WG_ON or any(o is None for o in outs) or not inputs[0].is_cuda:
-        return fn()
-    dev = inputs[0].device
-    ws = _wg_stream(dev)
-    ws.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(ws):
-        r = fn()
-    for t in inputs:
-        t.record_stream(ws)
-    return r
-
-
-# DFM_WGRAD_GROUP_STREAM=1: a Block's grouped weight-gradient launches (kernels.wgrad_group) are issued
-# on the weight-gradient stream, forked from the current stream at the end of the Block's backward,
-# so they overlap the next Block's data-gradient chain (joined like the offloaded weight gradients).
-_WG_GROUP_SIDE = os.environ.get("DFM_WGRAD_GROUP_STREAM", "0") == "1"
-
-
-def _flush_wgrad_side(pending):
-    dev = pending[0][2].device
-    ws = _wg_stream(dev)
-    ws.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(ws):
-        K.flush_wgrad(pending)
-    for item in pending:  # operands / outputs stay allocated until the stream is done with them
-        for t in item[2:5] + item[8:10]:
-            if t is not None:
-                t.record_stream(ws)
-
-
 def wgrad_group():
     """The weight-gradient queue of one Block backward (kernels.wgrad_group)."""
-    return K.wgrad_group(_flush_wgrad_side if _WG_GROUP_SIDE else None)
-
-
-def join_wgrad():
-    """The current stream waits for every weight-gradient launch issued so far."""
-    for dev, s in _WG_STREAM.items():
-        torch.cuda.current_stream(dev).wait_stream(s)
+    return K.wgrad_group()
 
 
 _SIDE_STREAMS = []
@@ -213,7 +152,7 @@ def join_streams(main=None):
     """The current stream waits for everything issued so far on `main` (the stream the step's
     backward was started from) and on every side stream of this package, so a collective enqueued
     next sees every gradient slot complete whichever stream autograd ran its last hook on."""
-    streams = ([main] if main is not None else []) + _SIDE_STREAMS + list(_WG_STREAM.values())
+    streams = ([main] if main is not None else []) + _SIDE_STREAMS
     if not streams:  # CPU tensors / nothing issued off the current stream
         return
     cur = torch.cuda.current_stream()
@@ -236,34 +175,15 @@ def _cat1(*vs):
     return out
 
 
-# DFM_FUSED_FFN=1 runs the ConvFFN on the fused kernels (csrc/convffn.hip) wherever they support the
-# width (C <= 64). Off by default: measured on MI355X (tools/ffn_ab.py, DFormer-B bf16 bs 16) the fused
-# forward beats the separate kernels (stage 0: 0.317 vs 0.574 ms) but the fused backward, which
-# recomputes fc1 on a 2-pixel halo and the depthwise / GELU chain per hidden chunk at two waves per
-# SIMD, does not (stage 0 fwd+bwd 1.70 vs 1.51 ms; the whole step 367 vs 381 images/s).
-FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
-# DFM_DW_FUSED_BWD=0: the unfused ConvFFN backward runs the DW3x3 input and weight gradients as two kernels
-_DW_FUSED_BWD = os.environ.get("DFM_DW_FUSED_BWD", "1") == "1"
-
-
-def _ffn_fusable(x, w1, *aligned):
-    """The fused kernels take 16-byte aligned rows and parameter vectors (true for every DFormer
-    size: channel counts are multiples of 16, so flat-buffer offsets are too)."""
-    return (FUSED_FFN and x.is_cuda and x.stride(1) == 1 and x.stride(0) % 8 == 0 and
-            all(t.data_ptr() % 16 == 0 for t in (x,) + aligned) and K.convffn_supported(x, x.shape[1], w1.shape[0]))
-
-
 # ====================================================================== ConvFFN (+ residual)
 class ConvFFNFn(torch.autograd.Function):
     """out = x + rowscale * ls * fc2(GELU(DW3x3(h) + h)),  h = fc1(LN(x))   on [P, C] rows.
 
-    fused (C <= 64, csrc/convffn.hip): LN, then one kernel for fc1 -> DW3x3 + identity -> GELU ->
-    fc2 -> residual (the [P, rC] hidden activation stays on chip; only f = the branch output is
-    saved); backward: residual chain rule, one kernel recomputing h / hpre per tile and producing
-    g, dh, dxn and the depthwise gradients, then the fc2 / fc1 weight-gradient GEMMs and the LN
-    backward.
-    unfused (wider C): LN, GEMM fc1(+bias), DW3x3(+bias+identity, +GELU second output),
-             GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue)."""
+    forward: LN, GEMM fc1(+bias), DW3x3(+bias+identity) writing GELU'(hpre) and GELU(hpre) from one
+    erf evaluation, GEMM fc2(+bias, preact f, residual/layer-scale/DropPath epilogue).
+    backward: residual chain rule, fc2 input gradient times the stored GELU', the DW3x3 input and
+    weight gradients in one pass, fc1 input gradient, LN backward; the fc2 / fc1 weight gradients
+    as one grouped launch at the end."""
 
     @staticmethod
     def forward(ctx, x, shape, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls):
@@ -274,11 +194,6 @@ class ConvFFNFn(torch.autograd.Function):
         ctx.tag = K.TAG
         xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
         ctx.shape = shape
-        ctx.fused = _ffn_fusable(x, w1, W1, W2, b1, wpos, bpos)
-        if ctx.fused:
-            out, f = K.convffn_fwd(xn, x, shape, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
-            ctx.save_for_backward(x, xn, mu, rs, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
-            return out
         h = K.linear(xn, W1, b1)
         g = torch.empty_like(h)
         # the DW kernel writes GELU'(hpre) instead of hpre (GELU and its derivative share one erf):
@@ -292,98 +207,40 @@ class ConvFFNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         K.TAG = ctx.tag + ".bwd"
-        if ctx.fused:
-            return ConvFFNFn._backward_fused(ctx, dout)
         with wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
-            return ConvFFNFn._backward_unfused(ctx, dout)
-
-    @staticmethod
-    def _backward_unfused(ctx, dout):
-        x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
-        B, H, W = ctx.shape
-        dt = x.dtype
-        dout = dout.contiguous()
-        W1, W2 = wcast(dt, w1), wcast(dt, w2)
-        rps = H * W
-        df, dls = K.residual_bwd(dout, f, ls, rowscale, rps)
-        o2, ob2 = gslot2(w2), gslot(b2)
-        dW2, db2 = offload_wgrad((o2, ob2), (df, g),
-                                 lambda: K.linear_wgrad(df, g, out=o2, bias_grad=True, bias_out=ob2))
-        dhpre = K.linear_dgrad(df, W2, mul=gp)  # GELU backward: times the stored GELU'(hpre)
-        ow, ob = gslot(wpos), gslot(bpos)
-        if _DW_FUSED_BWD:  # input and weight gradients of DW3x3 + identity in one pass over dhpre, h
-            dh, dwpos, dbpos = K.dwconv_bwd(h, dhpre, ctx.shape, wpos, 3, add_identity=True, dw=ow, db=ob)
-        else:
-            dwpos, dbpos = offload_wgrad((ow, ob), (h, dhpre),
-                                         lambda: K.dwconv_bwd_weight(h, dhpre, ctx.shape, 3, dw=ow, db=ob))
-            dh = K.dwconv_bwd_data(dhpre, ctx.shape, wpos, 3, add_identity=True)
-        o1, ob1 = gslot2(w1), gslot(b1)
-        dW1, db1 = offload_wgrad((o1, ob1), (dh, xn),
-                                 lambda: K.linear_wgrad(dh, xn, out=o1, bias_grad=True, bias_out=ob1))
-        dxn = K.linear_dgrad(dh, W1)
-        dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
-        return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
-                dls)
-
-    @staticmethod
-    def _backward_fused(ctx, dout):
-        x, xn, mu, rs, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
-        B, H, W = ctx.shape
-        dt = x.dtype
-        dout = dout.contiguous()
-        df, dls = K.residual_bwd(dout, f, ls, rowscale, H * W)
-        g, dh, dxn, dwpos, dbpos = K.convffn_bwd(xn, df, ctx.shape, wcast(dt, w1), b1, wpos, bpos, wcast(dt, w2),
-                                                 dw=gslot(wpos), db=gslot(bpos))
-        dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
-        dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
-        dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
+            x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
+            B, H, W = ctx.shape
+            dt = x.dtype
+            dout = dout.contiguous()
+            W1, W2 = wcast(dt, w1), wcast(dt, w2)
+            df, dls = K.residual_bwd(dout, f, ls, rowscale, H * W)
+            dW2, db2 = K.linear_wgrad(df, g, out=gslot2(w2), bias_grad=True, bias_out=gslot(b2))
+            dhpre = K.linear_dgrad(df, W2, mul=gp)  # GELU backward: times the stored GELU'(hpre)
+            # input and weight gradients of DW3x3 + identity in one pass over dhpre, h
+            dh, dwpos, dbpos = K.dwconv_bwd(h, dhpre, ctx.shape, wpos, 3, add_identity=True, dw=gslot(wpos),
+                                            db=gslot(bpos))
+            dW1, db1 = K.linear_wgrad(dh, xn, out=gslot2(w1), bias_grad=True, bias_out=gslot(b1))
+            dxn = K.linear_dgrad(dh, W1)
+            dx, dlnw, dlnb = K.layernorm_bwd(x, dxn, ln_w, mu, rs, dres=dout)
         return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
                 dls)
 
 
 # ====================================================================== Attention (+ residuals)
-# The depth branch of the attention forward (LN_e -> e_fore -> DW7x7 -> e_back, DFormer.py:84-88,
-# 133) is independent of the RGB branch until the projections: it runs on a side stream forked at
-# the Block's start and joined before proj (DFM_ATTN_STREAM=1). Off by default: measured on the
-# DFormer-B step it does not pay (381.6 vs 383.4 images/s, two A/B pairs) — unlike the depth-branch
-# ConvFFN stream, the branch is short and the fork/join events cost what the overlap gains.
-_ATTN_SIDE_ON = os.environ.get("DFM_ATTN_STREAM", "0") == "1"
-_ATTN_SIDE = {}
 # The depth branch of the attention BACKWARD (dual product -> e_back -> DW7x7 -> e_fore gradients,
 # DFormer.py:84-88, 133) is the longer chain (8 launches) and independent of the RGB branch until
-# the q|q_cut|l gradients, so it is issued on a side stream (DFM_ATTN_BWD_STREAM=0: one stream).
-# Measured on MI355X, DFormer-B bf16 bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s.
-_ATTN_BWD_SIDE_ON = os.environ.get("DFM_ATTN_BWD_STREAM", "1") == "1"
-_ATTN_BWD_SIDE_FROM = int(os.environ.get("DFM_ATTN_BWD_SIDE_FROM", "0"))  # first stage that uses it
-
-
-def _stage_no(tag):
-    """Stage index of a component tag such as 's2.attn' (9 when unknown: side streams stay on)."""
-    t = (tag or "").split(".")[0]
-    return int(t[1:]) if t[:1] == "s" and t[1:].isdigit() else 9
+# the q|q_cut|l gradients, so it is issued on a side stream. Measured on MI355X, DFormer-B bf16
+# bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s on one stream. (The forward's depth
+# branch on a side stream measured 381.6 vs 383.4 images/s and was dropped: it is short and the
+# fork / join costs what the overlap gains; a second backward stream for the pooled-attention
+# branch gained nothing either.)
 _ATTN_BWD_SIDE = {}
-# DFM_ATTN_BWD_STREAM2=1 (with the above): the pooled-attention part of the RGB branch (bilinear,
-# attention, short_cut_linear and kv gradients) on a second side stream, overlapping the
-# conv-modulation part (q*a, a, DW7x7 gradients); dg = DW7x7^T(...) + dkv Wkv after the join.
-_ATTN_BWD_SIDE2_ON = os.environ.get("DFM_ATTN_BWD_STREAM2", "0") == "1"
 
 
-def _attn_bwd_side(dev, which=1):
-    if not _ATTN_BWD_SIDE_ON or (which == 2 and not _ATTN_BWD_SIDE2_ON):
-        return None
-    st = _ATTN_BWD_SIDE.get((dev, which))
+def _attn_bwd_side(dev):
+    st = _ATTN_BWD_SIDE.get(dev)
     if st is None:
-        st = _ATTN_BWD_SIDE[(dev, which)] = torch.cuda.Stream(device=dev)
-        register_side_stream(st)
-    return st
-
-
-def _attn_side(dev):
-    if not _ATTN_SIDE_ON:
-        return None
-    st = _ATTN_SIDE.get(dev)
-    if st is None:
-        st = _ATTN_SIDE[dev] = torch.cuda.Stream(device=dev)
+        st = _ATTN_BWD_SIDE[dev] = torch.cuda.Stream(device=dev)
         register_side_stream(st)
     return st
 
@@ -406,79 +263,48 @@ class AttentionFn(torch.autograd.Function):
         dev = x.device
         rps = H * W
         ctx.tag = K.TAG
-        side = _attn_side(dev) if x.is_cuda else None
-        main = torch.cuda.current_stream(dev) if side is not None else None
         fw = 2 * C if window else C + Ch
         f = torch.empty(P, fw, device=dev, dtype=dt)
-        if side is not None:
-            side.wait_stream(main)
-            with torch.cuda.stream(side):  # depth branch, part 1: LN_e, e_fore, DW7x7
-                xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
-                ev_xen = torch.cuda.Event()
-                ev_xen.record(side)
-                e1 = K.linear(xen, wcast(dt, wef), bef)
-                e2 = K.dwconv(e1, shape, wec, bec, 7)
-        else:
-            xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
+        xen, mu2, rs2 = K.layernorm(xe, ne_w, ne_b, 1e-6)
         xn, mu1, rs1 = K.layernorm(x, n_w, n_b, 1e-6)
         # q | q_cut | l in one GEMM; GELU only on the l columns, whose derivative (act 3) is stored
-        # for the backward. Without the side stream, e_fore joins it in one grouped launch.
+        # for the backward
         Wqcl = wcast(dt, wq, wqc, wl)
         bqcl = _cat1(bq, bqc, bl)
         qcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         lpre = torch.empty(P, C, device=dev, dtype=dt)
-        with K.gemm_group():
-            K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl, defer=True)
-            if side is None:
-                e1 = K.linear(xen, wcast(dt, wef), bef, defer=True)
+        K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl)
+        e1 = K.linear(xen, wcast(dt, wef), bef)
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         xep = torch.empty(P, Ch, device=dev, dtype=dt)
-        if side is not None:  # depth branch, part 2: e_back * cx (needs the q|q_cut|l GEMM)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
-        # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward); with kv = Linear(g) and (no
-        # side stream) e_back(DW7(e_fore)) * cx as one grouped launch
+        # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward)
         apre = K.dwconv(g, shape, wconv, bconv, 7)
-        if side is None:
-            e2 = K.dwconv(e1, shape, wec, bec, 7)
+        e2 = K.dwconv(e1, shape, wec, bec, 7)
         a = torch.empty(P, C, device=dev, dtype=dt)
-        with K.gemm_group():
-            K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C], defer=True)
-            if window:
-                kv = K.linear(g, wcast(dt, wkv), bkv, defer=True)
-            if side is None:
-                K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:], defer=True)
+        K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C])
+        if window:
+            kv = K.linear(g, wcast(dt, wkv), bkv)
+        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
+        K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
         saved_attn = ()
         if window:
             dh = C // heads // 2
             pooled = torch.empty(B * 49, C + Ch, device=dev, dtype=dt)
             K.pool7(xn, shape, out=pooled[:, :C])
-            if side is not None:
-                main.wait_event(ev_xen)
             K.pool7(xen, shape, out=pooled[:, C:])
             m = K.linear(pooled, wcast(dt, wsc), bsc)
             o, lse = K.pooled_attn(m, kv[:, :Ch], kv[:, Ch:], B, heads, P // B, dh, dh ** -0.5)
             K.bilinear(o, (7, 7), (H, W), B, out=f[:, C:C + Ch])
             saved_attn = (kv, pooled, m, o, lse)
-        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe' (grouped above)
-        if side is not None:  # join; tensors that crossed streams stay alive until both are done with them
-            main.wait_stream(side)
-            for t in (xen, mu2, rs2, e1, e2):
-                t.record_stream(main)
-            for t in (xe, f, qcl, xep):
-                t.record_stream(side)
         # projections with the Block's residual / layer-scale / DropPath epilogue
         p1 = torch.empty(P, C, device=dev, dtype=dt)
-        with K.gemm_group():  # proj and proj_e (each with its own residual epilogue) in one launch
-            x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale,
-                          rows_per_scale=rps, defer=True)
-            if drop_depth:
-                xe1, p1e = xe, None
-            else:
-                p1e = torch.empty(P, Ch, device=dev, dtype=dt)
-                xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
-                               rows_per_scale=rps, defer=True)
+        x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
+        if drop_depth:
+            xe1, p1e = xe, None
+        else:
+            p1e = torch.empty(P, Ch, device=dev, dtype=dt)
+            xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
+                           rows_per_scale=rps)
         ctx.shape, ctx.heads, ctx.window, ctx.drop_depth = shape, heads, window, drop_depth
         ctx.n_attn = len(saved_attn)
         ctx.save_for_backward(x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1,
@@ -524,8 +350,7 @@ class AttentionFn(torch.autograd.Function):
             _, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps, df=dpc[:, :C])
             _, grads["ls1e"] = K.residual_bwd(dxe1, p1e, ls1e, rowscale_e, rps, df=dpc[:, C:])
             ow, ob = gslot_rows(wp, wpe), gslot_rows(bp, bpe)
-            dWc, dbc = offload_wgrad((ow, ob), (dpc, f),
-                                     lambda: K.linear_wgrad(dpc, f, out=ow, bias_grad=True, bias_out=ob))
+            dWc, dbc = K.linear_wgrad(dpc, f, out=ow, bias_grad=True, bias_out=ob)
             grads["wp"], grads["wpe"] = dWc[:C], dWc[C:]
             grads["bp"], grads["bpe"] = dbc[:C], dbc[C:]
             df = K.linear_dgrad(dpc, wcast(dt, wp, wpe))
@@ -533,23 +358,20 @@ class AttentionFn(torch.autograd.Function):
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
-        side = _attn_bwd_side(dev) if x.is_cuda and _stage_no(ctx.tag) >= _ATTN_BWD_SIDE_FROM else None
+        side = _attn_bwd_side(dev) if x.is_cuda else None
         main = torch.cuda.current_stream(dev) if side is not None else None
 
         def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))
             dcxe = df[:, fw - Ch:]
             _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
             ow, ob = gslot2(web), gslot(beb)
-            grads["web"], grads["beb"] = offload_wgrad((ow, ob), (dxep, e2), lambda: K.linear_wgrad(
-                dxep, e2, out=ow, bias_grad=True, bias_out=ob))
+            grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=ow, bias_grad=True, bias_out=ob)
             de2 = K.linear_dgrad(dxep, wcast(dt, web))
             ow, ob = gslot(wec), gslot(bec)
-            grads["wec"], grads["bec"] = offload_wgrad((ow, ob), (e1, de2), lambda: K.dwconv_bwd_weight(
-                e1, de2, shape, 7, dw=ow, db=ob))
+            grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7, dw=ow, db=ob)
             de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
             ow, ob = gslot2(wef), gslot(bef)
-            grads["wef"], grads["bef"] = offload_wgrad((ow, ob), (de1, xen), lambda: K.linear_wgrad(
-                de1, xen, out=ow, bias_grad=True, bias_out=ob))
+            grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, out=ow, bias_grad=True, bias_out=ob)
             return K.linear_dgrad(de1, wcast(dt, wef)), (dxep, de2, de1)
 
         if side is not None:  # the depth branch overlaps the RGB branch; joined before q|q_cut|l
@@ -563,8 +385,6 @@ class AttentionFn(torch.autograd.Function):
         dg = torch.empty(P, C, device=dev, dtype=dt)
         dxn = None
         dpooled_e = None
-        side2 = _attn_bwd_side(dev, 2) if (window and side is not None) else None
-        dkv = None
 
         def pooled_branch():  # softmax(q_pool k^T) v over the pooled queries, DFormer.py:119-131
             kv, pooled, m, o, lse = saved_attn
@@ -575,42 +395,26 @@ class AttentionFn(torch.autograd.Function):
             K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
                               dkv[:, :Ch], dkv[:, Ch:])
             ow, ob = gslot2(wsc), gslot(bsc)
-            grads["wsc"], grads["bsc"] = offload_wgrad((ow, ob), (dm, pooled), lambda: K.linear_wgrad(
-                dm, pooled, out=ow, bias_grad=True, bias_out=ob))
+            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, out=ow, bias_grad=True, bias_out=ob)
             dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
             dxn = K.pool7_bwd(dpooled[:, :C], shape)
             ow, ob = gslot2(wkv), gslot(bkv)
-            grads["wkv"], grads["bkv"] = offload_wgrad((ow, ob), (dkv, g), lambda: K.linear_wgrad(
-                dkv, g, out=ow, bias_grad=True, bias_out=ob))
-            return dxn, dpooled, dkv, (do, dm)
+            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, out=ow, bias_grad=True, bias_out=ob)
+            return dxn, dpooled, dkv
 
-        if side2 is not None:  # the pooled-attention branch overlaps the conv-modulation branch
-            side2.wait_stream(main)
-            with torch.cuda.stream(side2):
-                dxn, dpooled, dkv, side2_tmp = pooled_branch()
-            for t in (df, g) + tuple(saved_attn):
-                t.record_stream(side2)
-            dpooled_e = dpooled[:, C:]
-        elif window:
-            dxn, dpooled, dkv, _ = pooled_branch()
+        if window:
+            dxn, dpooled, dkv = pooled_branch()
             dpooled_e = dpooled[:, C:]
             K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
         _, da = K.dual_mul(dqa, a, q, out1=dq)
         ow, ob = gslot2(wa), gslot(ba)
-        grads["wa"], grads["ba"] = offload_wgrad((ow, ob), (da, apre), lambda: K.linear_wgrad(
-            da, apre, out=ow, bias_grad=True, bias_out=ob))
+        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=ow, bias_grad=True, bias_out=ob)
         dapre = K.linear_dgrad(da, wcast(dt, wa))
         ow, ob = gslot(wconv), gslot(bconv)
-        grads["wconv"], grads["bconv"] = offload_wgrad((ow, ob), (g, dapre), lambda: K.dwconv_bwd_weight(
-            g, dapre, shape, 7, dw=ow, db=ob))
-        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window) and side2 is None)
-        if side2 is not None:  # join the pooled branch: dg += dkv Wkv
-            main.wait_stream(side2)
-            for t in (dxn, dpooled, dkv) + side2_tmp:
-                t.record_stream(main)
-            K.linear_dgrad(dkv, wcast(dt, wkv), out=dg, accumulate=True)
+        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=ow, db=ob)
+        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
         K.scale_mul(dg, mul=lpre, out=dl)  # lpre holds GELU'(l pre-activation)
         if side is not None:  # join the depth branch (dcx columns of dqcl, dxen)
             main.wait_stream(side)

@@ -5,7 +5,6 @@ All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose la
 Activations are float32 or bfloat16; statistics / params / param-grads are float32.
 """
 import ctypes
-import os
 
 import torch
 
@@ -96,45 +95,26 @@ def rows_of(t):
 # they are queued and issued at the end of the block as grouped launches (dfm_gemm_group, up to 8
 # problems each + one split-K combine), so the independent dW GEMMs of a Block's backward share the
 # chip instead of each splitting K over all of it. Their outputs must not be read before the block
-# ends (they only feed the optimizer). DFM_WGRAD_GROUP=0: immediate launches (A/B timing).
-WGRAD_GROUP = os.environ.get("DFM_WGRAD_GROUP", "1") == "1"
+# ends (they only feed the optimizer).
 _WG_PENDING = None
 
 
 class wgrad_group:
-    """Queue the weight-gradient GEMMs issued inside; at exit issue them with `flush` (default
-    flush_wgrad on the current stream)."""
-
-    def __init__(self, flush=None):
-        self.flush = flush
+    """Queue the weight-gradient GEMMs issued inside; at exit issue them with flush_wgrad on the
+    current stream."""
 
     def __enter__(self):
         global _WG_PENDING
         self.prev = _WG_PENDING
-        _WG_PENDING = [] if WGRAD_GROUP else None
+        _WG_PENDING = []
         return self
 
     def __exit__(self, exc_type, exc, tb):
         global _WG_PENDING
         pending, _WG_PENDING = _WG_PENDING, self.prev
         if pending and exc_type is None:
-            (self.flush or flush_wgrad)(pending)
+            flush_wgrad(pending)
         return False
-
-
-# Independent forward GEMMs of a Block issued as one grouped launch (kernels.linear(..., defer=True)
-# inside `with gemm_group():`); DFM_FWD_GROUP=0: separate launches (A/B timing).
-# Measured on MI355X: 403.6 vs 415.4 images/s — the grouped launch runs the register-staged 128x128
-# kernel, which loses more on these shapes than the saved launches give back, so it stays off.
-FWD_GROUP = os.environ.get("DFM_FWD_GROUP", "0") == "1"
-
-
-class gemm_group(wgrad_group):
-    def __enter__(self):
-        global _WG_PENDING
-        self.prev = _WG_PENDING
-        _WG_PENDING = [] if FWD_GROUP else None
-        return self
 
 
 def flush_wgrad(pending):
@@ -153,6 +133,7 @@ def flush_wgrad(pending):
             pc = (ctypes.c_void_p * n)(*[c[4].data_ptr() for c in chunk])
             dev = chunk[0][2].device
             ws = _ws(lib.dfm_gemm_group_workspace_size(n, descs), dev)
+            descs[0].workspace_bytes = ws.numel() if ws is not None else 0
             check(lib.dfm_gemm_group(dt, n, descs, ctypes.cast(pa, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p),
                                      ctypes.cast(pc, ctypes.c_void_p), ptr(ws), stream()), "dfm_gemm_group")
             if ACCOUNT is not None:
@@ -163,6 +144,8 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
          ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
          colsum_accumulate=False, mul_gelu_grad=False, defer=False):
+    """One dfm_gemm launch. defer=True (weight gradients) inside `with wgrad_group():` queues it for
+    the block's grouped launch instead."""
     dt = dtype_code(a)
     assert b.dtype == a.dtype, (a.dtype, b.dtype)
     c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
@@ -187,6 +170,7 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
         return out
     nbytes = lib.dfm_gemm_workspace_size(d)
     ws = _ws(nbytes, a.device)
+    d.workspace_bytes = ws.numel() if ws is not None else 0
     check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
     if ACCOUNT is not None:
         _acct(2.0 * M * N * K * nb, byt, peak)
@@ -194,9 +178,8 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
 
 
 def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=None, rowscale=None,
-           rows_per_scale=1, out=None, beta=0.0, act_col0=0, defer=False):
-    """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward). defer=True inside a gemm_group block:
-    queued and issued with the block's other GEMMs as one grouped launch at its end."""
+           rows_per_scale=1, out=None, beta=0.0, act_col0=0):
+    """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward)."""
     M, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -204,8 +187,7 @@ def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=
     return gemm(x, w, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=ld(x), ldb=ld(w), out=out, ldc=ld(out),
                 beta=beta, bias=bias, act=act, preact=preact, ldpre=ld(preact) if preact is not None else 0,
                 mul=mul, ldmul=ld(mul) if mul is not None else 0, res=res, ldres=ld(res) if res is not None else 0,
-                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0,
-                defer=defer)
+                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0)
 
 
 def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None):
@@ -297,52 +279,6 @@ def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
     if ACCOUNT is not None:
         _acct(0, rows * C * _es(dout) * 3)
     return df, dls
-
-
-# ------------------------------------------------------------------------------ fused ConvFFN
-def convffn_supported(x, C, hid):
-    return bool(lib.dfm_convffn_supported(dtype_code(x), C, hid))
-
-
-def convffn_fwd(xn, x, shape, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, out=None, f=None):
-    """out = x + rowscale*ls*(fc2(GELU(DW3(h) + bpos + h)) + b2), h = fc1(xn) + b1; also f = the
-    pre-residual branch (DFormer.py:48-67, 173-179). w1 [hid, C], w2 [C, hid] in the compute dtype."""
-    B, H, W = shape
-    P, C = xn.shape
-    hid = w1.shape[0]
-    if out is None:
-        out = torch.empty(P, C, device=x.device, dtype=x.dtype)
-    if f is None:
-        f = torch.empty(P, C, device=x.device, dtype=x.dtype)
-    check(lib.dfm_convffn_fwd(dtype_code(xn), B, H, W, C, hid, ptr(xn), ld(xn), ptr(x), ld(x), ptr(w1), ptr(b1),
-                              ptr(wpos), ptr(bpos), ptr(w2), ptr(b2), ptr(ls), ptr(rowscale), ptr(out), ld(out),
-                              ptr(f), ld(f), stream()), "dfm_convffn_fwd")
-    if ACCOUNT is not None:
-        _acct(4.0 * P * C * hid + 18.0 * P * hid, _es(x) * P * C * 4 + 2 * _es(x) * C * hid)
-    return out, f
-
-
-def convffn_bwd(xn, df, shape, w1, b1, wpos, bpos, w2, dw=None, db=None):
-    """Backward of convffn_fwd given df = dout*ls*rowscale: returns (g, dh, dxn, dwpos, dbpos) with
-    g = GELU(hpre) and dh = dL/dh ([P, hid], for the fc2 / fc1 weight-gradient GEMMs).
-    w1 [hid, C], w2 [C, hid] in the compute dtype (nn.Linear layouts)."""
-    B, H, W = shape
-    P, C = xn.shape
-    hid = w1.shape[0]
-    g = torch.empty(P, hid, device=xn.device, dtype=xn.dtype)
-    dh = torch.empty(P, hid, device=xn.device, dtype=xn.dtype)
-    dxn = torch.empty(P, C, device=xn.device, dtype=xn.dtype)
-    if dw is None:
-        dw = torch.empty(hid, 1, 3, 3, device=xn.device, dtype=torch.float32)
-    if db is None:
-        db = torch.empty(hid, device=xn.device, dtype=torch.float32)
-    ws = _ws(lib.dfm_convffn_bwd_workspace(dtype_code(xn), B, H, W, C, hid), xn.device)
-    check(lib.dfm_convffn_bwd(dtype_code(xn), B, H, W, C, hid, ptr(xn), ld(xn), ptr(df), ld(df), ptr(w1), ptr(b1),
-                              ptr(wpos), ptr(bpos), ptr(w2), ptr(g), ld(g), ptr(dh), ld(dh), ptr(dxn), ld(dxn),
-                              ptr(dw), ptr(db), ptr(ws), stream()), "dfm_convffn_bwd")
-    if ACCOUNT is not None:
-        _acct(6.0 * P * C * hid + 36.0 * P * hid, _es(xn) * (P * C * 3 + P * hid * 2) + 3 * _es(xn) * C * hid)
-    return g, dh, dxn, dw, db
 
 
 # ---------------------------------------------------------------------------- depthwise conv

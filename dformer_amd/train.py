@@ -54,20 +54,26 @@ class WarmUpPolyLR:
 
 def _chain_order(params, chains):
     """params reordered so that the members of each chain follow its first member (a chain's flat
-    slots are then adjacent: one view serves the fused GEMM over them, e.g. q | q_cut | l)."""
+    slots are then adjacent: one view serves the fused GEMM over them, e.g. q | q_cut | l).
+    Only chains whose head is in `params` are regrouped; a member whose head is frozen (or in the
+    other group) keeps its own position, so every parameter of `params` lands in the result exactly
+    once (the GEMM then falls back to separate slots: gslot_rows / _adjacent_rows return None)."""
+    present = {id(p) for p in params}
     follow = {}
     members = set()
     for ch in chains:
         ch = [p for p in ch if p is not None]
-        if len(ch) > 1:
-            follow[id(ch[0])] = ch[1:]
-            members.update(id(p) for p in ch[1:])
+        if len(ch) > 1 and id(ch[0]) in present:
+            tail = [q for q in ch[1:] if id(q) in present and id(q) not in members]
+            follow[id(ch[0])] = tail
+            members.update(id(q) for q in tail)
     out = []
     for p in params:
         if id(p) in members:
             continue
         out.append(p)
-        out.extend(q for q in follow.get(id(p), []) if any(q is r for r in params))
+        out.extend(follow.get(id(p), []))
+    assert len(out) == len(params), "chain reorder lost or duplicated a parameter"
     return out
 
 
@@ -147,8 +153,28 @@ class GradBuckets:
         self.fired = set()  # ids of parameters whose gradient arrived this step
         self.unfired = []  # (group, off, k) of the last finished step's parameters without a gradient
         self.main_stream = None  # the stream the step's backward starts from (set by train_step)
+        self.checked = False  # the unused-parameter set was compared across ranks (first step)
         for p in self.owner:
             p.register_post_accumulate_grad_hook(self._hook)
+
+    def _check_unused_consistent(self):
+        """The parameters that got no gradient must be the same on every rank: their slots are
+        zeroed and their values / moments restored per rank while their bucket is still summed, so
+        ranks with different unused sets would silently diverge (the reference's DDP,
+        find_unused_parameters=False, raises instead). One small all-reduce of the per-parameter
+        fired mask (MAX of [fired, -fired]) on the first step; the model's unused set is static."""
+        params = list(self.owner)
+        fired = torch.tensor([1.0 if id(p) in self.fired else 0.0 for p in params],
+                             device=self.buckets[0][0].device)
+        both = torch.cat([fired, -fired])
+        dist.all_reduce(both, op=dist.ReduceOp.MAX)
+        n = len(params)
+        if not torch.equal(both[:n], -both[n:]):  # max(fired) != min(fired) somewhere
+            bad = [i for i in range(n) if float(both[i]) != float(-both[n + i])]
+            raise RuntimeError(f"ranks disagree on which parameters received gradients ({len(bad)} parameters, "
+                               f"e.g. shape {tuple(params[bad[0]].shape)}); DDP with "
+                               "find_unused_parameters=False would fail the same way")
+        self.checked = True
 
     def _add(self, g, members, start):
         end = max(g.slots[p][0] + g.slots[p][1] for p in members)
@@ -167,7 +193,9 @@ class GradBuckets:
         self.pending[bi] -= 1
         if self.pending[bi] == 0:
             self._flush(bi)
-            if collectives_on(self.world):
+            # first step: every bucket is reduced in finish(), after the cross-rank unused-set check
+            # (a collective issued here on one rank would pair with that check on another)
+            if collectives_on(self.world) and self.checked:
                 # the bucket mixes slots written on the main stream, the depth-branch ConvFFN stream
                 # and the weight-gradient stream, and this hook runs on whichever stream autograd
                 # replays the last AccumulateGrad on: wait for all of them before RCCL reads it
@@ -190,6 +218,9 @@ class GradBuckets:
         are left in `unfired`: torch's AdamW skips a parameter whose .grad is None, so FusedAdamW
         restores their value and moments after its flat update."""
         self.unfired = []
+        first = not self.checked
+        if collectives_on(self.world) and first:
+            self._check_unused_consistent()
         for bi, b in enumerate(self.buckets):
             if self.pending[bi] > 0:
                 for p in b[1]:
@@ -199,9 +230,9 @@ class GradBuckets:
                         g.grad[off:off + k].zero_()
                         self.unfired.append((g, off, k))
                 self._flush(bi)
-                if collectives_on(self.world):
-                    join_streams(self.main_stream)
-                    self.handles.append(dist.all_reduce(b[0], async_op=True))
+            if (self.pending[bi] > 0 or first) and collectives_on(self.world):
+                join_streams(self.main_stream)
+                self.handles.append(dist.all_reduce(b[0], async_op=True))
         for h in self.handles:
             h.wait()
         self.handles = []
@@ -264,7 +295,13 @@ class LossScaler:
 
 
 class FusedAdamW:
-    """torch.optim.AdamW semantics over the two group_weight groups (decay wd, no-decay 0)."""
+    """torch.optim.AdamW semantics over the two group_weight groups (decay wd, no-decay 0).
+
+    One step count for every parameter: torch's AdamW keeps a per-parameter 'step' and does not
+    advance it for a parameter without a gradient, whereas here a parameter that was skipped in
+    some steps (its value and moments restored, see GradBuckets.finish) still uses the global count
+    in the bias correction. DFormer's unused parameters never get a gradient, so this only matters
+    for a model whose used set changes between steps."""
 
     def __init__(self, model, lr=6e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, world=1,
                  compute_dtype=torch.float32, bucket_bytes=25 << 20):
@@ -358,12 +395,13 @@ class FusedAdamW:
         defaults = {k: v for k, v in torch.optim.AdamW([torch.zeros(1, requires_grad=True)]).param_groups[0].items()
                     if k != "params"}
         state, groups, idx = {}, [], 0
+        steps = self.step_count  # one read (a device sync with the fp16 scaler), not one per parameter
         for plist, g in zip(self.full_groups, self.groups):
             ids = []
             for p in plist:
-                if p in g.slots and self.step_count > 0:
+                if p in g.slots and steps > 0:
                     off, k = g.slots[p]
-                    state[idx] = {"step": torch.tensor(float(self.step_count)),
+                    state[idx] = {"step": torch.tensor(float(steps)),
                                   "exp_avg": g.m[off:off + k].view_as(p).detach().clone(),
                                   "exp_avg_sq": g.v[off:off + k].view_as(p).detach().clone()}
                 ids.append(idx)

@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 6 (round 3: dfm_gemm_group, dfm_dwconv_bwd, GELU' output modes) */
+int dfm_abi_version(void); /* 7 (round 4: DfmGemmDesc.workspace_bytes + stride / leading-dimension validation) */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -97,6 +97,9 @@ typedef struct DfmGemmDesc {
                     GEMM, computed as a virtual all-ones column of B (batch must be 1) */
   int colsum_accumulate;
   int mul_gelu_grad; /* 1: the multiplier is gelu'(mul[m,n]) (GELU backward fused into a dgrad GEMM) */
+  long workspace_bytes; /* size of the workspace passed with the call; it must be at least
+                           dfm_gemm_workspace_size(d) (for dfm_gemm_group: d[0] carries the size of
+                           the one shared workspace, >= dfm_gemm_group_workspace_size) */
 } DfmGemmDesc;
 
 size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);
@@ -155,30 +158,6 @@ int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const vo
 int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const void* dy,
                    long lddy, const float* w, int add_identity, void* dx, long lddx, int accumulate, float* dw,
                    float* db, void* workspace, dfm_stream_t stream);
-
-/* ---------------------------------------------------------------- fused ConvFFN
- * DFormer.py:48-67 (MLP: fc1 -> pos = DW3x3 + identity -> GELU -> fc2) inside the Block residual
- * DFormer.py:173-179, on NHWC rows of B images of H x W:
- *   fwd: h = xn W1^T + b1 ; hpre = DW3(h) + bpos + h ; f = GELU(hpre) W2^T + b2 ;
- *        out = x + rowscale[b] * ls[c] * f      (xn = LN(x) computed by dfm_layernorm_fwd)
- *        writes out and f (the pre-residual branch, for the layer-scale gradient); the [P, hid]
- *        activations stay on chip.
- *   bwd: given df = dL/df (dfm_residual_bwd), recomputes h / hpre per tile and writes g = GELU(hpre)
- *        and dh = dL/dh ([P, hid], the inputs of the fc2 / fc1 weight-gradient GEMMs), dxn = dL/dxn
- *        [P, C] (for dfm_layernorm_bwd) and dwpos [hid][9], dbpos [hid] (overwritten).
- * w1 [hid][C], w2 [C][hid] in `dtype` (nn.Linear layouts); b1, b2, wpos [hid][9], bpos, ls fp32;
- * rowscale fp32 [B] (DropPath) or NULL. Supported shapes: dfm_convffn_supported (16 <= C <= 64,
- * C % 16 == 0, hid % 32 == 0; bf16, f16 and f32). */
-int dfm_convffn_supported(int dtype, int C, int hid);
-int dfm_convffn_fwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* x,
-                    long ldx, const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
-                    const float* b2, const float* ls, const float* rowscale, void* out, long ldout, void* f,
-                    long ldf, dfm_stream_t stream);
-size_t dfm_convffn_bwd_workspace(int dtype, int B, int H, int W, int C, int hid);
-int dfm_convffn_bwd(int dtype, int B, int H, int W, int C, int hid, const void* xn, long ldxn, const void* df,
-                    long lddf, const void* w1, const float* b1, const float* wpos, const float* bpos,
-                    const void* w2, void* g, long ldg, void* dh, long lddh, void* dxn, long lddxn, float* dwpos,
-                    float* dbpos, void* workspace, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)

@@ -105,6 +105,51 @@ def golden_block(name, model, stage, B, H, W, last=False, drop_prob=0.0, masks=N
          meta=np.array([B, H, W, C, stage, int(last), drop_prob * 1e6]), **extra, **param_grads(blk))
 
 
+def golden_block_bf16_env(name, model, stage, B, H, W, last=False):
+    """The reference Block's OWN bf16 error (float32 weights / inputs under torch.autocast(bfloat16)
+    on CPU) against the fp64 golden `name`, per output: y, y_e, gx, gxe and every parameter gradient,
+    with the statistics the GPU gates use (rel-to-max for full tensors, tests/goldens.py fp_rel_err
+    for fingerprinted ones). tests/test_block_gpu.py gates the HIP bf16 Block at a stated multiple
+    of this envelope (a bf16 gate must be per Block and relative to what bf16 can do)."""
+    g = dict(np.load(os.path.join(OUT, name + ".npz")))
+    C = MODELS[model]["dims"][stage]
+    blk = make_block(model, stage, last)
+    load_weights(blk)
+    blk = blk.float().train()
+    x = torch.from_numpy(gen.normal(name + "/x", (B, H, W, C))).float().requires_grad_()
+    xe = torch.from_numpy(gen.normal(name + "/xe", (B, H, W, C // 2))).float().requires_grad_()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        y, ye = blk(x, xe)
+    loss = (y.float() * torch.from_numpy(gen.normal(name + "/gy", y.shape)).float()).sum()
+    if not last:
+        loss = loss + (ye.float() * torch.from_numpy(gen.normal(name + "/gye", ye.shape)).float()).sum()
+    loss.backward()
+
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+    env = {"env/y": rel(y.detach().double().numpy(), g["y"]), "env/gx": rel(x.grad.double().numpy(), g["gx"])}
+    if not last:
+        env["env/y_e"] = rel(ye.detach().double().numpy(), g["y_e"])
+        env["env/gxe"] = rel(xe.grad.double().numpy(), g["gxe"])
+    for n, p in blk.named_parameters():
+        if p.grad is None:
+            continue
+        a = p.grad.detach().double().numpy()
+        if "grad/" + n in g:
+            b = g["grad/" + n].astype(np.float64)
+            if np.abs(b).max() < 1e-12:  # mathematically zero gradient (fp64 noise): not gated
+                continue
+            env["env/grad/" + n] = rel(a, b)
+        elif "gradfp/" + n in g:
+            env["env/grad/" + n] = _fp_rel_err(gen.fingerprint(a, 256), g["gradfp/" + n])
+    gv = np.array([v for k, v in env.items() if k.startswith("env/grad/")])
+    print(f"  bf16env {name}: y {env['env/y']:.3e} gx {env['env/gx']:.3e} param-grad median {np.median(gv):.3e} "
+          f"max {gv.max():.3e}")
+    save("bf16env_" + name, **{k: np.array(v) for k, v in env.items()})
+
+
 def golden_nmf(name, B, C, H, W, train=True):
     nmf = ham.NMF2D(dict(device="cpu"))
     nmf.train(train)
@@ -407,7 +452,12 @@ def main():
     if want("msf"):
         golden_msf("msf_tiny_ham", "DFormer-Tiny", 2, 50, 70)
         golden_msf("msf_tiny_mlp", "DFormer-Tiny", 1, 45, 61, decoder="MLPDecoder", ncls=37, embed=64)
-    if want("bf16env"):
+    if want("bf16env_block"):
+        for n, mdl, st, B, H, W, last in blocks:
+            if n in ("block_tiny_s1", "block_base_s0", "block_base_s1", "block_base_s2", "block_base_s3",
+                     "block_base_s3_last", "block_large_s2"):
+                golden_block_bf16_env(n, mdl, st, B, H, W, last)
+    if want("bf16env") and not which == ["bf16env_block"]:
         golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
         golden_bf16_env("e2e_base_small", "DFormer-Base", 2, 64, 80)
         golden_bf16_env("e2e_large_mlp_small", "DFormer-Large", 1, 53, 73, decoder="MLPDecoder", ncls=37)

@@ -42,7 +42,7 @@ def test_binding_signatures_match_header():
 
 def test_abi_version_and_error_path():
     from dformer_amd import _lib
-    assert _lib.lib.dfm_abi_version() == 6
+    assert _lib.lib.dfm_abi_version() == 7
     # argument validation fails before touching the GPU
     st = _lib.lib.dfm_layernorm_fwd(0, 10, 100000, None, 0, None, None, 1e-6, None, 0, None, None, None)
     assert st == -1
@@ -68,3 +68,27 @@ def test_gemm_desc_layout_matches_c_struct(tmp_path):
     vals = [int(v) for v in subprocess.run([str(tmp_path / "t")], capture_output=True, text=True).stdout.split()]
     assert vals[0] == ctypes.sizeof(_lib.GemmDesc)
     assert vals[1:] == [getattr(_lib.GemmDesc, n).offset for n in names]
+
+
+@pytest.mark.parametrize("bad", [
+    dict(lda=800),                      # k-contiguous A rows of K = 896 elements in an 800-element pitch
+    dict(ldb=512),                      # same for B
+    dict(ldc=500),                      # output rows narrower than N
+    dict(stride_a=4800 * 896 - 1),      # consecutive batch matrices of A overlap
+    dict(stride_b=100),
+    dict(stride_c=0),                   # every batch writing one output
+    dict(split_k=4, workspace_bytes=1024),  # split-K partials need 4 * 16 * 4800 * 512 * 4 bytes
+])
+def test_gemm_validation_rejects_bad_descriptors(bad):
+    """dfm_gemm validates leading dimensions, batch strides and the workspace size before any launch
+    (the NMF backward's input-gradient descriptor, ham_head.py:120-145 / decoders.py gx, perturbed)."""
+    from dformer_amd import _lib
+    d = dict(M=4800, N=512, K=896, batch=16, a_kcontig=1, b_kcontig=1, lda=896, ldb=896, ldc=512,
+             stride_a=4800 * 896, stride_b=512 * 896, stride_c=4800 * 512, alpha=1.0, beta=0.0, rows_per_scale=1,
+             workspace_bytes=0)
+    d.update(bad)
+    desc = _lib.GemmDesc(**d)
+    fake = ctypes.c_void_p(1 << 20)  # never dereferenced: validation fails first
+    st = _lib.lib.dfm_gemm(_lib.BF16, desc, fake, fake, fake, fake if "split_k" in bad else None, None)
+    assert st == -1, _lib.lib.dfm_last_error()
+    assert _lib.lib.dfm_last_error().startswith(b"dfm_gemm: ")

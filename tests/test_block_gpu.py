@@ -73,13 +73,45 @@ def test_block_fp32_vs_reference_goldens(name):
     check_param_grads(g, grads, tol)
 
 
+# bf16 gates relative to the reference's OWN bf16 error on the same Block (tests/golden/bf16env_block_*,
+# oracle/make_goldens.py golden_block_bf16_env: reference float32 under torch.autocast(bfloat16) vs
+# its fp64 golden, per output and per parameter gradient). The HIP path stores every activation in
+# bf16 (autocast keeps LN / GELU / elementwise results in fp32), so each error may be up to
+# BF16_ENV_MULT times the envelope, the envelope floored at one bf16 rounding (2^-8): gates that
+# move with what bf16 can do on that tensor instead of one flat number.
+BF16_ENV_MULT = 4.0
+BF16_FLOOR = 2.0 ** -8
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["block_tiny_s1", "block_base_s0", "block_base_s1", "block_base_s2",
-                                  "block_base_s3", "block_large_s2"])
+                                  "block_base_s3", "block_base_s3_last", "block_large_s2"])
 def test_block_bf16_vs_reference_goldens(name):
-    """bf16 gate is per Block on rel-to-max: forward 1e-2; input grads 2e-2."""
+    """bf16 per Block: forward also within 1e-2 rel-to-max; forward, input gradients and
+    EVERY parameter gradient within BF16_ENV_MULT x the reference's own bf16 envelope."""
+    from goldens import fp_rel_err
     g, blk, x, xe, y, ye, last = run_block(name, torch.bfloat16)
-    assert rel_err(y.float().cpu(), g["y"]) < 1e-2
-    assert rel_err(ye.float().cpu(), g["y_e"]) < 1e-2
-    assert rel_err(x.grad.float().cpu(), g["gx"]) < 2e-2
-    assert rel_err(xe.grad.float().cpu(), g["gxe"]) < 2e-2
+    env = load("bf16env_" + name)
+
+    def gate(key):
+        return BF16_ENV_MULT * max(float(env["env/" + key]), BF16_FLOOR)
+
+    errs = {"y": rel_err(y.float().cpu(), g["y"]), "gx": rel_err(x.grad.float().cpu(), g["gx"])}
+    if not last:
+        errs["y_e"] = rel_err(ye.float().cpu(), g["y_e"])
+        errs["gxe"] = rel_err(xe.grad.float().cpu(), g["gxe"])
+    assert errs["y"] < 1e-2 and errs.get("y_e", 0.0) < 1e-2, errs
+    grads = {k: p.grad for k, p in blk.named_parameters() if p.grad is not None}
+    for k in env:
+        if k.startswith("env/grad/"):
+            n = k[len("env/grad/"):]
+            a = grads[n].detach().double().cpu()
+            if "grad/" + n in g:
+                errs["grad/" + n] = rel_err(a, g["grad/" + n])
+            else:
+                errs["grad/" + n] = fp_rel_err(gen.fingerprint(a.numpy(), 256), g["gradfp/" + n])
+    ratios = {k: v / max(float(env["env/" + k]), BF16_FLOOR) for k, v in errs.items()}
+    worst = max(ratios, key=ratios.get)
+    print(f"{name}: worst {worst} err {errs[worst]:.3e} = {ratios[worst]:.2f} x envelope")
+    bad = {k: (errs[k], gate(k)) for k in errs if errs[k] >= gate(k)}
+    assert not bad, bad

@@ -236,3 +236,43 @@ def test_syncbn_merge_matches_full_batch():
     assert torch.allclose(var, x.var(0, unbiased=False), rtol=1e-4, atol=1e-6)
     one = _bn_merge_model(parts[0][None], torch.tensor([700.0]))
     assert torch.equal(one, parts[0])
+
+
+def _unused_mismatch_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dformer_amd.functional import clear_grad_slots
+        from dformer_amd.train import GradBuckets, _FlatGroup, group_weight
+        torch.manual_seed(0)
+        net = _Net()
+        decay, no_decay = group_weight(net)
+        groups = [_FlatGroup(decay, 0.01, "cpu", torch.float32), _FlatGroup(no_decay, 0.0, "cpu", torch.float32)]
+        buckets = GradBuckets(groups, world, 1 << 30)
+        x = torch.randn(4, 3, 6, 7)
+        net(x, use_extra=(rank == 0)).square().mean().backward()  # rank 1 leaves `extra` unused
+        try:
+            buckets.finish()
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, "raised" if "disagree" in str(e) else str(e)))
+        clear_grad_slots()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unused_parameter_sets_must_match_across_ranks():
+    """Ranks whose unused-parameter sets differ would diverge (each rank restores its own unused
+    parameters while the bucket is summed): GradBuckets raises on every rank, as DDP would."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unused_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: "raised", 1: "raised"}, res

@@ -7,7 +7,11 @@ SyncBatchNorm, utils/engine/engine.py:53-66).
 With every label valid both ranks hold the same number of pixels, so DDP's average of the two
 half-batch gradients is exactly the whole-batch gradient and SyncBN over the two ranks is BatchNorm
 over the whole batch (the stems' plain BatchNorm2d layers, per-rank in the reference as well, run on
-their running statistics): everything must agree to fp32 rounding (the step runs in float32)."""
+their running statistics): everything must agree to fp32 rounding (the step runs in float32).
+
+Two sizes: DFormer-Tiny at 4 x 96 x 128, and BASELINE config 4's own model and image size,
+DFormer-Base at 480 x 640 (2 ranks x 4 images against 1 rank x 8; config 4 runs 16 per GPU on 8 GPUs
+over RCCL, which a one-GPU box cannot host: RCCL at N > 1 stays unmeasured here)."""
 import os
 import socket
 import sys
@@ -20,7 +24,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-BATCH, H, W = 4, 96, 128
+CASES = {"tiny": ("DFormer-Tiny", 4, 96, 128), "base480": ("DFormer-Base", 8, 480, 640)}
 
 
 def _free_port():
@@ -29,15 +33,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(rank, world):
-    """One train step of DFormer-Tiny + ham on this rank's share of a fixed batch; returns the flat
-    gradients divided by world (the buffers hold the SUM over ranks), the BN running statistics and
-    the all-reduced loss."""
+def _run(rank, world, case):
+    """One train step of the case's model + ham on this rank's share of a fixed batch; returns the
+    flat gradients divided by world (the buffers hold the SUM over ranks), the BN running statistics
+    and the all-reduced loss."""
     import bench
+    backbone, BATCH, H, W = CASES[case]
     from dformer_amd.segmentor import EncoderDecoder
     from dformer_amd.train import FusedAdamW, train_step
     dev = torch.device("cuda", 0)
-    cfg = bench.make_cfg("DFormer-Tiny", "ham")
+    cfg = bench.make_cfg(backbone, "ham")
     cfg["drop_path_rate"] = 0.0
     torch.manual_seed(3)
     model = EncoderDecoder(cfg=cfg, syncbn=world > 1)
@@ -78,14 +83,14 @@ def _run(rank, world):
     return grads, bn_grads, running, float(loss)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, case):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        grads, bn_grads, running, loss = _run(rank, world)
+        grads, bn_grads, running, loss = _run(rank, world, case)
         # numpy copies travel by value: a torch CPU tensor would be shared through a file descriptor
         # that vanishes when this process exits before the parent unpickles it
         q.put((rank, ([g.numpy() for g in grads], {k: v.numpy() for k, v in bn_grads.items()},
@@ -100,18 +105,22 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
 
 
-def test_two_ranks_syncbn_ddp_equal_whole_batch():
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("case", ["tiny", "base480"])
+def test_two_ranks_syncbn_ddp_equal_whole_batch(case):
+    """The attention-backward side stream and the bucket hooks' join_streams are active (eager step)."""
     if not torch.cuda.is_available():
         pytest.skip("needs an MI355X")
     import torch.multiprocessing as mp
-    ref_grads, ref_bn, ref_run, ref_loss = _run(0, 1)
+    ref_grads, ref_bn, ref_run, ref_loss = _run(0, 1, case)
+    torch.cuda.empty_cache()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, case)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (out, err)) for r, out, err in (q.get(timeout=240) for _ in procs))
+    res = dict((r, (out, err)) for r, out, err in (q.get(timeout=400) for _ in procs))
     for p in procs:
         p.join(timeout=60)
     for r in range(2):

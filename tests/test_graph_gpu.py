@@ -14,9 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def _gpu():
     if not torch.cuda.is_available():
         pytest.skip("needs an MI355X")
-    # the library convolutions of the stem / downsample layers (MIOpen) pick deterministic
-    # algorithms: every kernel of the step is then run-to-run reproducible and the graphed and
-    # eager steps must agree bit for bit
+    # every kernel of the step is a libdformer_hip kernel with fixed-order reductions (no vendor
+    # convolutions since round 3), so the step is run-to-run reproducible and the graphed and eager
+    # steps must agree bit for bit; the cudnn flags are pinned anyway for any torch op
     det, bm = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
     yield

@@ -82,3 +82,40 @@ def test_warmup_poly_lr():
     lrs = [s.get_lr(i) for i in range(10, 1000)]
     assert all(a > b for a, b in zip(lrs, lrs[1:])) and lrs[-1] > 0.0
     assert s.get_lr(1000) == 0.0
+
+
+def test_frozen_chain_head_keeps_members_in_their_group():
+    """A chain member (q_cut / l, proj_e, BN weight) whose chain head is frozen must still get a
+    flat slot: FusedAdamW would otherwise leave it ungrouped and silently never update it."""
+    import bench
+    from dformer_amd.functional import clear_grad_slots
+    from dformer_amd.segmentor import EncoderDecoder
+    from dformer_amd.train import FusedAdamW, _chain_order, group_weight
+
+    torch.manual_seed(0)
+    model = EncoderDecoder(cfg=bench.make_cfg("DFormer-Tiny", "ham"))
+    attn = model.encoder_backbone.stages[1][0].attn
+    attn.q.weight.requires_grad_(False)        # head of q | q_cut | l (weights)
+    attn.proj.bias.requires_grad_(False)       # head of proj | proj_e (biases)
+    bn = model.decode_head.squeeze.bn
+    bn.bias.requires_grad_(False)              # head of bias | weight
+    decay, no_decay = group_weight(model)
+    opt = FusedAdamW(model)
+    try:
+        grouped = {id(p) for g in opt.groups for p in g.params}
+        for p in decay + no_decay:
+            assert (id(p) in grouped) == p.requires_grad
+        for p in (attn.q_cut.weight, attn.l.weight, attn.proj_e.bias, bn.weight):
+            assert id(p) in grouped and all(p is not q for q in opt.ungrouped)
+        # every parameter exactly once; untouched chains stay adjacent
+        for g in opt.groups:
+            assert len({id(p) for p in g.params}) == len(g.params)
+        other = model.encoder_backbone.stages[1][1].attn
+        g0 = opt.groups[0]
+        oq, oqc, ol = (g0.slots[p][0] for p in (other.q.weight, other.q_cut.weight, other.l.weight))
+        assert oqc == oq + other.q.weight.numel() and ol == oqc + other.q_cut.weight.numel()
+    finally:
+        clear_grad_slots()
+    a, b, c, d = (torch.zeros(1, requires_grad=True) for _ in range(4))
+    assert _chain_order([b, c, d], [[a, b, c]]) == [b, c, d]   # head absent: members keep their place
+    assert _chain_order([c, d, a], [[a, b, c]]) == [d, a, c]   # head present, b absent: c follows a

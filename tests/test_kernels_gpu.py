@@ -29,6 +29,10 @@ def rel(a, b):
 
 
 TOL = {torch.float32: 2e-5, torch.bfloat16: 2e-2, torch.float16: 3e-3}
+# GEMM gates: rel-to-max on identical (already rounded) 16-bit inputs with fp32 accumulation, so the
+# only error left is the rounding of the 16-bit output (2^-9 relative for bf16, 2^-11 for fp16) plus
+# accumulation order — about two output roundings, not percent-level drift
+GTOL = {torch.float32: 2e-5, torch.bfloat16: 5e-3, torch.float16: 1.5e-3}
 DTYPES = [torch.float32, torch.bfloat16, torch.float16]
 
 
@@ -42,16 +46,16 @@ def test_gemm_layouts(dt, M, N, Kd):
     b = torch.randn(N, device=DEV)
     y = k.linear(x, w, b)
     ref = x.float() @ w.float().t() + b
-    assert rel(y.float(), ref) < TOL[dt]
+    assert rel(y.float(), ref) < GTOL[dt]
     dy = torch.randn(M, N, device=DEV).to(dt)
     dx = k.linear_dgrad(dy, w)
-    assert rel(dx.float(), dy.float() @ w.float()) < TOL[dt]
+    assert rel(dx.float(), dy.float() @ w.float()) < GTOL[dt]
     dw = k.linear_wgrad(dy, x)
     assert dw.dtype == torch.float32
-    assert rel(dw, dy.float().t() @ x.float()) < TOL[dt]
+    assert rel(dw, dy.float().t() @ x.float()) < GTOL[dt]
     dw2, db = k.linear_wgrad(dy, x, bias_grad=True)
-    assert rel(dw2, dy.float().t() @ x.float()) < TOL[dt]
-    assert rel(db, dy.float().sum(0)) < TOL[dt]
+    assert rel(dw2, dy.float().t() @ x.float()) < GTOL[dt]
+    assert rel(db, dy.float().sum(0)) < GTOL[dt]
 
 
 @pytest.mark.parametrize("M,N,Kd", [(140000, 64, 64), (131072 + 77, 256, 128), (140001, 160, 64),
@@ -69,14 +73,14 @@ def test_gemm_stream_large_m(M, N, Kd):
     pre = torch.empty(M, N, device=DEV, dtype=dt)
     y = k.linear(x, w, b, preact=pre, res=res, colscale=ls)
     f = x.float() @ w.float().t() + b
-    assert rel(pre.float(), f) < TOL[dt]
-    assert rel(y.float(), res.float() + ls * f) < TOL[dt]
+    assert rel(pre.float(), f) < GTOL[dt]
+    assert rel(y.float(), res.float() + ls * f) < GTOL[dt]
     dy = torch.randn(M, N, device=DEV).to(dt)
     h = torch.randn(M, Kd, device=DEV).to(dt)
     dx = k.linear_dgrad(dy, w, gelu_grad_of=h)
     hf = h.float()
     gg = 0.5 * (1 + torch.erf(hf / math.sqrt(2))) + hf * torch.exp(-0.5 * hf * hf) / math.sqrt(2 * math.pi)
-    assert rel(dx.float(), (dy.float() @ w.float()) * gg) < TOL[dt]
+    assert rel(dx.float(), (dy.float() @ w.float()) * gg) < GTOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -86,11 +90,11 @@ def test_gemm_splitk_and_strided(dt):
     x = big[:, 16:80]  # strided view, ld=96
     dy = torch.randn(20000, 48, device=DEV).to(dt)
     dw = k.linear_wgrad(dy, x)
-    assert rel(dw, dy.float().t() @ x.float()) < TOL[dt]
+    assert rel(dw, dy.float().t() @ x.float()) < GTOL[dt]
     acc = torch.randn(48, 64, device=DEV)
     ref = acc + dy.float().t() @ x.float()
     k.linear_wgrad(dy, x, out=acc, accumulate=True)
-    assert rel(acc, ref) < TOL[dt]
+    assert rel(acc, ref) < GTOL[dt]
 
 
 @pytest.mark.parametrize("M,N,Kd", [(1000, 128, 256), (777, 200, 1000), (4800, 512, 2048), (130, 40, 136),
@@ -109,17 +113,17 @@ def test_gemm_lds_dma_paths(M, N, Kd):
     pre = torch.empty(M, N, device=DEV, dtype=dt)
     y = k.linear(x, w, b, preact=pre, res=res, colscale=ls)
     f = x.float() @ w.float().t() + b
-    assert rel(pre.float(), f) < TOL[dt]
-    assert rel(y.float(), res.float() + ls * f) < TOL[dt]
+    assert rel(pre.float(), f) < GTOL[dt]
+    assert rel(y.float(), res.float() + ls * f) < GTOL[dt]
     dy = torch.randn(M, Kd, device=DEV).to(dt)
     wd = (torch.randn(Kd, N, device=DEV) / Kd ** 0.5).to(dt)   # dx[M, N] = dy[M, Kd] @ wd[Kd, N]
     dx = k.linear_dgrad(dy, wd)
-    assert rel(dx.float(), dy.float() @ wd.float()) < TOL[dt]
+    assert rel(dx.float(), dy.float() @ wd.float()) < GTOL[dt]
     g = torch.randn(Kd, M, device=DEV).to(dt)     # wgrad over Kd "pixels": dW[M, N] = g^T x2
     x2 = torch.randn(Kd, N, device=DEV).to(dt)
     dw, db = k.linear_wgrad(g, x2, bias_grad=True)
-    assert rel(dw, g.float().t() @ x2.float()) < TOL[dt]
-    assert rel(db, g.float().sum(0)) < TOL[dt]
+    assert rel(dw, g.float().t() @ x2.float()) < GTOL[dt]
+    assert rel(db, g.float().sum(0)) < GTOL[dt]
     dw2 = k.linear_wgrad(g, x2)
     assert torch.equal(dw2, dw)
 
@@ -134,15 +138,15 @@ def test_gemm_epilogues(dt):
     pre = torch.empty(M, N, device=DEV, dtype=dt)
     y = k.linear(x, w, b, act=1, preact=pre)
     lin = x.float() @ w.float().t() + b
-    assert rel(pre.float(), lin) < TOL[dt]
-    assert rel(y.float(), F.gelu(lin)) < TOL[dt]
+    assert rel(pre.float(), lin) < GTOL[dt]
+    assert rel(y.float(), F.gelu(lin)) < GTOL[dt]
     mul = torch.randn(M, N, device=DEV).to(dt)
     res = torch.randn(M, N, device=DEV).to(dt)
     cs = torch.rand(N, device=DEV)
     rs = torch.rand(3, device=DEV)
     y = k.linear(x, w, b, mul=mul, res=res, colscale=cs, rowscale=rs, rows_per_scale=171)
     rsx = rs.repeat_interleave(171)[:M, None]
-    assert rel(y.float(), res.float() + cs * rsx * (lin * mul.float())) < TOL[dt]
+    assert rel(y.float(), res.float() + cs * rsx * (lin * mul.float())) < GTOL[dt]
 
 
 @pytest.mark.parametrize("dt", [torch.float32])
@@ -150,16 +154,16 @@ def test_bmm_layouts(dt):
     k = K()
     a = torch.randn(3, 70, 40, device=DEV, dtype=dt)
     b = torch.randn(3, 40, 24, device=DEV, dtype=dt)
-    assert rel(k.bmm(a, b), a @ b) < TOL[dt]
+    assert rel(k.bmm(a, b), a @ b) < GTOL[dt]
     at = a.transpose(1, 2).contiguous()
-    assert rel(k.bmm(at, b, a_t=True), a @ b) < TOL[dt]
+    assert rel(k.bmm(at, b, a_t=True), a @ b) < GTOL[dt]
     bt = b.transpose(1, 2).contiguous()
-    assert rel(k.bmm(a, bt, b_t=True), a @ b) < TOL[dt]
-    assert rel(k.bmm(at, bt, a_t=True, b_t=True), a @ b) < TOL[dt]
+    assert rel(k.bmm(a, bt, b_t=True), a @ b) < GTOL[dt]
+    assert rel(k.bmm(at, bt, a_t=True, b_t=True), a @ b) < GTOL[dt]
     # odd N (not a multiple of the vector width): NMF at 530x730 (N = 67*92)
     x = torch.rand(2, 64, 6164, device=DEV)
     c = torch.rand(2, 6164, 32, device=DEV)
-    assert rel(k.bmm(x, c), x @ c) < TOL[dt]
+    assert rel(k.bmm(x, c), x @ c) < GTOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -328,7 +332,7 @@ def test_gemm_act3_gelu_grad_preact(dt):
     assert rel(y3.float(), y1.float()) < 1e-6  # the same GELU (contraction may differ in the last bit)
     p = pre1.float().requires_grad_()
     F.gelu(p).sum().backward()
-    assert rel(pre3.float(), p.grad) < TOL[dt] * 2
+    assert rel(pre3.float(), p.grad) < GTOL[dt] * 2
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -643,3 +647,25 @@ def test_wgrad_group(dt, rows):
         sw = single[0] if bias else single
         if i != 2:
             assert rel(dw, sw) < (1e-5 if dt == torch.float32 else TOL[dt]), i
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_nmf_backward_input_gradient_descriptor(dt):
+    """The exact descriptor of the NMF backward's input gradient (decoders.py NMF2DFn.backward:
+    gx = Pc Qc^T, M = N_pix 4800, N = D 512, K = T*R 896, batch 16, both operands k-contiguous), the
+    call a round-3 profiling run faulted next to (hipErrorIllegalAddress): through dfm_gemm vs torch
+    fp32, synchronised, plus a re-run into a poisoned output (every element rewritten)."""
+    k = K()
+    B, N, D, KR = 16, 4800, 512, 896
+    pc = torch.randn(B, N, KR, device=DEV).to(dt)
+    qc = torch.randn(B, D, KR, device=DEV).to(dt)
+    gx = k.bmm(pc, qc, b_t=True)
+    torch.cuda.synchronize()
+    ref = torch.bmm(pc.float(), qc.float().transpose(1, 2))
+    assert gx.shape == (B, N, D) and gx.dtype == dt
+    assert rel(gx.float(), ref) < GTOL[dt]
+    out = torch.full_like(gx, float("nan"))
+    k.bmm(pc, qc, b_t=True, out=out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    assert torch.equal(out, gx)  # deterministic

@@ -52,6 +52,7 @@ def run(d):
                          b.shape[1] * b.shape[2], M * N, 1.0, 0.0, 0, None, 0, None, 0, None, 0, None, 0,
                          None, None, 1, 0, 0, None, 0, 0)
     ws = K._ws(_lib.lib.dfm_gemm_workspace_size(desc), dev)
+    desc.workspace_bytes = ws.numel() if ws is not None else 0
     s = _lib.stream()
 
     def mine():

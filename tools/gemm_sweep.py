@@ -89,6 +89,7 @@ def replay(d, splits, iters=20):
                          ptrs["colscale"], ptrs["rowscale"], d["rows_per_scale"], splits, d["act_col0"],
                          ptrs["colsum"], d["colsum_accumulate"], d["mul_gelu_grad"])
     ws = K._ws(_lib.lib.dfm_gemm_workspace_size(desc), dev)
+    desc.workspace_bytes = ws.numel() if ws is not None else 0
     s = _lib.stream()
 
     def launch():
