@@ -52,7 +52,7 @@ struct GemmArgs {
   int tiles_n;     // output column tiles (grid.x enumerates tiles_m * tiles_n)
   int tiles_m;     // output row tiles (glds kernel)
   int n_fast;      // glds kernel: consecutive (XCD-local) blocks walk column tiles of one row tile
-  int xcd_map;     // gemm_kernel: XCD-aware block renumbering (DFM_GEMM_XCD=0 disables)
+  int xcd_map;     // gemm_kernel: XCD-aware block renumbering (always on)
 };
 
 

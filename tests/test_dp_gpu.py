@@ -131,10 +131,13 @@ def test_two_ranks_syncbn_ddp_equal_whole_batch(case):
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
     for a, b in zip(grads, ref_grads):
         assert _rel(a, b) < 1e-4, _rel(a, b)
-    # the BN affine gradients are local statistics averaged by DDP, not all-reduced twice
+    # the BN affine gradients are local statistics averaged by DDP, not all-reduced twice. Per layer
+    # the gate is SURVEY's fp32 1e-3: at 480 x 640 one SyncBN layer sums dy * xhat over 153,600 rows
+    # with heavy cancellation, and the two-rank order of that fp32 sum differs from the one-rank
+    # order (measured 3.9e-4 on downsample_layers.1.0; a double-counted all-reduce would be 1.0)
     assert len(bn_grads) >= 4
     for k, v in bn_grads.items():
-        assert _rel(v, ref_bn[k]) < 1e-4, (k, _rel(v, ref_bn[k]))
+        assert _rel(v, ref_bn[k]) < 1e-3, (k, _rel(v, ref_bn[k]))
     for k, v in running.items():
         if v.dtype.is_floating_point:
             assert _rel(v, ref_run[k]) < 1e-5, (k, _rel(v, ref_run[k]))

@@ -669,3 +669,63 @@ def test_gemm_nmf_backward_input_gradient_descriptor(dt):
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
     assert torch.equal(out, gx)  # deterministic
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,Kd,ldx", [(19200, 256, 256, 256), (4800 + 37, 200, 1024, 1032), (130, 64, 64, 64),
+                                        (307200 // 16, 512, 64, 64), (777, 1152, 128, 136)])
+def test_gemm_fused_epilogues_step_shapes(dt, M, N, Kd, ldx):
+    """Forward and input-gradient GEMMs at step-like shapes (whichever kernel the routing picks) with
+    every fused epilogue the Block uses: bias + GELU with GELU' stored from a column offset (act 3),
+    the multiplier, the residual with column / row scales, beta accumulation, the GELU'-multiplier
+    of an input gradient; ragged M, N % 64 != 0, strided A, one-slice (K = 64) tiles."""
+    k = K()
+    tol = GTOL[dt]
+    xb = torch.randn(M, ldx, device=DEV).to(dt)
+    x = xb[:, :Kd]
+    w = (torch.randn(N, Kd, device=DEV) / Kd ** 0.5).to(dt)
+    b = torch.randn(N, device=DEV)
+    lin = x.float() @ w.float().t() + b
+    # act 3 from column c0: GELU(v) out, GELU'(v) in preact[:, :N - c0]
+    c0 = (N // 2) // 8 * 8
+    pre = torch.empty(M, N - c0, device=DEV, dtype=dt)
+    y = k.linear(x, w, b, act=3, preact=pre, act_col0=c0)
+    v = lin[:, c0:]
+    cdf = 0.5 * (1 + torch.erf(v / math.sqrt(2)))
+    pdf = torch.exp(-0.5 * v * v) / math.sqrt(2 * math.pi)
+    assert rel(y[:, :c0].float(), lin[:, :c0]) < tol
+    assert rel(y[:, c0:].float(), v * cdf) < tol
+    assert rel(pre.float(), cdf + v * pdf) < 2 * tol
+    # multiplier with preact (the conv-modulation q * a)
+    mul = torch.randn(M, N, device=DEV).to(dt)
+    pre2 = torch.empty(M, N, device=DEV, dtype=dt)
+    y = k.linear(x, w, b, mul=mul, preact=pre2)
+    assert rel(pre2.float(), lin) < tol
+    assert rel(y.float(), lin * mul.float()) < tol
+    # residual + layer scale + per-image row scale (Block residual / DropPath epilogue)
+    res = torch.randn(M, N, device=DEV).to(dt)
+    cs = torch.rand(N, device=DEV)
+    rps = max(1, M // 5)
+    rs = torch.rand((M + rps - 1) // rps, device=DEV)
+    y = k.linear(x, w, b, res=res, colscale=cs, rowscale=rs, rows_per_scale=rps)
+    rsx = rs.repeat_interleave(rps)[:M, None]
+    assert rel(y.float(), res.float() + cs * rsx * lin) < tol
+    # beta accumulate into the output
+    acc = torch.randn(M, N, device=DEV).to(dt)
+    want = acc.float() + lin
+    k.linear(x, w, b, out=acc, beta=1.0)
+    assert rel(acc.float(), want) < tol
+    # input gradient: dx[M, N] = dy[M, Kd] @ wd[Kd, N], plain / GELU'-multiplier / accumulate
+    dy = xb[:, :Kd]
+    wd = (torch.randn(Kd, N, device=DEV) / Kd ** 0.5).to(dt)
+    ref = dy.float() @ wd.float()
+    assert rel(k.linear_dgrad(dy, wd).float(), ref) < tol
+    h = torch.randn(M, N, device=DEV).to(dt)
+    hf = h.float()
+    gg = 0.5 * (1 + torch.erf(hf / math.sqrt(2))) + hf * torch.exp(-0.5 * hf * hf) / math.sqrt(2 * math.pi)
+    assert rel(k.linear_dgrad(dy, wd, gelu_grad_of=h).float(), ref * gg) < tol
+    assert rel(k.linear_dgrad(dy, wd, mul=h).float(), ref * hf) < tol
+    dx = torch.randn(M, N, device=DEV).to(dt)
+    want = dx.float() + ref
+    k.linear_dgrad(dy, wd, out=dx, accumulate=True)
+    assert rel(dx.float(), want) < tol
