@@ -1189,6 +1189,8 @@ int choose_splits(const DfmGemmDesc* d, int elem_bytes) {
   return p;
 }
 
+#include "gemm_wide.h"
+
 template <typename T>
 bool al16(const void* p, long ld) {
   return p == nullptr || (((uintptr_t)p % 16 == 0) && (ld % 8 == 0));
@@ -1233,6 +1235,13 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
     a.stream = sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb &&
                d->K % BKsel == 0 && d->K / BKsel <= 8 && tiles >= 1024;
+  }
+  // tall short-K GEMMs with more than one 128-column slice (gemm_wide.h): measured per shape on the
+  // DFormer-B step's census (profiles/r04_wide_gemm_ab.txt) it wins from 65,536 rows and N >= 144
+  // (stage-0 fc1 104 vs 138 us, stage-1 fc2 input gradient x GELU' 106 vs 124 us) and loses on
+  // narrower outputs (a 128-column slice half empty) and on the 19,200-row stage-2 shapes
+  if constexpr (sizeof(T) == 2) {
+    if (wide_eligible<T>(a, d)) return wide_launch<T>(a, d, s);
   }
   // LDS-DMA ring kernel: bf16 with a k-contiguous A (forward, dgrad) and >= 2 whole k-slices. Routing
   // fitted on the DFormer-B step's GEMM census (tools/gemm_sweep.py --replay): it wins on the forward
