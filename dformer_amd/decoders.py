@@ -499,20 +499,16 @@ class DecoderHead(nn.Module):
 
     def forward(self, inputs):
         B = inputs[0].shape[0]
-        embs, hw = [], []
-        for i in (3, 2, 1, 0):
+        lvl, hw = [], []
+        for i in range(4):  # c1 (finest, the output resolution) .. c4
             r, (b, h, w) = _nhwc_rows(inputs[i])
             lin = getattr(self, f"linear_c{i + 1}").proj
-            embs.append(LinearActFn.apply(r, lin.weight, lin.bias, 0, False))
+            lvl += [r, lin.weight, lin.bias]
             hw.append((h, w))
-        H, W = hw[-1]
-        order = [3, 0, 1, 2]  # resize target = c1 size: put c1 first for ResizeCatFn, then restore order
-        cat = ResizeCatFn.apply(B, [hw[3], hw[0], hw[1], hw[2]], embs[3], embs[0], embs[1], embs[2])
+        H, W = hw[0]
         E = self.embed_dim
-        # channel order of the reference cat is [_c4, _c3, _c2, _c1]: permute the fuse weight columns
-        x = FuseBNReLUFn.apply(cat, self.linear_fuse[0].weight, self.linear_fuse[0].bias,
-                               self.linear_fuse[1].weight, self.linear_fuse[1].bias, self.linear_fuse[1], E,
-                               self.syncbn)
+        fuse, bn = self.linear_fuse[0], self.linear_fuse[1]
+        x = MLPFoldFn.apply(B, hw, E, bn, self.syncbn, fuse.weight, fuse.bias, bn.weight, bn.bias, *lvl)
         scale = None
         if self.training and self.dropout_ratio > 0:
             keep = 1.0 - self.dropout_ratio
@@ -520,44 +516,113 @@ class DecoderHead(nn.Module):
                 (torch.rand(B, E, device=x.device) < keep)
             scale = mask.to(device=x.device, dtype=torch.float32) / keep
         logits = ChannelDropoutLinearFn.apply(x, scale, B, self.linear_pred.weight, self.linear_pred.bias)
-        del order
         return logits.view(B, H, W, self.num_classes).permute(0, 3, 1, 2)
 
 
-class FuseBNReLUFn(torch.autograd.Function):
-    """linear_fuse: 1x1 conv(4E->E, bias) + BN + ReLU over cat rows ordered [c1 | c4 | c3 | c2];
-    the reference concatenates [c4 | c3 | c2 | c1] (MLPDecoder.py:77), so the weight's column blocks
-    are permuted accordingly (the conv bias cancels in train-mode BN but is kept for parity)."""
+def _mm32(a, b, out, a_t=False, b_t=False, beta=0.0):
+    """out (+)= op(a) @ op(b) for float32 2-D views (weight algebra of the folded decoder)."""
+    M = a.shape[1] if a_t else a.shape[0]
+    Kd = a.shape[0] if a_t else a.shape[1]
+    N = b.shape[0] if b_t else b.shape[1]
+    return K.gemm(a, b, M=M, N=N, K=Kd, a_kcontig=not a_t, b_kcontig=b_t, lda=K.ld(a), ldb=K.ld(b), out=out,
+                  ldc=K.ld(out), beta=beta)
+
+
+class MLPFoldFn(torch.autograd.Function):
+    """DecoderHead's linear_c1..c4 + bilinear resize + cat + linear_fuse + BN + ReLU
+    (MLPDecoder.py:59-81), folded: bilinear upsampling (align_corners=False, weights
+    summing to one) commutes with 1x1 channel mixing, so
+
+        W_f cat[up(L_4 c_4 + b_4), .., L_1 c_1 + b_1] + b_f = sum_i up((F_i L_i) c_i) + (b_f + sum_i F_i b_i)
+
+    with F_i the column block of W_f that the reference's cat order [c4 | c3 | c2 | c1] gives level i.
+    Each level's product W'_i = F_i L_i runs at that level's own resolution with K = C_i, instead of
+    a K = 4E GEMM over the concatenated 1/4-resolution map (config 5: 51 GF per image). Gradients of
+    the original parameters: G_i = up_i^T(dy0), dW'_i = G_i^T c_i, dc_i = G_i W'_i, dL_i = F_i^T dW'_i,
+    dF_i = dW'_i L_i^T + (sum dy0) b_i^T, db_i = F_i^T sum dy0, db_f = sum dy0.
+    lvl = (rows_1, L_1, b_1, .., rows_4, L_4, b_4), level 1 the finest."""
 
     @staticmethod
-    def forward(ctx, cat, w, b, gamma, beta, bn, E, sync):
-        dt = cat.dtype
-        w2 = w.detach().reshape(E, 4 * E)
-        wperm = torch.cat([w2[:, 3 * E:], w2[:, :3 * E]], 1).contiguous()
-        Wc = K.cast(wperm, dt) if dt != torch.float32 else wperm
-        y0 = K.linear(cat, Wc, b)
-        rows = cat.shape[0]
+    def forward(ctx, B, hw, E, bn, sync, wf, bf, gamma, beta, *lvl):
+        rows = lvl[0::3]
+        Ls, bs = lvl[1::3], lvl[2::3]
+        dt = rows[0].dtype
+        dev = rows[0].device
+        H0, W0 = hw[0]
+        wf2 = wf.detach().view(E, 4 * E)
+        Fs = [wf2[:, (3 - i) * E:(4 - i) * E] for i in range(4)]
+        # W'_i = F_i L_i (float32), b' = b_f + sum_i F_i b_i
+        Wp32 = [_mm32(Fs[i], Ls[i].detach(), torch.empty(E, Ls[i].shape[1], device=dev, dtype=torch.float32))
+                for i in range(4)]
+        bp = torch.empty(1, E, device=dev, dtype=torch.float32)
+        for i in range(4):
+            K.linear(bs[i].detach().view(1, E), Fs[i], bf.detach() if i == 0 else None, out=bp,
+                     beta=0.0 if i == 0 else 1.0)
+        Wpc = [w if dt == torch.float32 else K.cast(w, dt) for w in Wp32]
+        y0 = K.linear(rows[0], Wpc[0], bp.view(E))
+        for i in range(1, 4):
+            h, w = hw[i]
+            if (h, w) == (H0, W0):
+                K.linear(rows[i], Wpc[i], out=y0, beta=1.0)
+            else:  # at the level's own resolution, then upsampled into the sum
+                K.bilinear(K.linear(rows[i], Wpc[i]), (h, w), (H0, W0), B, out=y0, accumulate=True)
+        count = y0.shape[0]
         if bn.training:
             mean, rstd, count = bn_batch_stats(y0, bn, sync)
         else:
-            mean, rstd, count = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps), rows
+            mean, rstd = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps)
         y = K.bn_apply(y0, mean, rstd, gamma, beta, act=2)
-        ctx.save_for_backward(cat, Wc, y0, y, mean, rstd, gamma)
-        ctx.E, ctx.count, ctx.sync, ctx.wshape, ctx.bn = E, count, sync, w.shape, bn
+        ctx.save_for_backward(y0, y, mean, rstd, gamma, wf, bf, *rows, *Ls, *bs, *Wpc)
+        ctx.meta = (B, hw, E, count, sync, bn)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         K.TAG = "decoder.bwd"
-        cat, Wc, y0, y, mean, rstd, gamma = ctx.saved_tensors
-        E = ctx.E
+        sv = ctx.saved_tensors
+        y0, y, mean, rstd, gamma, wf, bf = sv[:7]
+        rows, Ls, bs, Wpc = sv[7:11], sv[11:15], sv[15:19], sv[19:23]
+        B, hw, E, count, sync, bn = ctx.meta
+        H0, W0 = hw[0]
+        dev = y0.device
         dy = K.relu_bwd(dy.contiguous(), y)
-        st2, dgamma, dbeta = bn_grad_stats(y0, dy, mean, rstd, ctx.bn, ctx.sync)
-        dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, ctx.count)
-        dWp, db = K.linear_wgrad(dy0, cat, bias_grad=True)  # columns [c1 | c4 | c3 | c2]
-        dW = torch.cat([dWp[:, E:], dWp[:, :E]], 1).reshape(ctx.wshape)
-        dcat = K.linear_dgrad(dy0, Wc)
-        return dcat, dW, db, dgamma, dbeta, None, None, None
+        st2, dgamma, dbeta = bn_grad_stats(y0, dy, mean, rstd, bn, sync)
+        dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, count)
+        f32 = dict(device=dev, dtype=torch.float32)
+        dbf = gslot(bf)
+        if dbf is None:
+            dbf = torch.empty(E, **f32)
+        dWp, drows = [], []
+        with K.wgrad_group():  # the four dW'_i as one grouped launch
+            for i in range(4):
+                h, w = hw[i]
+                G = dy0 if (h, w) == (H0, W0) else K.bilinear_bwd(dy0, (h, w), (H0, W0), B)
+                if i == 0:  # sum dy0 rides along as the bias gradient of level 1's product
+                    dWp.append(K.linear_wgrad(G, rows[i], bias_grad=True, bias_out=dbf)[0])
+                else:
+                    dWp.append(K.linear_wgrad(G, rows[i]))
+                drows.append(K.linear_dgrad(G, Wpc[i]))
+        wf2 = wf.detach().view(E, 4 * E)
+        dWf = gslot2(wf)
+        if dWf is None:
+            dWf = torch.empty(E, 4 * E, **f32)
+        dLs, dbs = [], []
+        for i in range(4):
+            Fi = wf2[:, (3 - i) * E:(4 - i) * E]
+            L = Ls[i].detach()
+            dL = gslot2(Ls[i])
+            dLs.append(_mm32(Fi, dWp[i], dL if dL is not None else torch.empty(E, L.shape[1], **f32), a_t=True))
+            dFi = dWf[:, (3 - i) * E:(4 - i) * E]
+            _mm32(dWp[i], L, dFi, b_t=True)                                 # dW'_i L_i^T
+            _mm32(dbf.view(E, 1), bs[i].detach().view(1, E), dFi, beta=1.0)  # + (sum dy0) b_i^T
+            dbi = gslot(bs[i])
+            dbi = dbi if dbi is not None else torch.empty(E, **f32)
+            K.linear_dgrad(dbf.view(1, E), Fi, out=dbi.view(1, E))           # F_i^T sum dy0
+            dbs.append(dbi)
+        grads = []
+        for i in range(4):
+            grads += [drows[i], dLs[i].view_as(Ls[i]), dbs[i]]
+        return (None, None, None, None, None, dWf.view_as(wf), dbf, dgamma, dbeta, *grads)
 
 
 # ========================================================================================== loss
