@@ -58,6 +58,7 @@ _SIGS = {
     "dfm_colsum_workspace": (c_size_t, [c_long, c_int]),
     "dfm_colsum": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_int, P, P]),
     "dfm_cast": (c_int, [c_int, c_int, c_long, P, P, P]),
+    "dfm_pack_slices": (c_int, [c_int, c_int, P, P, c_long, c_int, P, P]),
     "dfm_gelu_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, c_int, P]),
     "dfm_scale_mul": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, c_float, P, c_long, c_int,
                               P]),

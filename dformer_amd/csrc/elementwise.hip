@@ -599,6 +599,55 @@ extern "C" int dfm_cast(int din, int dout, long n, const void* x, void* y, dfm_s
   return DFM_OK;
 }
 
+// ---- pack n row-major [rows, cols] sources (each float32 / bf16 / f16) side by side into one
+// [rows, n * cols] destination (the NMF backward's rank-R input-gradient factors, ham_head.py:120-145)
+constexpr int PACK_MAX = 32;
+struct PackSrc {
+  const void* p[PACK_MAX];
+  int dt[PACK_MAX];
+};
+
+template <typename TO>
+__global__ __launch_bounds__(256) void pack_slices_kernel(PackSrc src, int n, long rows, int cols, TO* __restrict__ dst) {
+  const long total = rows * (long)n * cols;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / ((long)n * cols);
+    const int q = (int)(e - r * n * cols), i = q / cols, c = q - i * cols;
+    const long si = r * cols + c;
+    float v;
+    if (src.dt[i] == DFM_F32) v = ((const float*)src.p[i])[si];
+    else if (src.dt[i] == DFM_BF16) v = bf2f(((const bf16_t*)src.p[i])[si]);
+    else v = Num<f16_t>::to_f(((const f16_t*)src.p[i])[si]);
+    dst[e] = Num<TO>::from_f(v);
+  }
+}
+
+extern "C" int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, const int* src_dtypes, long rows,
+                               int cols, void* dst, dfm_stream_t stream) {
+  DFM_CHECK_ARG(n >= 1 && n <= PACK_MAX && srcs && src_dtypes && dst && rows >= 0 && cols > 0,
+                "dfm_pack_slices: 1 <= n <= %d sources, non-null pointers", PACK_MAX);
+  PackSrc ps{};
+  for (int i = 0; i < n; ++i) {
+    DFM_CHECK_ARG(srcs[i] != nullptr, "dfm_pack_slices: null source %d", i);
+    DFM_CHECK_ARG(src_dtypes[i] == DFM_F32 || src_dtypes[i] == DFM_BF16 || src_dtypes[i] == DFM_F16,
+                  "dfm_pack_slices: bad source dtype %d", src_dtypes[i]);
+    ps.p[i] = srcs[i];
+    ps.dt[i] = src_dtypes[i];
+  }
+  if (rows == 0) return DFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = ew_grid(rows * (long)n * cols);
+  if (dtype_out == DFM_BF16) DFM_LAUNCH(pack_slices_kernel<bf16_t>, dim3(g), dim3(256), 0, s, ps, n, rows, cols, (bf16_t*)dst);
+  else if (dtype_out == DFM_F16) DFM_LAUNCH(pack_slices_kernel<f16_t>, dim3(g), dim3(256), 0, s, ps, n, rows, cols, (f16_t*)dst);
+  else if (dtype_out == DFM_F32) DFM_LAUNCH(pack_slices_kernel<float>, dim3(g), dim3(256), 0, s, ps, n, rows, cols, (float*)dst);
+  else {
+    dfm_set_error("dfm_pack_slices: bad dtype %d", dtype_out);
+    return DFM_ERR_DTYPE;
+  }
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
 extern "C" int dfm_gelu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* pre, long ldpre,
                             void* dx, long lddx, int accumulate, dfm_stream_t stream) {
   DFM_CHECK_ARG(dy && pre && dx, "dfm_gelu_bwd: null argument");

@@ -307,15 +307,11 @@ class NMF2DFn(torch.autograd.Function):
         # side by side and applied by ONE GEMM over the concatenated K = T*R at the end, instead of
         # T read-modify-write passes over the [N, D] gradient.
         T = 2 * len(ctx.hist) + 2
-        Pc = torch.empty(Bb, N, T * R, device=x.device, dtype=x.dtype)
-        Qc = torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype)
-        slot = [0]
+        Ps, Qs = [], []
 
-        def gx_term(P, Q):
-            i = slot[0]
-            Pc[:, :, i * R:(i + 1) * R].copy_(P)
-            Qc[:, :, i * R:(i + 1) * R].copy_(Q)
-            slot[0] += 1
+        def gx_term(P, Q):  # packed side by side at the end, one launch per operand (K.pack_slices)
+            Ps.append(P)
+            Qs.append(Q)
 
         # final coef update: Cf = Ct * num / (Ct M + eps), num = x B, M = B^T B
         gCt, gnum, gden, gnum16 = upd_bwd(gC, Ct, num, den, Cf)
@@ -341,7 +337,9 @@ class NMF2DFn(torch.autograd.Function):
         # coef0 = softmax(x B0)  (B0 is a random constant)
         gS = K.softmax_rows_bwd(coef0, gC)
         gx_term(gS, B0)                                           # gx += gS B0^T
-        assert slot[0] == T
+        assert len(Ps) == T
+        Pc = K.pack_slices(Ps, torch.empty(Bb, N, T * R, device=x.device, dtype=x.dtype))
+        Qc = K.pack_slices(Qs, torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype))
         gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T, x.dtype
         ctx.hist = ctx.final = None
         return gx, None, None, None

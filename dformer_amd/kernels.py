@@ -369,6 +369,22 @@ def cast(x, dtype, out=None):
     return out
 
 
+def pack_slices(srcs, out):
+    """out [..., n * cols] <- the n tensors [..., cols] side by side (converted to out.dtype), one launch."""
+    n, cols = len(srcs), srcs[0].shape[-1]
+    rows = srcs[0].numel() // cols
+    assert out.is_contiguous() and out.shape[-1] == n * cols and out.numel() == rows * n * cols
+    for t in srcs:
+        assert t.is_contiguous() and t.shape[-1] == cols and t.numel() == rows * cols
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    dts = (ctypes.c_int * n)(*[dtype_code(t) for t in srcs])
+    check(lib.dfm_pack_slices(dtype_code(out), n, ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(dts, ctypes.c_void_p),
+                              rows, cols, ptr(out), stream()), "dfm_pack_slices")
+    if ACCOUNT is not None:
+        _acct(0, sum(t.numel() * _es(t) for t in srcs) + out.numel() * _es(out))
+    return out
+
+
 def gelu_bwd(dy, pre, out=None, accumulate=False):
     rows, C = dy.shape
     if out is None:

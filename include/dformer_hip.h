@@ -168,6 +168,10 @@ int dfm_colsum(int dtype, long rows, int C, const void* x, long ldx, const void*
                dfm_stream_t stream);
 /* y = op(x): 0 copy/cast, used for float32 <-> bf16 conversion (dtype_in, dtype_out). */
 int dfm_cast(int dtype_in, int dtype_out, long n, const void* x, void* y, dfm_stream_t stream);
+/* n (<= 32) row-major [rows, cols] sources of dtypes src_dtypes[i] packed side by side (converted) into
+ * dst [rows, n * cols] of dtype_out, one launch (the NMF backward's rank-R factors, ham_head.py:120-145) */
+int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, const int* src_dtypes, long rows, int cols,
+                    void* dst, dfm_stream_t stream);
 /* dx (+= when accumulate) = dy * gelu'(pre)   (nn.GELU backward, DFormer.py:56,97,113) */
 int dfm_gelu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* pre, long ldpre,
                  void* dx, long lddx, int accumulate, dfm_stream_t stream);

@@ -729,3 +729,15 @@ def test_gemm_fused_epilogues_step_shapes(dt, M, N, Kd, ldx):
     want = dx.float() + ref
     k.linear_dgrad(dy, wd, out=dx, accumulate=True)
     assert rel(dx.float(), want) < tol
+
+
+def test_pack_slices():
+    """dfm_pack_slices: n sources of mixed dtypes side by side into one [rows, n*cols] tensor (the NMF
+    backward's rank-R factors), exactly torch.cat of the converted sources."""
+    k = K()
+    srcs = [torch.randn(3, 50, 64, device=DEV).to(dt) for dt in (torch.float32, torch.bfloat16, torch.float32,
+                                                                    torch.float16, torch.float32)]
+    for odt in (torch.bfloat16, torch.float32, torch.float16):
+        out = torch.empty(3, 50, 5 * 64, device=DEV, dtype=odt)
+        k.pack_slices(srcs, out)
+        assert torch.equal(out, torch.cat([s.to(odt) for s in srcs], -1))
