@@ -1236,6 +1236,11 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     a.stream = sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb &&
                d->K % BKsel == 0 && d->K / BKsel <= 8 && tiles >= 1024;
   }
+  // bf16 k-contiguous A on the LDS-DMA ring: split-K off (one unsplit 64x64 ring block per tile beats
+  // the split + reduction at 4,800 rows x K >= 1024: 16.8 vs 34.8 us, profiles/r04_glds_variants.txt)
+  bool glds_ok = std::is_same<T, bf16_t>::value && ak && a.ala && a.alb;
+  if (glds_ok && d->split_k < 1) a.splits = 1;
+  glds_ok = glds_ok && (d->K + a.splits - 1) / a.splits >= 2 * GBK;  // >= 2 whole k-slices per split
   // tall short-K GEMMs with more than one 128-column slice (gemm_wide.h): measured per shape on the
   // DFormer-B step's census (profiles/r04_wide_gemm_ab.txt) it wins from 65,536 rows and N >= 144
   // (stage-0 fc1 104 vs 138 us, stage-1 fc2 input gradient x GELU' 106 vs 124 us) and loses on
@@ -1249,11 +1254,13 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // images/s vs 415.4-416.0 from K = 640); with a row-contiguous A (weight gradients) the
   // register-staged kernel stays ahead (a 3/4-stage ring there measured 386.3 vs 408 images/s).
   // 64x64 tiles for every width: the stage-1..3 shapes are latency-bound and gain from twice the
-  // blocks more than they lose in B-tile reuse (421.5 vs 418.1-418.5 images/s with 64x128).
+  // blocks more than they lose in B-tile reuse (421.5 vs 418.1-418.5 images/s with 64x128). Bigger
+  // tiles chosen per shape (128x128 from 65,536 rows, 128x64 / 64x128 elsewhere: 1 ms less GEMM time
+  // per step replayed in isolation, tools/gemm_variants.py) measured flat on the step (37.45-37.59
+  // ms/step either way, profiles/r04_glds_variants.txt).
   if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
-    const int kper = (d->K + a.splits - 1) / a.splits;
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 128);
-    if (route && !a.stream && a.ala && a.alb && kper >= 2 * GBK) {
+    if (glds_ok && route && !a.stream) {
       if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
       return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
     }
