@@ -465,6 +465,11 @@ class GraphedTrainStep:
                 train_step(model, opt, rgb, depth, label)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        if collectives_on(opt.world) and dist.get_backend() == "nccl":
+            # the RCCL watchdog thread polls the events of the warm-up's collectives until it retires
+            # them; a poll failing under the capture makes it rethrow on its own thread (SIGABRT seen
+            # once in capture_end): nothing of the eager steps may still be pending when capture begins
+            dist.distributed_c10d._get_default_group()._wait_for_pending_works()
         self.graph = torch.cuda.CUDAGraph()
         opt.external_hyper = True  # inside the graph AdamW only reads hyper
         try:
