@@ -33,6 +33,12 @@ class GemmDesc(ctypes.Structure):
                 ("workspace_bytes", ctypes.c_long)]
 
 
+class PartialSum(ctypes.Structure):
+    """DfmPartialSum: a deferred reduction second stage (dfm_partial_sum_group)."""
+    _fields_ = [("part", P), ("out0", P), ("out1", P), ("n", c_long), ("n0", c_long), ("nblk", c_int),
+                ("layout", c_int), ("accumulate", c_int)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dfm_last_error": (ctypes.c_char_p, []),
@@ -44,17 +50,19 @@ _SIGS = {
     "dfm_layernorm_fwd": (c_int, [c_int, c_long, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P]),
     "dfm_layernorm_bwd_workspace": (c_size_t, [c_long, c_int]),
     "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, P, c_long, c_int,
-                                  P, P, P, P]),
+                                  P, P, P, P, P]),
     "dfm_residual_bwd_workspace": (c_size_t, [c_long, c_int]),
-    "dfm_residual_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, P]),
+    "dfm_residual_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, P, P]),
     "dfm_dwconv_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, P, c_int, P, c_long, P, c_long,
                                P]),
     "dfm_dwconv_bwd_data": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_int, P, c_long,
                                     c_int, P]),
     "dfm_dwconv_bwd_weight_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
-    "dfm_dwconv_bwd_weight": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P]),
+    "dfm_dwconv_bwd_weight": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, P, P, P,
+                                      P]),
     "dfm_dwconv_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
-                               c_int, P, P, P, P]),
+                               c_int, P, P, P, P, P]),
+    "dfm_partial_sum_group": (c_int, [c_int, P, P]),
     "dfm_colsum_workspace": (c_size_t, [c_long, c_int]),
     "dfm_colsum": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_int, P, P]),
     "dfm_cast": (c_int, [c_int, c_int, c_long, P, P, P]),

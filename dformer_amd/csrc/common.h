@@ -288,3 +288,19 @@ void dfm_set_error(const char* fmt, ...);
   } while (0)
 
 static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// The second stage of a parameter-gradient reduction: launched now (defer NULL) or described in
+// *defer for the caller's grouped launch (dfm_partial_sum_group, elementwise.hip).
+static inline int second_stage(int layout, int nblk, long n, const float* part, float* out0, float* out1, long n0,
+                               int accumulate, DfmPartialSum* defer, hipStream_t s) {
+  if (defer) {
+    *defer = DfmPartialSum{part, out0, out1, n, n0, nblk, layout, accumulate};
+    return DFM_OK;
+  }
+  const dim3 grid(cdiv(n, 64));
+  if (layout == 0) DFM_LAUNCH(partial_sum_kernel<0>, grid, dim3(1024), 0, s, nblk, n, part, out0, out1, n0, accumulate);
+  else if (layout == 1) DFM_LAUNCH(partial_sum_kernel<1>, grid, dim3(1024), 0, s, nblk, n, part, out0, out1, n0, accumulate);
+  else DFM_LAUNCH(partial_sum_kernel<2>, grid, dim3(1024), 0, s, nblk, n, part, out0, out1, n0, accumulate);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}

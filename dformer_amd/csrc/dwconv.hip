@@ -1017,7 +1017,9 @@ extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, in
 
 extern "C" int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
                               const void* dy, long lddy, const float* w, int add_identity, void* dx, long lddx,
-                              int accumulate, float* dw, float* db, void* workspace, dfm_stream_t stream) {
+                              int accumulate, float* dw, float* db, void* workspace, DfmPartialSum* defer,
+                              dfm_stream_t stream) {
+  if (defer) *defer = DfmPartialSum{};
   DFM_CHECK_ARG(x && dy && w && dx && dw && workspace, "dfm_dwconv_bwd: null argument");
   DFM_CHECK_ARG(k == 3, "dfm_dwconv_bwd: k=%d unsupported (3x3 only)", k);
   DFM_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd: bad shape");
@@ -1041,15 +1043,13 @@ extern "C" int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, cons
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  DFM_LAUNCH(partial_sum_kernel<2>, dim3(cdiv((long)C * 10, 64)), dim3(1024), 0, s, (int)nsb, (long)C * 10,
-                     (const float*)part, dw, db, 10L, 0);
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
+  return second_stage(2, (int)nsb, (long)C * 10, part, dw, db, 10L, 0, defer, s);
 }
 
 extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
                                      const void* dy, long lddy, float* dw, float* db, void* workspace,
-                                     dfm_stream_t stream) {
+                                     DfmPartialSum* defer, dfm_stream_t stream) {
+  if (defer) *defer = DfmPartialSum{};
   DFM_CHECK_ARG(x && dy && dw && workspace, "dfm_dwconv_bwd_weight: null argument");
   DFM_CHECK_ARG(k == 3 || k == 7, "dfm_dwconv_bwd_weight: k=%d unsupported", k);
   DFM_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd_weight: bad shape");
@@ -1074,8 +1074,5 @@ extern "C" int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int 
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  DFM_LAUNCH(partial_sum_kernel<2>, dim3(cdiv((long)C * (k * k + 1), 64)), dim3(1024), 0, s, (int)nsb,
-                     (long)C * (k * k + 1), (const float*)part, dw, db, (long)(k * k + 1), 0);
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
+  return second_stage(2, (int)nsb, (long)C * (k * k + 1), part, dw, db, (long)(k * k + 1), 0, defer, s);
 }

@@ -648,6 +648,73 @@ extern "C" int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, co
   return DFM_OK;
 }
 
+// ---- deferred second stages of up to PSG_MAX reductions in one launch: block b belongs to the sum q
+// with blk0[q] <= b < blk0[q + 1] and reduces its 64 columns exactly as partial_sum_kernel does
+// (16 row-lanes in block order, then the 16 lanes in order), so the results are bit-identical.
+constexpr int PSG_MAX = 16;
+struct PsGroup {
+  DfmPartialSum p[PSG_MAX];
+  int blk0[PSG_MAX + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(1024) void partial_sum_group_kernel(PsGroup g) {
+  int q = 0;
+  while (q + 1 < g.count && (int)blockIdx.x >= g.blk0[q + 1]) ++q;
+  const DfmPartialSum& ps = g.p[q];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const long e = (blockIdx.x - g.blk0[q]) * 64L + cl;
+  float s = 0.f;
+  if (e < ps.n) {
+#pragma unroll 4
+    for (int b = rl; b < ps.nblk; b += 16) s += ps.part[(long)b * ps.n + e];
+  }
+  __shared__ float red[16][64];
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && e < ps.n) {
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v += red[r][cl];
+    float* dst;
+    if (ps.layout == 0) dst = ps.out0 + e;
+    else if (ps.layout == 1) dst = e < ps.n0 ? ps.out0 + e : ps.out1 + (e - ps.n0);
+    else {
+      const long c = e / ps.n0, i = e % ps.n0;
+      dst = i < ps.n0 - 1 ? ps.out0 + c * (ps.n0 - 1) + i : (ps.out1 ? ps.out1 + c : nullptr);
+    }
+    if (dst) *dst = ps.accumulate ? *dst + v : v;
+  }
+}
+
+extern "C" int dfm_partial_sum_group(int n, const DfmPartialSum* sums, dfm_stream_t stream) {
+  DFM_CHECK_ARG(n >= 0 && (n == 0 || sums), "dfm_partial_sum_group: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  PsGroup g{};
+  auto issue = [&]() -> int {
+    if (g.count == 0) return DFM_OK;
+    DFM_LAUNCH(partial_sum_group_kernel, dim3(g.blk0[g.count]), dim3(1024), 0, s, g);
+    DFM_LAUNCH_CHECK();
+    g = PsGroup{};
+    return DFM_OK;
+  };
+  for (int i = 0; i < n; ++i) {
+    const DfmPartialSum& p = sums[i];
+    if (p.n == 0) continue;  // an entry point that returned before its first stage
+    DFM_CHECK_ARG(p.n > 0 && p.nblk >= 0 && p.part && p.out0 && p.layout >= 0 && p.layout <= 2 &&
+                      (p.layout != 1 || (p.out1 && p.n0 > 0 && p.n0 < p.n)) && (p.layout != 2 || p.n0 >= 2),
+                  "dfm_partial_sum_group: malformed sum %d", i);
+    if (g.count == PSG_MAX) {
+      const int r = issue();
+      if (r != DFM_OK) return r;
+    }
+    g.p[g.count] = p;
+    g.blk0[g.count + 1] = g.blk0[g.count] + (int)cdiv(p.n, 64);
+    ++g.count;
+  }
+  return issue();
+}
+
 extern "C" int dfm_gelu_bwd(int dtype, long rows, int C, const void* dy, long lddy, const void* pre, long ldpre,
                             void* dx, long lddx, int accumulate, dfm_stream_t stream) {
   DFM_CHECK_ARG(dy && pre && dx, "dfm_gelu_bwd: null argument");
@@ -956,7 +1023,8 @@ extern "C" size_t dfm_residual_bwd_workspace(long rows, int C) { return (size_t)
 
 extern "C" int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout, const void* f, long ldf_,
                                 const float* colscale, const float* rowscale, long rps, void* df, long lddf,
-                                float* dscale, void* ws, dfm_stream_t stream) {
+                                float* dscale, void* ws, DfmPartialSum* defer, dfm_stream_t stream) {
+  if (defer) *defer = DfmPartialSum{};
   DFM_CHECK_ARG(dout && f && df && dscale && ws && C % 8 == 0 && C <= 2048, "dfm_residual_bwd: bad argument");
   DFM_CHECK_ARG(lddout % 8 == 0 && ldf_ % 8 == 0 && lddf % 8 == 0 && (uintptr_t)dout % 16 == 0 &&
                     (uintptr_t)f % 16 == 0 && (uintptr_t)df % 16 == 0,
@@ -978,8 +1046,5 @@ extern "C" int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, l
     return DFM_ERR_DTYPE;
   }
   DFM_LAUNCH_CHECK();
-  DFM_LAUNCH(partial_sum_kernel<0>, dim3(cdiv(C, 64)), dim3(1024), 0, s, nblk, (long)C, (const float*)ws, dscale,
-                     (float*)nullptr, 0L, 0);
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
+  return second_stage(0, nblk, (long)C, (const float*)ws, dscale, nullptr, 0L, 0, defer, s);
 }

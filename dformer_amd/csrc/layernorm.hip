@@ -382,7 +382,7 @@ int ln_fwd(long rows, int C, const void* x, long ldx, const float* gamma, const 
 template <typename T>
 int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy, const float* gamma,
            const float* mean, const float* rstd, const void* dres, long lddres, void* dx, long lddx, int acc,
-           float* dg, float* db, void* ws,
+           float* dg, float* db, void* ws, DfmPartialSum* defer,
            hipStream_t s) {
   float* part = (float*)ws;
   int VG, VNV;
@@ -400,10 +400,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
 #undef GOV
     if (launched) {
       DFM_LAUNCH_CHECK();
-      DFM_LAUNCH(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)vgrid, 2L * C,
-                         (const float*)part, dg, db, (long)C, 0);
-      DFM_LAUNCH_CHECK();
-      return DFM_OK;
+      return second_stage(1, (int)vgrid, 2L * C, part, dg, db, (long)C, 0, defer, s);
     }
   }
   const int G = pick_g(C);
@@ -419,10 +416,7 @@ int ln_bwd(long rows, int C, const void* x, long ldx, const void* dy, long lddy,
   }
 #undef GO
   DFM_LAUNCH_CHECK();
-  DFM_LAUNCH(partial_sum_kernel<1>, dim3(cdiv(2L * C, 64)), dim3(1024), 0, s, (int)grid, 2L * C,
-                     (const float*)part, dg, db, (long)C, 0);
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
+  return second_stage(1, (int)grid, 2L * C, part, dg, db, (long)C, 0, defer, s);
 }
 }  // namespace
 
@@ -447,20 +441,21 @@ extern "C" size_t dfm_layernorm_bwd_workspace(long rows, int C) {
 extern "C" int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
                                  const float* gamma, const float* mean, const float* rstd, const void* dres,
                                  long lddres, void* dx, long lddx, int accumulate, float* dgamma, float* dbeta,
-                                 void* workspace, dfm_stream_t stream) {
+                                 void* workspace, DfmPartialSum* defer, dfm_stream_t stream) {
+  if (defer) *defer = DfmPartialSum{};  // n = 0: nothing to sum unless the first stage runs
   DFM_CHECK_ARG(C > 0 && C <= 1024, "dfm_layernorm_bwd: C=%d unsupported", C);
   DFM_CHECK_ARG(x && dy && dx && gamma && mean && rstd && dgamma && dbeta && workspace,
                 "dfm_layernorm_bwd: null argument");
   if (rows == 0) return DFM_OK;
   if (dtype == DFM_BF16)
     return ln_bwd<bf16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
-                          workspace, (hipStream_t)stream);
+                          workspace, defer, (hipStream_t)stream);
   else if (dtype == DFM_F16)
     return ln_bwd<f16_t>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
-                          workspace, (hipStream_t)stream);
+                          workspace, defer, (hipStream_t)stream);
   if (dtype == DFM_F32)
     return ln_bwd<float>(rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dres, lddres, dx, lddx, accumulate, dgamma, dbeta,
-                         workspace, (hipStream_t)stream);
+                         workspace, defer, (hipStream_t)stream);
   dfm_set_error("dfm_layernorm_bwd: bad dtype");
   return DFM_ERR_DTYPE;
 }

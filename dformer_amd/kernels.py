@@ -61,6 +61,10 @@ def _es(t):
     return t.element_size()
 
 
+def _pref(ps):
+    return None if ps is None else ctypes.byref(ps)
+
+
 def _ws(nbytes, dev):
     """Scratch buffer per (device, stream) that only grows (the library never allocates); one per
     stream so kernels running concurrently on a side stream never share a workspace. A buffer that
@@ -96,25 +100,57 @@ def rows_of(t):
 # problems each + one split-K combine), so the independent dW GEMMs of a Block's backward share the
 # chip instead of each splitting K over all of it. Their outputs must not be read before the block
 # ends (they only feed the optimizer).
+# The second stages of the parameter-gradient reductions issued inside (LayerNorm dgamma / dbeta,
+# layer-scale dscale, depthwise dw / db: fixed-order sums over per-block partials) are deferred the
+# same way and issued as ONE dfm_partial_sum_group launch per block instead of one small launch each;
+# every deferred reduction keeps its own partials buffer until then.
 _WG_PENDING = None
+_RED_PENDING = None
 
 
 class wgrad_group:
-    """Queue the weight-gradient GEMMs issued inside; at exit issue them with flush_wgrad on the
-    current stream."""
+    """Queue the weight-gradient GEMMs and reduction second stages issued inside; at exit issue
+    them (flush_wgrad, flush_reductions) on the current stream."""
 
     def __enter__(self):
-        global _WG_PENDING
-        self.prev = _WG_PENDING
-        _WG_PENDING = []
+        global _WG_PENDING, _RED_PENDING
+        self.prev = (_WG_PENDING, _RED_PENDING)
+        _WG_PENDING, _RED_PENDING = [], []
         return self
 
     def __exit__(self, exc_type, exc, tb):
-        global _WG_PENDING
-        pending, _WG_PENDING = _WG_PENDING, self.prev
-        if pending and exc_type is None:
-            flush_wgrad(pending)
+        global _WG_PENDING, _RED_PENDING
+        pending, reds = _WG_PENDING, _RED_PENDING
+        _WG_PENDING, _RED_PENDING = self.prev
+        if exc_type is None:
+            if pending:
+                flush_wgrad(pending)
+            if reds:
+                flush_reductions(reds)
         return False
+
+
+def _red_ws(nbytes, dev):
+    """(workspace, DfmPartialSum or None): inside a wgrad_group a reduction gets a partials buffer of
+    its own and a descriptor its entry point fills instead of launching the second stage."""
+    if _RED_PENDING is None or nbytes == 0:
+        return _ws(nbytes, dev), None
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ps = _lib.PartialSum()
+    _RED_PENDING.append((ps, buf))
+    return buf, ps
+
+
+def flush_reductions(reds):
+    """Issue deferred reduction second stages as one dfm_partial_sum_group launch (16 per launch)."""
+    n = len(reds)
+    arr = (_lib.PartialSum * n)(*[r[0] for r in reds])
+    cur = torch.cuda.current_stream()
+    for _, buf in reds:  # partials written on a side stream are read here: no reuse before that
+        buf.record_stream(cur)
+    check(lib.dfm_partial_sum_group(n, ctypes.cast(arr, ctypes.c_void_p), stream()), "dfm_partial_sum_group")
+    if ACCOUNT is not None:  # second stages: no algorithmic bytes (the partials are not algorithmic)
+        _acct(0, 0)
 
 
 def flush_wgrad(pending):
@@ -257,10 +293,10 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dres=None
         accumulate = False
     dg = torch.empty(C, device=x.device, dtype=torch.float32)
     db = torch.empty(C, device=x.device, dtype=torch.float32)
-    ws = _ws(lib.dfm_layernorm_bwd_workspace(rows, C), x.device)
+    ws, ps = _red_ws(lib.dfm_layernorm_bwd_workspace(rows, C), x.device)
     check(lib.dfm_layernorm_bwd(dtype_code(x), rows, C, ptr(x), ld(x), ptr(dy), ld(dy), ptr(gamma), ptr(mean),
                                 ptr(rstd), ptr(dres), ld(dres) if dres is not None else 0, ptr(dx), ld(dx),
-                                int(accumulate), ptr(dg), ptr(db), ptr(ws), stream()), "dfm_layernorm_bwd")
+                                int(accumulate), ptr(dg), ptr(db), ptr(ws), _pref(ps), stream()), "dfm_layernorm_bwd")
     if ACCOUNT is not None:
         _acct(0, rows * C * _es(x) * (3 + (dres is not None) + bool(accumulate)) + 8 * rows)
     return dx, dg, db
@@ -272,9 +308,9 @@ def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
     if df is None:
         df = torch.empty(rows, C, device=dout.device, dtype=dout.dtype)
     dls = torch.empty(C, device=dout.device, dtype=torch.float32)
-    ws = _ws(lib.dfm_residual_bwd_workspace(rows, C), dout.device)
+    ws, ps = _red_ws(lib.dfm_residual_bwd_workspace(rows, C), dout.device)
     check(lib.dfm_residual_bwd(dtype_code(dout), rows, C, ptr(dout), ld(dout), ptr(f), ld(f), ptr(colscale),
-                               ptr(rowscale), rows_per_scale, ptr(df), ld(df), ptr(dls), ptr(ws), stream()),
+                               ptr(rowscale), rows_per_scale, ptr(df), ld(df), ptr(dls), ptr(ws), _pref(ps), stream()),
           "dfm_residual_bwd")
     if ACCOUNT is not None:
         _acct(0, rows * C * _es(dout) * 3)
@@ -322,9 +358,10 @@ def dwconv_bwd(x, dy, shape, w, k, add_identity=False, dx=None, accumulate=False
         dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
     if db is None:
         db = torch.empty(C, device=x.device, dtype=torch.float32)
-    ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
+    ws, ps = _red_ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
     check(lib.dfm_dwconv_bwd(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(w), int(add_identity),
-                             ptr(dx), ld(dx), int(accumulate), ptr(dw), ptr(db), ptr(ws), stream()), "dfm_dwconv_bwd")
+                             ptr(dx), ld(dx), int(accumulate), ptr(dw), ptr(db), ptr(ws), _pref(ps), stream()),
+          "dfm_dwconv_bwd")
     if ACCOUNT is not None:
         _acct(4 * k * k * C * x.shape[0], x.shape[0] * C * _es(x) * (3 + bool(accumulate)))
     return dx, dw, db
@@ -337,9 +374,9 @@ def dwconv_bwd_weight(x, dy, shape, k, dw=None, db=None):
         dw = torch.empty(C, 1, k, k, device=x.device, dtype=torch.float32)
     if db is None:
         db = torch.empty(C, device=x.device, dtype=torch.float32)
-    ws = _ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
+    ws, ps = _red_ws(lib.dfm_dwconv_bwd_weight_workspace(B, H, W, C, k), x.device)
     check(lib.dfm_dwconv_bwd_weight(dtype_code(x), B, H, W, C, k, ptr(x), ld(x), ptr(dy), ld(dy), ptr(dw), ptr(db),
-                                    ptr(ws), stream()), "dfm_dwconv_bwd_weight")
+                                    ptr(ws), _pref(ps), stream()), "dfm_dwconv_bwd_weight")
     if ACCOUNT is not None:
         _acct(2 * k * k * C * x.shape[0], x.shape[0] * C * _es(x) * 2)
     return dw, db

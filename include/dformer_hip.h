@@ -39,7 +39,8 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 7 (round 4: DfmGemmDesc.workspace_bytes + stride / leading-dimension validation) */
+int dfm_abi_version(void); /* 8 (round 4: DfmGemmDesc.workspace_bytes + stride / leading-dimension validation;
+                              deferred reduction second stages, dfm_partial_sum_group) */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -113,10 +114,34 @@ size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d);
 int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
                    void* const* C, void* workspace, dfm_stream_t stream);
 
+/* ---------------------------------------------------------------- deferred reduction second stages
+ * The parameter-gradient reductions below (LayerNorm dgamma / dbeta, layer-scale dscale, depthwise
+ * dw / db) run in two stages: per-block partials in the caller's workspace, then a fixed-order sum
+ * over the blocks. With `defer` NULL an entry point launches both. With `defer` non-NULL it launches
+ * only the first stage and describes the second in *defer; dfm_partial_sum_group then runs up to 16
+ * such sums in ONE launch (a Block's backward issues them together at its end, with its grouped
+ * weight gradients). Until that launch the workspace must stay untouched and the outputs unread.
+ * Results are bit-identical to the undeferred call (same partials, same summation order).
+ *   layout 0: out0[e] = sum_b part[b*n + e]                      (e < n)
+ *   layout 1: e < n0 ? out0[e] : out1[e - n0]
+ *   layout 2: depthwise [C][n0] with n0 = k*k + 1: out0[c*(n0-1) + i] for i < n0-1, out1[c] (bias)
+ *   accumulate: out += sum instead of out = sum. */
+typedef struct DfmPartialSum {
+  const float* part;
+  float* out0;
+  float* out1;
+  long n;
+  long n0;
+  int nblk;
+  int layout;
+  int accumulate;
+} DfmPartialSum;
+int dfm_partial_sum_group(int n, const DfmPartialSum* sums, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- LayerNorm, channels_last
  * DFormer.py:21-45 (F.layer_norm over the last dim, eps 1e-6). mean/rstd: float32 [rows].
  * bwd: dx (+= when accumulate), dgamma/dbeta float32 [C] (overwritten); workspace from
- * dfm_layernorm_bwd_workspace. */
+ * dfm_layernorm_bwd_workspace; defer: see dfm_partial_sum_group. */
 int dfm_layernorm_fwd(int dtype, long rows, int C, const void* x, long ldx, const float* gamma,
                       const float* beta, float eps, void* y, long ldy, float* mean, float* rstd,
                       dfm_stream_t stream);
@@ -125,16 +150,17 @@ size_t dfm_layernorm_bwd_workspace(long rows, int C);
 int dfm_layernorm_bwd(int dtype, long rows, int C, const void* x, long ldx, const void* dy, long lddy,
                       const float* gamma, const float* mean, const float* rstd, const void* dres, long lddres,
                       void* dx, long lddx, int accumulate, float* dgamma, float* dbeta, void* workspace,
-                      dfm_stream_t stream);
+                      DfmPartialSum* defer, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- residual / layer-scale backward
  * Block.forward's x + DropPath(ls * f) (DFormer.py:173-179), backward in one pass over dout and f:
  *   df[r,c] = dout[r,c] * colscale[c] * rowscale[r/rps];   dscale[c] = sum_r dout * f * rowscale[r/rps]
- * (rowscale NULL = 1; dscale overwritten; workspace from dfm_residual_bwd_workspace). */
+ * (rowscale NULL = 1; dscale overwritten; workspace from dfm_residual_bwd_workspace; defer: see
+ * dfm_partial_sum_group). */
 size_t dfm_residual_bwd_workspace(long rows, int C);
 int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout, const void* f, long ldf,
                      const float* colscale, const float* rowscale, long rows_per_scale, void* df, long lddf,
-                     float* dscale, void* workspace, dfm_stream_t stream);
+                     float* dscale, void* workspace, DfmPartialSum* defer, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- depthwise conv k x k, NHWC
  * DFormer.py:80-81 (7x7 conv/e_conv, pad 3) and DFormer.py:54,62 (3x3 pos + identity).
@@ -142,7 +168,8 @@ int dfm_residual_bwd(int dtype, long rows, int C, const void* dout, long lddout,
  * gelu_out): y receives gelu'(y) instead of y. gelu_out (optional): GELU(y) as well (the ConvFFN
  * activation, DFormer.py:64).
  * bwd_data: dx (+= when accumulate) = conv(dy, flipped w) (+ dy when add_identity).
- * bwd_weight: dw [C][k][k], db [C] (overwritten), workspace from dfm_dwconv_bwd_weight_workspace. */
+ * bwd_weight: dw [C][k][k], db [C] (overwritten), workspace from dfm_dwconv_bwd_weight_workspace;
+ * defer: see dfm_partial_sum_group. */
 int dfm_dwconv_fwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const float* w,
                    const float* bias, int add_identity, void* y, long ldy, void* gelu_out, long ldg,
                    dfm_stream_t stream);
@@ -152,12 +179,12 @@ int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k, const void
 size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k);
 int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
                           const void* dy, long lddy, float* dw, float* db, void* workspace,
-                          dfm_stream_t stream);
+                          DfmPartialSum* defer, dfm_stream_t stream);
 /* bwd_data and bwd_weight of a 3x3 in one pass over dy and x (the ConvFFN's pos conv): dx (+= when
  * accumulate), dw, db as above; workspace from dfm_dwconv_bwd_weight_workspace (k = 3 only). */
 int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const void* dy,
                    long lddy, const float* w, int add_identity, void* dx, long lddx, int accumulate, float* dw,
-                   float* db, void* workspace, dfm_stream_t stream);
+                   float* db, void* workspace, DfmPartialSum* defer, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)

@@ -741,3 +741,44 @@ def test_pack_slices():
         out = torch.empty(3, 50, 5 * 64, device=DEV, dtype=odt)
         k.pack_slices(srcs, out)
         assert torch.equal(out, torch.cat([s.to(odt) for s in srcs], -1))
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_deferred_reductions_bit_identical(dt):
+    """Inside wgrad_group the reduction second stages (LN dgamma/dbeta, layer-scale dscale, DW3x3
+    fused and DW7x7 weight gradients) are deferred to one dfm_partial_sum_group launch: the results
+    must equal the immediate two-launch path bit for bit, including a DW7 weight gradient issued on a
+    side stream and joined before the flush (the attention backward's depth branch)."""
+    Kk = K()
+    B, H, W, C = 2, 30, 40, 96
+    P = B * H * W
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(P, C, device=DEV, generator=g).to(dt)
+    dy = torch.randn(P, C, device=DEV, generator=g).to(dt)
+    f = torch.randn(P, C, device=DEV, generator=g).to(dt)
+    gam = torch.rand(C, device=DEV, generator=g) + 0.5
+    bet = torch.randn(C, device=DEV, generator=g)
+    ls = torch.rand(C, device=DEV, generator=g)
+    rs = torch.rand(B, device=DEV, generator=g)
+    w3 = torch.randn(C, 1, 3, 3, device=DEV, generator=g) / 3
+    xn, mu, rstd = Kk.layernorm(x, gam, bet)
+
+    def run():
+        out = {}
+        out["ln"] = Kk.layernorm_bwd(x, dy, gam, mu, rstd, dres=f)
+        out["res"] = Kk.residual_bwd(dy, f, ls, rs, H * W)
+        out["dw3"] = Kk.dwconv_bwd(x, dy, (B, H, W), w3, 3, add_identity=True)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            out["dw7"] = Kk.dwconv_bwd_weight(x, dy, (B, H, W), 7)
+        torch.cuda.current_stream().wait_stream(side)
+        return out
+
+    ref = run()
+    with Kk.wgrad_group():
+        got = run()
+    torch.cuda.synchronize()
+    for k in ref:
+        for a, b in zip(got[k], ref[k]):
+            assert torch.equal(a, b), k
