@@ -392,6 +392,97 @@ __global__ void attn_fwd_combine_kernel(AttnArgs a) {
   }
 }
 
+// Combine for the MFMA path (dh % 4 == 0): one thread per (b, h, query, 4 dims) reads its partials as
+// float4 and walks the chunks 4 at a time with independent maxima / sums, so a thread's loads of a
+// group of chunks are in flight together instead of one dependent load per chunk.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_combine_v4_kernel(AttnArgs a) {
+  const int d4n = a.dh / 4;
+  const long n = (long)a.B * a.heads * NQ * d4n;
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  if (e >= n) return;
+  const int d = (int)(e % d4n) * 4;
+  const long bhq = e / d4n;
+  const int qi = bhq % NQ;
+  const long bh = bhq / NQ;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const float* pm = a.ws + (long)a.B * a.heads * a.nchunk * NQ * a.dh;
+  const float* pl = pm + (long)a.B * a.heads * a.nchunk * NQ;
+  const long i0 = bh * a.nchunk * NQ + qi;  // partial (chunk c) at i0 + c * NQ
+  const int nc = a.nchunk, nc4 = nc & ~3;
+  float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int c = 0; c < nc4; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m4[u] = fmaxf(m4[u], pm[i0 + (long)(c + u) * NQ]);
+  }
+  for (int c = nc4; c < nc; ++c) m4[0] = fmaxf(m4[0], pm[i0 + (long)c * NQ]);
+  const float M = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+  float L4[4] = {0.f, 0.f, 0.f, 0.f};
+  float4 O4[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) O4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto acc = [&](int u, int c) {
+    const long idx = i0 + (long)c * NQ;
+    const float f = __expf(pm[idx] - M);
+    const float4 o = *reinterpret_cast<const float4*>(a.ws + idx * a.dh + d);
+    L4[u] += pl[idx] * f;
+    O4[u].x += o.x * f;
+    O4[u].y += o.y * f;
+    O4[u].z += o.z * f;
+    O4[u].w += o.w * f;
+  };
+  for (int c = 0; c < nc4; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc(u, c + u);
+  }
+  for (int c = nc4; c < nc; ++c) acc(0, c);
+  const float L = (L4[0] + L4[1]) + (L4[2] + L4[3]);
+  const float inv = 1.0f / L;
+  float ov[4] = {((O4[0].x + O4[1].x) + (O4[2].x + O4[3].x)) * inv, ((O4[0].y + O4[1].y) + (O4[2].y + O4[3].y)) * inv,
+                 ((O4[0].z + O4[1].z) + (O4[2].z + O4[3].z)) * inv, ((O4[0].w + O4[1].w) + (O4[2].w + O4[3].w)) * inv};
+  T* op = (T*)a.o + ((long)b * NQ + qi) * a.ldo + h * a.dh + d;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) stf(op + u, ov[u]);
+  if (d == 0) a.lse[bhq] = M + __logf(L);
+}
+
+// dQ = sum over chunks of the per-chunk partials, MFMA path: float4 partials, 4 chunks in flight
+template <typename T>
+__global__ __launch_bounds__(256) void attn_dq_reduce_v4_kernel(AttnArgs a) {
+  const int d4n = a.dh / 4;
+  const long n = (long)a.B * a.heads * NQ * d4n;
+  const long e = blockIdx.x * 256L + threadIdx.x;
+  if (e >= n) return;
+  const int d = (int)(e % d4n) * 4;
+  const long bhq = e / d4n;
+  const int qi = bhq % NQ;
+  const long bh = bhq / NQ;
+  const int h = bh % a.heads, b = bh / a.heads;
+  const float* p0 = a.ws + (bh * a.nchunk * NQ + qi) * a.dh + d;
+  const long cs = (long)NQ * a.dh;  // chunk stride
+  const int nc = a.nchunk, nc4 = nc & ~3;
+  float4 s4[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) s4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [&](int u, int c) {
+    const float4 v = *reinterpret_cast<const float4*>(p0 + c * cs);
+    s4[u].x += v.x;
+    s4[u].y += v.y;
+    s4[u].z += v.z;
+    s4[u].w += v.w;
+  };
+  for (int c = 0; c < nc4; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add(u, c + u);
+  }
+  for (int c = nc4; c < nc; ++c) add(0, c);
+  const float ov[4] = {(s4[0].x + s4[1].x) + (s4[2].x + s4[3].x), (s4[0].y + s4[1].y) + (s4[2].y + s4[3].y),
+                       (s4[0].z + s4[1].z) + (s4[2].z + s4[3].z), (s4[0].w + s4[1].w) + (s4[2].w + s4[3].w)};
+  T* qp = (T*)a.dq + ((long)b * NQ + qi) * a.ldq + h * a.dh + d;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) stf(qp + u, ov[u]);
+}
+
 // backward per chunk: recompute P, dV = P^T dO, dP = dO V^T, dS = P (dP - D), dK = scale dS^T Q,
 // dQ_partial = scale dS K.
 template <typename T>
@@ -1050,13 +1141,15 @@ static void attn_mfma(int dtype, AttnArgs& a, bool bwd, hipStream_t s) {
   if (dtype == DFM_F16) attn_mfma_t<f16_t>(a, bwd, s);
   else attn_mfma_t<bf16_t>(a, bwd, s);
 }
-static void attn_combine16(int dtype, AttnArgs& a, unsigned g, hipStream_t s) {
-  if (dtype == DFM_F16) DFM_LAUNCH(attn_fwd_combine_kernel<f16_t>, dim3(g), dim3(256), 0, s, a);
-  else DFM_LAUNCH(attn_fwd_combine_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+static void attn_combine16(int dtype, AttnArgs& a, hipStream_t s) {
+  const dim3 g(cdiv((long)a.B * a.heads * NQ * (a.dh / 4), 256));
+  if (dtype == DFM_F16) DFM_LAUNCH(attn_fwd_combine_v4_kernel<f16_t>, g, dim3(256), 0, s, a);
+  else DFM_LAUNCH(attn_fwd_combine_v4_kernel<bf16_t>, g, dim3(256), 0, s, a);
 }
-static void attn_dq_reduce16(int dtype, AttnArgs& a, unsigned g, hipStream_t s) {
-  if (dtype == DFM_F16) DFM_LAUNCH(attn_dq_reduce_kernel<f16_t>, dim3(g), dim3(256), 0, s, a);
-  else DFM_LAUNCH(attn_dq_reduce_kernel<bf16_t>, dim3(g), dim3(256), 0, s, a);
+static void attn_dq_reduce16(int dtype, AttnArgs& a, hipStream_t s) {
+  const dim3 g(cdiv((long)a.B * a.heads * NQ * (a.dh / 4), 256));
+  if (dtype == DFM_F16) DFM_LAUNCH(attn_dq_reduce_v4_kernel<f16_t>, g, dim3(256), 0, s, a);
+  else DFM_LAUNCH(attn_dq_reduce_v4_kernel<bf16_t>, g, dim3(256), 0, s, a);
 }
 
 static size_t attn_partials_bytes(int B, int heads, int N, int dh) {
@@ -1100,7 +1193,7 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
     a.dh = dp; a.q = pq; a.ldq = ldp; a.k = pk; a.v = pv; a.ldkv = ldp; a.o = po; a.ldo = ldp;
     a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
     attn_mfma(dtype, a, false, s);
-    attn_combine16(dtype, a, grid_for((long)B * heads * NQ * dp), s);
+    attn_combine16(dtype, a, s);
     head_repack((long)B * NQ, heads, dp, ldp, dh, ldo, po, o, s);
     DFM_LAUNCH_CHECK();
     return DFM_OK;
@@ -1112,7 +1205,7 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
       attn_mfma(dtype, a, false, s);
       DFM_LAUNCH_CHECK();
-      attn_combine16(dtype, a, grid_for((long)B * heads * NQ * dh), s);
+      attn_combine16(dtype, a, s);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
@@ -1172,7 +1265,7 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
     a.dout = pdo; a.lddo = ldp; a.dq = pdq; a.dk = pdk; a.dv = pdv; a.lddkv = ldp;
     a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
     attn_mfma(dtype, a, true, s);
-    attn_dq_reduce16(dtype, a, grid_for((long)B * heads * NQ * dp), s);
+    attn_dq_reduce16(dtype, a, s);
     head_repack((long)B * NQ, heads, dp, ldp, dh, ldq, pdq, dq, s);
     head_repack((long)B * N, heads, dp, ldp, dh, lddkv, pdk, dk, s);
     head_repack((long)B * N, heads, dp, ldp, dh, lddkv, pdv, dv, s);
@@ -1186,7 +1279,7 @@ extern "C" int dfm_pooled_attn_bwd(int dtype, int B, int heads, int N, int dh, c
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
       attn_mfma(dtype, a, true, s);
       DFM_LAUNCH_CHECK();
-      attn_dq_reduce16(dtype, a, grid_for((long)B * heads * NQ * dh), s);
+      attn_dq_reduce16(dtype, a, s);
       DFM_LAUNCH_CHECK();
       return DFM_OK;
     }
