@@ -654,27 +654,45 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt) o[dt][nt] = float4_t{0.f, 0.f, 0.f, 0.f};
   }
-  for (int kb = n0; kb < n1; kb += 32) {
-    // V block -> LDS [key][d] (zero rows past the chunk)
-    constexpr int VCH = DH / 8;
+  // the next 32-key block's V rows and K fragments are loaded into registers while this block is
+  // multiplied (one global round trip per block hidden behind the MFMAs instead of paid in series)
+  constexpr int VCH = DH / 8, VIT = (32 * VCH + 63) / 64;
+  uint4 vreg[VIT];
+  bf16x8_t kf[2][KD];
+  auto load_block = [&](int kb, uint4 (&vr)[VIT], bf16x8_t (&kr)[2][KD]) {
 #pragma unroll
-    for (int it = 0; it < (32 * VCH + 63) / 64; ++it) {
+    for (int it = 0; it < VIT; ++it) {
       const int idx = lane + 64 * it;
-      if (idx < 32 * VCH) {
-        const int key = idx / VCH, ch = idx % VCH;
-        const uint4 u = kb + key < n1 ? *reinterpret_cast<const uint4*>(V + (long)(kb + key) * a.ldkv + ch * 8)
-                                      : make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(sv + key * LDV + ch * 8) = u;
-      }
+      const int key = idx / VCH, ch = idx % VCH;
+      vr[it] = idx < 32 * VCH && kb + key < n1
+                   ? *reinterpret_cast<const uint4*>(V + (long)(kb + key) * a.ldkv + ch * 8)
+                   : make_uint4(0, 0, 0, 0);
     }
-    bf16x8_t kf[2][KD];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ks = 0; ks < KD; ++ks) {
         const int key = kb + 8 * (j >> 2) + 4 * t + (j & 3), d0 = 32 * ks + 8 * g;
-        kf[t][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+        kr[t][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
       }
+  };
+  if (n0 < n1) load_block(n0, vreg, kf);
+  for (int kb = n0; kb < n1; kb += 32) {
+    // V block -> LDS [key][d] (zero rows past the chunk)
+#pragma unroll
+    for (int it = 0; it < VIT; ++it) {
+      const int idx = lane + 64 * it;
+      if (idx < 32 * VCH) {
+        const int key = idx / VCH, ch = idx % VCH;
+        *reinterpret_cast<uint4*>(sv + key * LDV + ch * 8) = vreg[it];
+      }
+    }
+    bf16x8_t kc[2][KD];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < KD; ++ks) kc[t][ks] = kf[t][ks];
+    if (kb + 32 < n1) load_block(kb + 32, vreg, kf);
     float4_t st[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -682,7 +700,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
       for (int nt = 0; nt < 4; ++nt) {
         float4_t acc = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KD; ++ks) acc = MFMA16(kf[t][ks], qf[nt][ks], acc);
+        for (int ks = 0; ks < KD; ++ks) acc = MFMA16(kc[t][ks], qf[nt][ks], acc);
         st[t][nt] = acc;
       }
     bf16x8_t pf[4];
@@ -828,26 +846,48 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) dq[dt][nt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-  for (int kb = n0; kb < n1; kb += 32) {
+  // the next 32-key block's K rows and K / V fragments are loaded into registers while this block
+  // is processed (its global round trip hidden behind the MFMAs)
+  constexpr int KIT = (32 * VCH + 63) / 64;
+  uint4 kreg[KIT];
+  bf16x8_t kn[2][KD], vn[2][KD];  // B (k = d, n = key)
+  auto load_block = [&](int kb) {
 #pragma unroll
-    for (int it = 0; it < (32 * VCH + 63) / 64; ++it) {  // K block -> LDS [key][d]
+    for (int it = 0; it < KIT; ++it) {
       const int idx = lane + 64 * it;
-      if (idx < 32 * VCH) {
-        const int key = idx / VCH, ch = idx % VCH;
-        const uint4 u = kb + key < n1 ? *reinterpret_cast<const uint4*>(K + (long)(kb + key) * a.ldkv + ch * 8)
-                                      : make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(sk + key * LDD + ch * 8) = u;
-      }
+      const int key = idx / VCH, ch = idx % VCH;
+      kreg[it] = idx < 32 * VCH && kb + key < n1
+                     ? *reinterpret_cast<const uint4*>(K + (long)(kb + key) * a.ldkv + ch * 8)
+                     : make_uint4(0, 0, 0, 0);
     }
-    bf16x8_t kf[2][KD], vf[2][KD];  // B (k = d, n = key)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int ks = 0; ks < KD; ++ks) {
         const int key = kb + 16 * kt + j, d0 = 32 * ks + 8 * g;
-        kf[kt][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
-        vf[kt][ks] = ldfrag16(V + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+        kn[kt][ks] = ldfrag16(K + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
+        vn[kt][ks] = ldfrag16(V + (long)key * a.ldkv + d0, key < n1 && d0 < DH);
       }
+  };
+  if (n0 < n1) load_block(n0);
+  for (int kb = n0; kb < n1; kb += 32) {
+#pragma unroll
+    for (int it = 0; it < KIT; ++it) {  // K block -> LDS [key][d]
+      const int idx = lane + 64 * it;
+      if (idx < 32 * VCH) {
+        const int key = idx / VCH, ch = idx % VCH;
+        *reinterpret_cast<uint4*>(sk + key * LDD + ch * 8) = kreg[it];
+      }
+    }
+    bf16x8_t kf[2][KD], vf[2][KD];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int ks = 0; ks < KD; ++ks) {
+        kf[kt][ks] = kn[kt][ks];
+        vf[kt][ks] = vn[kt][ks];
+      }
+    if (kb + 32 < n1) load_block(kb + 32);
     bf16x8_t pb[2][2], dsb[2][2];  // [kt][qb]: B (k = q 32qb + 8g + e, n = key 16kt + j)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
