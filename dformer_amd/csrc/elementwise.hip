@@ -3,6 +3,8 @@
 // All reductions are two-stage with fixed order (deterministic, no float atomics).
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -733,6 +735,51 @@ extern "C" int dfm_scale_mul(int dtype, long rows, int C, const void* src, long 
   DFM_CHECK_ARG(src && dst, "dfm_scale_mul: null argument");
   return ew2d<0>(dtype, rows, C, src, ldsrc, mul, ldmul, colscale, rowscale, rps, alpha, dst, lddst, accumulate,
                  (hipStream_t)stream);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void group_scale_kernel(long rows, int C, const T* __restrict__ x, long ldx,
+                                                          const float* __restrict__ scale, long rpg, T* y, long ldy) {
+  const int nv = C / 8;
+  const long n = rows * nv;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const long r = i / nv;
+    const int c = (int)(i - r * nv) * 8;
+    const float* sc = scale + (r / rpg) * C + c;
+    float v[8];
+    ld8<T>(x + r * ldx + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= sc[e];
+    st8<T>(y + r * ldy + c, v);
+  }
+}
+
+extern "C" int dfm_group_scale(int dtype, long rows, int C, const void* x, long ldx, const float* scale,
+                               long rows_per_group, void* y, long ldy, dfm_stream_t stream) {
+  DFM_CHECK_ARG(x && y && scale && rows_per_group > 0 && C > 0, "dfm_group_scale: bad argument");
+  DFM_CHECK_ARG(dtype == DFM_BF16 || dtype == DFM_F16 || dtype == DFM_F32, "dfm_group_scale: bad dtype %d", dtype);
+  if (rows == 0) return DFM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const bool vec = C % 8 == 0 && ew_al<float>(x, ldx) && ew_al<float>(y, ldy);
+  if (!vec || dtype == DFM_F32) {  // fp32 / unaligned: the elementwise path, one group at a time
+    for (long r0 = 0; r0 < rows; r0 += rows_per_group) {
+      const long n = std::min(rows_per_group, rows - r0);
+      const long eb = dtype == DFM_F32 ? 4 : 2;
+      const int rc = ew2d<0>(dtype, n, C, (const char*)x + r0 * ldx * eb, ldx, nullptr, 0,
+                             scale + (r0 / rows_per_group) * C, nullptr, 1, 1.f, (char*)y + r0 * ldy * eb, ldy, 0, s);
+      if (rc) return rc;
+    }
+    return DFM_OK;
+  }
+  const unsigned g = ew_grid(rows * C / 8);
+  if (dtype == DFM_BF16)
+    DFM_LAUNCH(group_scale_kernel<bf16_t>, dim3(g), dim3(256), 0, s, rows, C, (const bf16_t*)x, ldx, scale,
+               rows_per_group, (bf16_t*)y, ldy);
+  else
+    DFM_LAUNCH(group_scale_kernel<f16_t>, dim3(g), dim3(256), 0, s, rows, C, (const f16_t*)x, ldx, scale,
+               rows_per_group, (f16_t*)y, ldy);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
 }
 
 extern "C" int dfm_dual_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* m1, long ld1,

@@ -1176,12 +1176,20 @@ void pick_tile(const DfmGemmDesc* d, int& BM, int& BN) {
 // elements per split, rounded down to a power of two (fitted on the DFormer-B step's GEMM census,
 // tools/gemm_sweep.py).
 int choose_splits(const DfmGemmDesc* d, int elem_bytes) {
-  (void)elem_bytes;
   if (d->split_k >= 1) return d->split_k;
   int BM, BN;
   pick_tile(d, BM, BN);
   const int Nw = d->N + (d->colsum ? 1 : 0);
   const long tiles = (long)cdiv(d->M, BM) * cdiv(Nw, BN) * (d->batch > 0 ? d->batch : 1);
+  if (elem_bytes == 4 && d->batch > 1 && tiles < 64 && d->K >= 256) {
+    // batched fp32 products with one tile per batch over a long K (the NMF's R x R Gram products,
+    // ham_head.py:88-109): ~512 blocks of >= 128 reduction elements instead of one serial k-loop
+    // per batch (one 64 x 64 x 512 tile took 28 us)
+    long s = std::min((512 + tiles - 1) / tiles, (long)d->K / 128);
+    int p = 1;
+    while (2L * p <= s && p < 1024) p *= 2;
+    return p;
+  }
   if (d->K < 1024 || tiles >= 256) return 1;
   long s = std::min((256 + tiles - 1) / tiles, (long)d->K / 512);
   int p = 1;

@@ -211,11 +211,8 @@ class ChannelDropoutLinearFn(torch.autograd.Function):
     def forward(ctx, x, scale, B, w, b):
         dt = x.dtype
         xs = x
-        if scale is not None:  # [B, C] per-image channel scale
-            xs = torch.empty_like(x)
-            rows = x.shape[0] // B
-            for i in range(B):
-                K.scale_mul(x[i * rows:(i + 1) * rows], colscale=scale[i], out=xs[i * rows:(i + 1) * rows])
+        if scale is not None:  # [B, C] per-image channel scale, one launch
+            xs = K.group_scale(x, scale.contiguous(), x.shape[0] // B)
         y = K.linear(xs, wcast(dt, w), b)
         ctx.save_for_backward(xs, w, b, scale)
         ctx.B = B
@@ -231,9 +228,7 @@ class ChannelDropoutLinearFn(torch.autograd.Function):
         dW, db = K.linear_wgrad(dy, xs, out=gslot2(w), bias_grad=True, bias_out=gslot(b))
         dx = K.linear_dgrad(dy, wcast(xs.dtype, w))
         if scale is not None:
-            rows = dx.shape[0] // ctx.B
-            for i in range(ctx.B):
-                K.scale_mul(dx[i * rows:(i + 1) * rows], colscale=scale[i], out=dx[i * rows:(i + 1) * rows])
+            K.group_scale(dx, scale.contiguous(), dx.shape[0] // ctx.B, out=dx)
         return dx, None, None, dW.view_as(w), db
 
 

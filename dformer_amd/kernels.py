@@ -458,6 +458,19 @@ def scale_mul(src, mul=None, colscale=None, rowscale=None, rows_per_scale=1, alp
     return out
 
 
+def group_scale(x, scale, rows_per_group, out=None):
+    """out[r, c] = x[r, c] * scale[r // rows_per_group, c] (float32 scale [groups, C]); out may be x."""
+    rows, C = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    assert scale.dtype == torch.float32 and scale.is_contiguous() and scale.numel() >= -(-rows // rows_per_group) * C
+    check(lib.dfm_group_scale(dtype_code(x), rows, C, ptr(x), ld(x), ptr(scale), rows_per_group, ptr(out), ld(out),
+                              stream()), "dfm_group_scale")
+    if ACCOUNT is not None:
+        _acct(0, rows * C * _es(x) * 2)
+    return out
+
+
 def dual_mul(src, m1, m2, out1=None, out2=None):
     """(src * m1, src * m2) in one pass over src (the two gradients of an elementwise product)."""
     rows, C = src.shape

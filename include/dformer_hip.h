@@ -209,6 +209,11 @@ int dfm_scale_mul(int dtype, long rows, int C, const void* src, long ldsrc, cons
                   const float* colscale, const float* rowscale, long rows_per_scale, float alpha,
                   void* dst, long lddst, int accumulate, dfm_stream_t stream);
 
+/* y[r, c] = x[r, c] * scale[(r / rows_per_group) * C + c]: a per-group channel scale in one launch
+ * (Dropout2d's per-image channel mask / keep ahead of the classifier, decode_head.py:226-231, and its
+ * backward; y may alias x). */
+int dfm_group_scale(int dtype, long rows, int C, const void* x, long ldx, const float* scale,
+                    long rows_per_group, void* y, long ldy, dfm_stream_t stream);
 /* o1 = src * m1, o2 = src * m2 in one pass over src: the gradients of an elementwise product
  * d(q*a) -> (d*a, d*q), d(cx*xe') -> (d*xe', d*cx) (DFormer.py:134-135 backward). */
 int dfm_dual_mul(int dtype, long rows, int C, const void* src, long ldsrc, const void* m1, long ld1, const void* m2,

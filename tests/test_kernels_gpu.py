@@ -782,3 +782,20 @@ def test_deferred_reductions_bit_identical(dt):
     for k in ref:
         for a, b in zip(got[k], ref[k]):
             assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_group_scale(dt):
+    """dfm_group_scale: per-group (per-image) channel scale in one launch, in place and strided."""
+    Kk = K()
+    B, rows, C = 4, 300, 96
+    x = torch.randn(B * rows, C, device=DEV).to(dt)
+    sc = torch.rand(B, C, device=DEV)
+    ref = (x.float().view(B, rows, C) * sc[:, None, :]).view(B * rows, C)
+    got = Kk.group_scale(x, sc, rows)
+    assert rel(got.float(), ref) <= TOL[dt] / 4
+    wide = torch.randn(B * rows, C + 32, device=DEV).to(dt)
+    v = wide[:, 16:16 + C]
+    exp = (v.float().view(B, rows, C) * sc[:, None, :]).view(B * rows, C)
+    Kk.group_scale(v, sc, rows, out=v)
+    assert rel(v.float(), exp) <= TOL[dt] / 4
