@@ -935,6 +935,191 @@ extern "C" int dfm_nmf_update_bwd(long n, const float* g, const float* a, const 
   return DFM_OK;
 }
 
+// ---- NMF updates with the R x R denominator products fused (R = 64). A block owns 64 rows of one
+// batch; the 64 x 64 row tile (transposed: [k][row]) and the Gram matrices sit in LDS, and thread
+// (ty, tx) computes a 4 x 4 block of the row-by-Gram product (4 + 4 operands per k for 16 FMAs).
+constexpr int NMF_R = 64, NMF_P = 68;  // rank, LDS pitch (floats)
+
+DFM_INLINE void nmf_tile_t(float* sT, const float* src, long rows, long n0) {  // sT[k][r] = src[n0 + r][k]
+  for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+    const int r = i / 16, k4 = (i % 16) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (n0 + r < rows) v = *reinterpret_cast<const float4*>(src + (n0 + r) * NMF_R + k4);
+    sT[(k4 + 0) * NMF_P + r] = v.x;
+    sT[(k4 + 1) * NMF_P + r] = v.y;
+    sT[(k4 + 2) * NMF_P + r] = v.z;
+    sT[(k4 + 3) * NMF_P + r] = v.w;
+  }
+}
+DFM_INLINE void nmf_gram(float* sG, const float* G, bool sym) {  // sG[k][c] = G[k][c] (+ G[c][k])
+  for (int i = threadIdx.x; i < 64 * 16; i += 256) {
+    const int k = i / 16, c4 = (i % 16) * 4;
+    float4 v = *reinterpret_cast<const float4*>(G + k * NMF_R + c4);
+    if (sym) {
+      v.x += G[(c4 + 0) * NMF_R + k];
+      v.y += G[(c4 + 1) * NMF_R + k];
+      v.z += G[(c4 + 2) * NMF_R + k];
+      v.w += G[(c4 + 3) * NMF_R + k];
+    }
+    *reinterpret_cast<float4*>(sG + k * NMF_P + c4) = v;
+  }
+}
+DFM_INLINE void nmf_rowmm(float (&acc)[4][4], const float* sT, const float* sG, int ty, int tx) {
+#pragma unroll 8
+  for (int k = 0; k < NMF_R; ++k) {
+    const float4 av = *reinterpret_cast<const float4*>(sT + k * NMF_P + 4 * ty);
+    const float4 gv = *reinterpret_cast<const float4*>(sG + k * NMF_P + 4 * tx);
+    const float ar[4] = {av.x, av.y, av.z, av.w}, gc[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(ar[i], gc[j], acc[i][j]);
+  }
+}
+
+template <typename TC>
+__global__ __launch_bounds__(256) void nmf_update_mm_kernel(long rows, const float* __restrict__ a,
+                                                            const float* __restrict__ num, const float* __restrict__ M,
+                                                            float eps, float* __restrict__ den, float* __restrict__ out,
+                                                            TC* __restrict__ out16) {
+  __shared__ __attribute__((aligned(16))) float sT[NMF_R * NMF_P], sG[NMF_R * NMF_P];
+  const long b = blockIdx.y, n0 = (long)blockIdx.x * 64, off = b * rows * NMF_R;
+  nmf_gram(sG, M + b * NMF_R * NMF_R, false);
+  nmf_tile_t(sT, a + off, rows, n0);
+  __syncthreads();
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  float acc[4][4] = {};
+  nmf_rowmm(acc, sT, sG, ty, tx);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long n = n0 + 4 * ty + i;
+    if (n >= rows) break;
+    const long e = off + n * NMF_R + 4 * tx;
+    const float4 av = *reinterpret_cast<const float4*>(a + e), nv = *reinterpret_cast<const float4*>(num + e);
+    const float ar[4] = {av.x, av.y, av.z, av.w}, nr[4] = {nv.x, nv.y, nv.z, nv.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = ar[j] * nr[j] / (acc[i][j] + eps);
+    *reinterpret_cast<float4*>(den + e) = make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    *reinterpret_cast<float4*>(out + e) = make_float4(o[0], o[1], o[2], o[3]);
+    if (out16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out16[e + j] = Num<TC>::from_f(o[j]);
+    }
+  }
+}
+
+template <typename TC>
+__global__ __launch_bounds__(256) void nmf_update_bwd_mm_kernel(
+    long rows, const float* __restrict__ g, const float* __restrict__ A2, const float* __restrict__ S,
+    const float* __restrict__ a, const float* __restrict__ num, const float* __restrict__ den,
+    const float* __restrict__ out, float eps, const float* __restrict__ Mg, float* __restrict__ ga, int acc_ga,
+    float* __restrict__ gnum, float* __restrict__ gden, TC* __restrict__ gnum16) {
+  __shared__ __attribute__((aligned(16))) float sT[NMF_R * NMF_P], sS[NMF_R * NMF_P], sM[NMF_R * NMF_P];
+  const long b = blockIdx.y, n0 = (long)blockIdx.x * 64, off = b * rows * NMF_R;
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  if (A2) {
+    nmf_gram(sS, S + b * NMF_R * NMF_R, true);
+    nmf_tile_t(sT, A2 + off, rows, n0);
+  }
+  if (Mg) nmf_gram(sM, Mg + b * NMF_R * NMF_R, false);
+  __syncthreads();
+  float ge[4][4] = {};
+  if (A2) nmf_rowmm(ge, sT, sS, ty, tx);
+  float gd[4][4] = {}, gav[4][4] = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long n = n0 + 4 * ty + i;
+    if (n >= rows) break;
+    const long e = off + n * NMF_R + 4 * tx;
+    const float4 gv = *reinterpret_cast<const float4*>(g + e), av = *reinterpret_cast<const float4*>(a + e);
+    const float4 nv = *reinterpret_cast<const float4*>(num + e), dv = *reinterpret_cast<const float4*>(den + e);
+    const float4 ov = *reinterpret_cast<const float4*>(out + e);
+    const float gr[4] = {gv.x, gv.y, gv.z, gv.w}, ar[4] = {av.x, av.y, av.z, av.w}, nr[4] = {nv.x, nv.y, nv.z, nv.w};
+    const float dr[4] = {dv.x, dv.y, dv.z, dv.w}, orr[4] = {ov.x, ov.y, ov.z, ov.w};
+    float gn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gi = gr[j] + ge[i][j];
+      const float r = 1.f / (dr[j] + eps);
+      gav[i][j] = gi * nr[j] * r;
+      gn[j] = gi * ar[j] * r;
+      gd[i][j] = -gi * orr[j] * r;
+    }
+    *reinterpret_cast<float4*>(gnum + e) = make_float4(gn[0], gn[1], gn[2], gn[3]);
+    *reinterpret_cast<float4*>(gden + e) = make_float4(gd[i][0], gd[i][1], gd[i][2], gd[i][3]);
+    if (gnum16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gnum16[e + j] = Num<TC>::from_f(gn[j]);
+    }
+  }
+  if (Mg) {  // ga += gden Mg: this block's gden rows, transposed into the tile buffer
+    __syncthreads();  // every thread is done reading the A2 tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sT[(4 * tx + j) * NMF_P + 4 * ty + i] = gd[i][j];
+    __syncthreads();
+    nmf_rowmm(gav, sT, sM, ty, tx);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long n = n0 + 4 * ty + i;
+    if (n >= rows) break;
+    const long e = off + n * NMF_R + 4 * tx;
+    float4 v = make_float4(gav[i][0], gav[i][1], gav[i][2], gav[i][3]);
+    if (acc_ga) {
+      const float4 o = *reinterpret_cast<const float4*>(ga + e);
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *reinterpret_cast<float4*>(ga + e) = v;
+  }
+}
+
+static bool nmf_mm_al(const void* p) { return p == nullptr || (uintptr_t)p % 16 == 0; }
+
+extern "C" int dfm_nmf_update_mm(int batch, long rows, int R, const float* a, const float* num, const float* M,
+                                 float eps, float* den, float* out, void* out16, int copy_dtype, dfm_stream_t stream) {
+  DFM_CHECK_ARG(R == NMF_R, "dfm_nmf_update_mm: R=%d unsupported (64 only)", R);
+  DFM_CHECK_ARG(batch > 0 && rows >= 0 && a && num && M && den && out, "dfm_nmf_update_mm: bad argument");
+  DFM_CHECK_ARG(!out16 || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_nmf_update_mm: bad copy dtype");
+  DFM_CHECK_ARG(nmf_mm_al(a) && nmf_mm_al(num) && nmf_mm_al(M) && nmf_mm_al(den) && nmf_mm_al(out),
+                "dfm_nmf_update_mm: 16-byte aligned operands required");
+  if (rows == 0) return DFM_OK;
+  const dim3 grid(cdiv(rows, 64), batch);
+  hipStream_t s = (hipStream_t)stream;
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(nmf_update_mm_kernel<f16_t>, grid, dim3(256), 0, s, rows, a, num, M, eps, den, out, (f16_t*)out16);
+  else
+    DFM_LAUNCH(nmf_update_mm_kernel<bf16_t>, grid, dim3(256), 0, s, rows, a, num, M, eps, den, out, (bf16_t*)out16);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+extern "C" int dfm_nmf_update_bwd_mm(int batch, long rows, int R, const float* g, const float* A2, const float* S,
+                                     const float* a, const float* num, const float* den, const float* out, float eps,
+                                     const float* Mg, float* ga, int accumulate_ga, float* gnum, float* gden,
+                                     void* gnum16, int copy_dtype, dfm_stream_t stream) {
+  DFM_CHECK_ARG(R == NMF_R, "dfm_nmf_update_bwd_mm: R=%d unsupported (64 only)", R);
+  DFM_CHECK_ARG(batch > 0 && rows >= 0 && g && a && num && den && out && ga && gnum && gden && (!A2 || S),
+                "dfm_nmf_update_bwd_mm: bad argument");
+  DFM_CHECK_ARG(!gnum16 || copy_dtype == DFM_BF16 || copy_dtype == DFM_F16, "dfm_nmf_update_bwd_mm: bad copy dtype");
+  DFM_CHECK_ARG(nmf_mm_al(g) && nmf_mm_al(A2) && nmf_mm_al(S) && nmf_mm_al(a) && nmf_mm_al(num) && nmf_mm_al(den) &&
+                    nmf_mm_al(out) && nmf_mm_al(Mg) && nmf_mm_al(ga) && nmf_mm_al(gnum) && nmf_mm_al(gden),
+                "dfm_nmf_update_bwd_mm: 16-byte aligned operands required");
+  if (rows == 0) return DFM_OK;
+  const dim3 grid(cdiv(rows, 64), batch);
+  hipStream_t s = (hipStream_t)stream;
+  if (copy_dtype == DFM_F16)
+    DFM_LAUNCH(nmf_update_bwd_mm_kernel<f16_t>, grid, dim3(256), 0, s, rows, g, A2, S, a, num, den, out, eps, Mg, ga,
+               accumulate_ga, gnum, gden, (f16_t*)gnum16);
+  else
+    DFM_LAUNCH(nmf_update_bwd_mm_kernel<bf16_t>, grid, dim3(256), 0, s, rows, g, A2, S, a, num, den, out, eps, Mg, ga,
+               accumulate_ga, gnum, gden, (bf16_t*)gnum16);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
 extern "C" int dfm_grad_nonfinite(long n, const float* g, int* flag, dfm_stream_t stream) {
   DFM_CHECK_ARG(g && flag && n >= 0, "dfm_grad_nonfinite: bad argument");
   if (n == 0) return DFM_OK;

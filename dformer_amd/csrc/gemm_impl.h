@@ -1270,6 +1270,9 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 128);
     if (glds_ok && route && !a.stream) {
       if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
+      // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
+      // (438.7-438.4 -> 439.0-440.3 images/s on one box; 65-93 vs 81-127 us per launch alone)
+      if (a.splits == 1 && d->M >= 65536 && a.Nw >= 512 && d->K >= 512) return glds_ak<128, 128, 8, 2, 2, 2>(a, bk, s);
       return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
     }
   }

@@ -258,21 +258,29 @@ class NMF2DFn(torch.autograd.Function):
         hist = []
         Bt, Ct = B0, coef
         Bt16 = K.cast(B0, x.dtype) if lp else B0
+        fused = B0.shape[2] == 64  # rank 64 (the config's MD_R): the den products fused into the updates
+        ctx.fused = fused
+
+        def update(a, num, G):  # a * num / (a G + eps) -> (out, den, 16-bit copy)
+            if fused:
+                r = K.nmf_update_mm(a, num, G, eps, bf16_copy=x.dtype if lp else False)
+                return r if lp else (r[0], r[1], r[0])
+            den = K.bmm(a, G)
+            o = K.nmf_update(a, num, den, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(a, num, den, eps),) * 2
+            return o[0], den, o[1]
+
         for _ in range(steps):
             num1 = xmm(Bt16)                                      # x^T B        [N,R]
             M = K.bmm(Bt, Bt, a_t=True)                           # B^T B        [R,R]
-            den1 = K.bmm(Ct, M)                                   # C (B^T B)
-            Cn, Cn16 = K.nmf_update(Ct, num1, den1, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Ct, num1, den1, eps),) * 2
+            Cn, den1, Cn16 = update(Ct, num1, M)                  # den1 = C (B^T B)
             num2 = xmm(Cn16, a_t=True)                            # x C          [D,R]
             Q = K.bmm(Cn, Cn, a_t=True)                           # C^T C        [R,R]
-            den2 = K.bmm(Bt, Q)                                   # B (C^T C)
-            Bn, Bn16 = K.nmf_update(Bt, num2, den2, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Bt, num2, den2, eps),) * 2
+            Bn, den2, Bn16 = update(Bt, num2, Q)                  # den2 = B (C^T C)
             hist.append((Bt, Ct, num1, M, den1, Cn, Cn16, num2, Q, den2, Bn))
             Bt, Ct, Bt16 = Bn, Cn, Bn16
         num = xmm(Bt16)
         M = K.bmm(Bt, Bt, a_t=True)
-        den = K.bmm(Ct, M)
-        Cf, Cf16 = K.nmf_update(Ct, num, den, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(Ct, num, den, eps),) * 2
+        Cf, den, Cf16 = update(Ct, num, M)
         y = K.bmm(Cf16, Bt16, b_t=True)                           # (B C^T)^T    [N,D], x.dtype
         ctx.hist = hist
         ctx.final = (Bt, Bt16, Ct, num, M, den, Cf, Cf16)
@@ -308,6 +316,47 @@ class NMF2DFn(torch.autograd.Function):
             Ps.append(P)
             Qs.append(Q)
 
+        if ctx.fused:
+            # the den products' gradients ride in the fused update kernels: each C / B update's
+            # gden M (gden Q) is added to its ga in place, and the symmetric Gram gradients
+            # B (gM + gM^T) / C (gQ + gQ^T) are folded into the g of the update that consumes them
+            def upd_mm(g, a, nm, dn, out, A2=None, S=None, Mg=None):
+                r = K.nmf_update_bwd_mm(g, a, nm, dn, out, A2=A2, S=S, Mg=Mg, eps=eps,
+                                        bf16_copy=x.dtype if lp else False)
+                return r if lp else (*r, r[1])
+
+            gCt, gnum, gden, gnum16 = upd_mm(gC, Ct, num, den, Cf, Mg=M)   # + gden M
+            gx_term(gnum, Bt)                                             # gx += gnum B^T
+            K.bmm(x, gnum16, a_t=True, out=gB, beta=1.0)                  # gB += x^T gnum
+            pend = (Bt, K.bmm(Ct, gden, a_t=True))                        # gB += Bt (gM + gM^T)
+            gC = gCt
+            for (Bp, Cp, num1, M1, den1, Cn, Cn16, num2, Q, den2, Bn) in reversed(ctx.hist):
+                assert pend[0] is Bn
+                gBp, gnum2, gden2, gnum2_16 = upd_mm(gB, Bp, num2, den2, Bn, A2=pend[0], S=pend[1], Mg=Q)
+                gx_term(Cn, gnum2)                                        # gx += Cn gnum2^T
+                K.bmm(x, gnum2_16, out=gC, beta=1.0)                      # gCn += x gnum2
+                gQ = K.bmm(Bp, gden2, a_t=True)                           # Bp^T gden2
+                gCp, gnum1, gden1, gnum1_16 = upd_mm(gC, Cp, num1, den1, Cn, A2=Cn, S=gQ, Mg=M1)
+                gx_term(gnum1, Bp)                                        # gx += gnum1 Bp^T
+                K.bmm(x, gnum1_16, a_t=True, out=gBp, beta=1.0)           # gBp += x^T gnum1
+                pend = (Bp, K.bmm(Cp, gden1, a_t=True))
+                gB, gC = gBp, gCp
+            # (the pending Gram term belongs to the random bases B0: no gradient)
+        else:
+            gC = NMF2DFn._backward_unfused(ctx, x, gy, gC, gB, upd_bwd, gx_term)
+        gS = K.softmax_rows_bwd(coef0, gC)
+        gx_term(gS, B0)                                           # gx += gS B0^T
+        assert len(Ps) == T
+        Pc = K.pack_slices(Ps, torch.empty(Bb, N, T * R, device=x.device, dtype=x.dtype))
+        Qc = K.pack_slices(Qs, torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype))
+        gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T, x.dtype
+        ctx.hist = ctx.final = None
+        return gx, None, None, None
+
+    @staticmethod
+    def _backward_unfused(ctx, x, gy, gC, gB, upd_bwd, gx_term):
+        """Backward with every den product a separate batched GEMM (ranks other than 64)."""
+        Bt, Bt16, Ct, num, M, den, Cf, Cf16 = ctx.final
         # final coef update: Cf = Ct * num / (Ct M + eps), num = x B, M = B^T B
         gCt, gnum, gden, gnum16 = upd_bwd(gC, Ct, num, den, Cf)
         gx_term(gnum, Bt)                                         # gx += gnum B^T
@@ -329,15 +378,7 @@ class NMF2DFn(torch.autograd.Function):
             K.bmm(x, gnum1_16, a_t=True, out=gBp, beta=1.0)       # gBp += x^T gnum1
             _acc_CM(gCp, gBp, Cp, Bp, M1, gden1)
             gB, gC = gBp, gCp
-        # coef0 = softmax(x B0)  (B0 is a random constant)
-        gS = K.softmax_rows_bwd(coef0, gC)
-        gx_term(gS, B0)                                           # gx += gS B0^T
-        assert len(Ps) == T
-        Pc = K.pack_slices(Ps, torch.empty(Bb, N, T * R, device=x.device, dtype=x.dtype))
-        Qc = K.pack_slices(Qs, torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype))
-        gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T, x.dtype
-        ctx.hist = ctx.final = None
-        return gx, None, None, None
+        return gC  # coef0 = softmax(x B0)  (B0 is a random constant)
 
 
 def _acc_CM(gC, gB, C, Bt, M, gden):

@@ -778,6 +778,36 @@ def nmf_update_bwd(g, a, num, den, out, ga=None, accumulate=False, eps=1e-6, bf1
     return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
 
 
+def nmf_update_mm(a, num, M, eps=1e-6, bf16_copy=False):
+    """Batched [B, rows, 64] update with its denominator product fused: den = a M, out = a * num /
+    (den + eps). Returns (out, den[, 16-bit copy of out])."""
+    Bb, rows, R = a.shape
+    out, den = torch.empty_like(a), torch.empty_like(a)
+    cdt = _copy_dtype(bf16_copy)
+    o16 = torch.empty(a.shape, device=a.device, dtype=cdt) if cdt is not None else None
+    check(lib.dfm_nmf_update_mm(Bb, rows, R, ptr(a), ptr(num), ptr(M), eps, ptr(den), ptr(out), ptr(o16),
+                                dtype_code(o16) if o16 is not None else 0, stream()), "dfm_nmf_update_mm")
+    if ACCOUNT is not None:
+        _acct(2.0 * a.numel() * R, a.numel() * (16 + 2 * bool(bf16_copy)) + M.numel() * 4)
+    return (out, den, o16) if bf16_copy else (out, den)
+
+
+def nmf_update_bwd_mm(g, a, num, den, out, A2=None, S=None, Mg=None, eps=1e-6, bf16_copy=False):
+    """Backward of nmf_update_mm with g' = g + A2 (S + S^T) and ga = g' num / (den+eps) + gden Mg.
+    Returns (ga, gnum, gden[, 16-bit copy of gnum])."""
+    Bb, rows, R = a.shape
+    ga, gnum, gden = torch.empty_like(a), torch.empty_like(a), torch.empty_like(a)
+    cdt = _copy_dtype(bf16_copy)
+    g16 = torch.empty(a.shape, device=a.device, dtype=cdt) if cdt is not None else None
+    check(lib.dfm_nmf_update_bwd_mm(Bb, rows, R, ptr(g), ptr(A2), ptr(S), ptr(a), ptr(num), ptr(den), ptr(out), eps,
+                                    ptr(Mg), ptr(ga), 0, ptr(gnum), ptr(gden), ptr(g16),
+                                    dtype_code(g16) if g16 is not None else 0, stream()), "dfm_nmf_update_bwd_mm")
+    if ACCOUNT is not None:
+        _acct(2.0 * a.numel() * R * ((A2 is not None) + (Mg is not None)),
+              a.numel() * (4 * (8 + (A2 is not None)) + 2 * bool(bf16_copy)))
+    return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
+
+
 def softmax_rows(x):
     y = torch.empty_like(x)
     check(lib.dfm_softmax_rows(x.numel() // x.shape[-1], x.shape[-1], ptr(x), ptr(y), stream()), "dfm_softmax_rows")

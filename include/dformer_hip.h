@@ -329,6 +329,21 @@ int dfm_nmf_update(long n, const float* a, const float* num, const float* den, f
 int dfm_nmf_update_bwd(long n, const float* g, const float* a, const float* num, const float* den,
                        const float* out, float eps, float* ga, int accumulate_ga, float* gnum, float* gden,
                        void* gnum16, int copy_dtype, dfm_stream_t stream);
+/* The same updates with their rank-R denominator products fused in (R = 64), per batch b and row n
+ * of [batch][rows][R] float32 operands and [batch][R][R] Gram matrices:
+ *   dfm_nmf_update_mm:     den = a M (ham_head.py:120-141's  C (B^T B)  /  B (C^T C)), written;
+ *                          out = a * num / (den + eps) (+ out16).
+ *   dfm_nmf_update_bwd_mm: g' = g [+ A2 (S + S^T)]  (the symmetric Gram gradient of the NEXT update
+ *                          in time, e.g. gC += Cn (gQ + gQ^T), folded into this pass);
+ *                          ga (+=) = g' num / (den+eps) [+ gden Mg]; gnum = g' a / (den+eps) (+ gnum16);
+ *                          gden = -g' out / (den+eps)   (Mg: the Gram matrix of this update's den).
+ * Each replaces one or three row-by-R x R GEMM launches and their [rows, R] round trips. */
+int dfm_nmf_update_mm(int batch, long rows, int R, const float* a, const float* num, const float* M, float eps,
+                      float* den, float* out, void* out16, int copy_dtype, dfm_stream_t stream);
+int dfm_nmf_update_bwd_mm(int batch, long rows, int R, const float* g, const float* A2, const float* S,
+                          const float* a, const float* num, const float* den, const float* out, float eps,
+                          const float* Mg, float* ga, int accumulate_ga, float* gnum, float* gden, void* gnum16,
+                          int copy_dtype, dfm_stream_t stream);
 /* row softmax over R (NMF coef init, ham_head.py:48-49) and its backward */
 int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream);
 int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int accumulate,

@@ -799,3 +799,33 @@ def test_group_scale(dt):
     exp = (v.float().view(B, rows, C) * sc[:, None, :]).view(B * rows, C)
     Kk.group_scale(v, sc, rows, out=v)
     assert rel(v.float(), exp) <= TOL[dt] / 4
+
+
+@pytest.mark.parametrize("rows", [4800, 77, 512])
+def test_nmf_update_mm_fused(rows):
+    """dfm_nmf_update_mm / _bwd_mm (rank 64, the den products fused) vs torch fp32 compositions of
+    the same update (ham_head.py:120-141) and of its backward with the folded Gram gradient terms."""
+    Kk = K()
+    Bb, R, eps = 3, 64, 1e-6
+    g0 = torch.Generator(device=DEV).manual_seed(9)
+    a = torch.rand(Bb, rows, R, device=DEV, generator=g0) + 0.1
+    num = torch.rand(Bb, rows, R, device=DEV, generator=g0)
+    Bm = torch.rand(Bb, 96, R, device=DEV, generator=g0)
+    M = Bm.transpose(1, 2) @ Bm
+    out, den, o16 = Kk.nmf_update_mm(a, num, M, eps, bf16_copy=True)
+    den_ref = a @ M
+    out_ref = a * num / (den_ref + eps)
+    assert rel(den, den_ref) < 1e-5 and rel(out, out_ref) < 1e-5
+    assert torch.equal(o16, out.to(torch.bfloat16))
+    g = torch.randn(Bb, rows, R, device=DEV, generator=g0)
+    A2 = torch.rand(Bb, rows, R, device=DEV, generator=g0)
+    S = torch.randn(Bb, R, R, device=DEV, generator=g0)
+    ga, gnum, gden, g16 = Kk.nmf_update_bwd_mm(g, a, num, den, out, A2=A2, S=S, Mg=M, eps=eps, bf16_copy=True)
+    ge = g + A2 @ (S + S.transpose(1, 2))
+    r = 1.0 / (den + eps)
+    gden_ref = -ge * out * r
+    assert rel(gnum, ge * a * r) < 1e-5 and rel(gden, gden_ref) < 1e-5
+    assert rel(ga, ge * num * r + gden_ref @ M) < 1e-5
+    assert torch.equal(g16, gnum.to(torch.bfloat16))
+    ga2, gnum2, gden2 = Kk.nmf_update_bwd_mm(g, a, num, den, out, eps=eps)  # no folded terms
+    assert rel(ga2, g * num * r) < 1e-5 and rel(gden2, -g * out * r) < 1e-5
