@@ -115,6 +115,9 @@ _SIGS = {
     "dfm_seg_loss_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P]),
     "dfm_seg_loss_bwd_workspace": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "dfm_seg_loss_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P, P, P, P]),
+    "dfm_seg_loss_grad_partials_size": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "dfm_seg_loss_fwd_grad": (c_int, [c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P, c_int, P, P, P]),
+    "dfm_seg_loss_bwd_gather": (c_int, [c_int, c_int, c_int, c_int, c_int, P, P, P, P, P]),
     "dfm_adamw": (c_int, [c_long, P, P, P, P, c_float, c_float, c_float, c_float, c_float, c_int, c_float, P, c_int,
                           P]),
     "dfm_adamw_dev": (c_int, [c_long, P, P, P, P, P, c_float, c_float, c_float, c_float, c_float, P, c_int, P]),

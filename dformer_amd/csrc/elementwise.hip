@@ -624,6 +624,32 @@ __global__ __launch_bounds__(256) void pack_slices_kernel(PackSrc src, int n, lo
   }
 }
 
+// 8 consecutive elements of one source slice per thread (cols % 8 == 0, 16-byte aligned sources):
+// one or two 16-byte loads, one 16-byte store (the scalar kernel above ran at ~0.3 of HBM on the
+// NMF backward's 157 MB factor pack)
+template <typename TO>
+__global__ __launch_bounds__(256) void pack_slices_vec_kernel(PackSrc src, int n, long rows, int cols,
+                                                              TO* __restrict__ dst) {
+  const int cv = cols / 8;
+  const long total = rows * (long)n * cv;
+  for (long v = (long)blockIdx.x * 256 + threadIdx.x; v < total; v += (long)gridDim.x * 256) {
+    const long r = v / ((long)n * cv);
+    const int q = (int)(v - r * n * cv), i = q / cv, c = (q - i * cv) * 8;
+    const long si = r * cols + c;
+    float f[8];
+    if (src.dt[i] == DFM_F32) {
+      const float4 a = *reinterpret_cast<const float4*>((const float*)src.p[i] + si);
+      const float4 b = *reinterpret_cast<const float4*>((const float*)src.p[i] + si + 4);
+      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    } else if (src.dt[i] == DFM_BF16) {
+      ld8<bf16_t>((const bf16_t*)src.p[i] + si, f);
+    } else {
+      ld8<f16_t>((const f16_t*)src.p[i] + si, f);
+    }
+    st8<TO>(dst + v * 8, f);
+  }
+}
+
 extern "C" int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, const int* src_dtypes, long rows,
                                int cols, void* dst, dfm_stream_t stream) {
   DFM_CHECK_ARG(n >= 1 && n <= PACK_MAX && srcs && src_dtypes && dst && rows >= 0 && cols > 0,
@@ -638,6 +664,17 @@ extern "C" int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, co
   }
   if (rows == 0) return DFM_OK;
   hipStream_t s = (hipStream_t)stream;
+  bool vec = cols % 8 == 0 && (dtype_out == DFM_BF16 || dtype_out == DFM_F16) && (uintptr_t)dst % 16 == 0;
+  for (int i = 0; i < n; ++i) vec = vec && (uintptr_t)srcs[i] % 16 == 0;
+  if (vec) {
+    const unsigned gv = ew_grid(rows * (long)n * cols / 8);
+    if (dtype_out == DFM_BF16)
+      DFM_LAUNCH(pack_slices_vec_kernel<bf16_t>, dim3(gv), dim3(256), 0, s, ps, n, rows, cols, (bf16_t*)dst);
+    else
+      DFM_LAUNCH(pack_slices_vec_kernel<f16_t>, dim3(gv), dim3(256), 0, s, ps, n, rows, cols, (f16_t*)dst);
+    DFM_LAUNCH_CHECK();
+    return DFM_OK;
+  }
   const unsigned g = ew_grid(rows * (long)n * cols);
   if (dtype_out == DFM_BF16) DFM_LAUNCH(pack_slices_kernel<bf16_t>, dim3(g), dim3(256), 0, s, ps, n, rows, cols, (bf16_t*)dst);
   else if (dtype_out == DFM_F16) DFM_LAUNCH(pack_slices_kernel<f16_t>, dim3(g), dim3(256), 0, s, ps, n, rows, cols, (f16_t*)dst);

@@ -364,6 +364,191 @@ __global__ void seg_loss_gather_kernel(int B, int h, int w, int ncls, const floa
   }
 }
 
+// ---- forward + gradient in one pass (training, integer factor S in {4, 8}): the corner-tile
+// geometry of seg_loss_bwd_tile_kernel, with each tile's 2 x 2 low-res logit rows staged in LDS once
+// (every pixel of the tile interpolates from them: the forward kernel above re-read its 4 taps from
+// L2 per pixel) and the loss terms reduced per block. The residual (softmax - onehot) and the corner
+// partials are left unscaled; seg_loss_gather_scaled_kernel applies gscale / count once the count is
+// known (the backward then costs one gather).
+template <typename T, int S>
+__global__ __launch_bounds__(TILE_NT) void seg_loss_fused_tile_kernel(int B, int h, int w, int ncls,
+                                                                      const T* __restrict__ lg, int H, int W,
+                                                                      const long* __restrict__ label, int ignore,
+                                                                      float* __restrict__ part,
+                                                                      float* __restrict__ lpart, long ntiles) {
+  constexpr int TP = S * S, TPW = 64 / TP;
+  constexpr int RP = MAXC + 1;
+  __shared__ float res[TILE_NT][RP];
+  __shared__ float wts[TILE_NT][4];
+  __shared__ float corner[TILE_NT / 64][TPW][4][MAXC];
+  __shared__ float lred[2][TILE_NT / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long tile0 = ((long)blockIdx.x * (TILE_NT / 64) + wid) * TPW;
+  const int tw = w + 1, th = h + 1;
+  // this wave's tiles' 4 corner cells (clamped; a clamped slot always carries weight 0)
+  for (int e = lane; e < TPW * 4 * ncls; e += 64) {
+    const int tt = e / (4 * ncls), k = (e / ncls) % 4, c = e % ncls;
+    const long t = tile0 + tt;
+    float v = 0.f;
+    if (t < ntiles) {
+      const int tx = t % tw, ty = (t / tw) % th, b = t / ((long)tw * th);
+      const int cy = min(max(ty - 1 + (k >> 1), 0), h - 1), cx = min(max(tx - 1 + (k & 1), 0), w - 1);
+      v = ldf(lg + (((long)b * h + cy) * w + cx) * ncls + c);
+    }
+    corner[wid][tt][k][c] = v;
+  }
+  __syncthreads();
+  const long tile = tile0 + lane / TP;
+  const int tt = lane / TP, d = lane % TP, dy = d / S, dx = d % S;
+  float* row = res[threadIdx.x];
+  float wv[4] = {0.f, 0.f, 0.f, 0.f};
+  float ls = 0.f, lc = 0.f;
+  if (tile < ntiles) {
+    const int tx = tile % tw, ty = (tile / tw) % th, b = tile / ((long)tw * th);
+    const int y = S * ty - S / 2 + dy, x = S * tx - S / 2 + dx;
+    long lab = -1;
+    if (y >= 0 && y < H && x >= 0 && x < W) lab = label[((long)b * H + y) * W + x];
+    if (lab != ignore && lab >= 0 && lab < ncls) {
+      int a0, a1, b0, b1;
+      float ly, lx;
+      src_idx(y, h, H, a0, a1, ly);
+      src_idx(x, w, W, b0, b1, lx);
+      const float wy[2] = {(a0 == ty - 1 ? 1.f - ly : 0.f) + (a1 == ty - 1 ? ly : 0.f),
+                           (a0 == ty ? 1.f - ly : 0.f) + (a1 == ty ? ly : 0.f)};
+      const float wx[2] = {(b0 == tx - 1 ? 1.f - lx : 0.f) + (b1 == tx - 1 ? lx : 0.f),
+                           (b0 == tx ? 1.f - lx : 0.f) + (b1 == tx ? lx : 0.f)};
+      wv[0] = wy[0] * wx[0]; wv[1] = wy[0] * wx[1]; wv[2] = wy[1] * wx[0]; wv[3] = wy[1] * wx[1];
+      float z[MAXC];
+      float m = -INFINITY, zl = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < ncls) {
+          z[c] = wv[0] * corner[wid][tt][0][c] + wv[1] * corner[wid][tt][1][c] + wv[2] * corner[wid][tt][2][c] +
+                 wv[3] * corner[wid][tt][3][c];
+          m = fmaxf(m, z[c]);
+          zl = c == lab ? z[c] : zl;
+        }
+      }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncls) {
+          z[c] = __expf(z[c] - m);
+          se += z[c];
+        }
+      ls = m + __logf(se) - zl;
+      lc = 1.f;
+      const float rs = 1.f / se;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncls) row[c] = z[c] * rs - (c == lab ? 1.f : 0.f);
+    } else {
+      for (int c = 0; c < ncls; ++c) row[c] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wts[threadIdx.x][k] = wv[k];
+  ls = wave_sum(ls);
+  lc = wave_sum(lc);
+  if (lane == 0) {
+    lred[0][wid] = ls;
+    lred[1][wid] = lc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int q = 0; q < TILE_NT / 64; ++q) {
+      a += lred[0][q];
+      c += lred[1][q];
+    }
+    lpart[blockIdx.x * 2] = a;
+    lpart[blockIdx.x * 2 + 1] = c;
+  }
+  for (int pr = lane; pr < TPW * ncls; pr += 64) {
+    const int t2 = pr / ncls, c = pr % ncls;
+    const long t = tile0 + t2;
+    if (t >= ntiles) continue;
+    const int base = wid * 64 + t2 * TP;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < TP; ++q) {
+      const float r = res[base + q][c];
+      s0 = fmaf(wts[base + q][0], r, s0);
+      s1 = fmaf(wts[base + q][1], r, s1);
+      s2 = fmaf(wts[base + q][2], r, s2);
+      s3 = fmaf(wts[base + q][3], r, s3);
+    }
+    float* o = part + t * 4 * ncls + c;
+    o[0] = s0;
+    o[ncls] = s1;
+    o[2 * ncls] = s2;
+    o[3 * ncls] = s3;
+  }
+}
+
+// (loss sum, valid count) of nblk block partials: 1024 lanes, fixed order
+__global__ __launch_bounds__(1024) void seg_loss_sum_wide_kernel(int nblk, const float* __restrict__ part,
+                                                                  float* __restrict__ out) {
+  float s0 = 0.f, s1 = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 1024) {
+    s0 += part[b * 2];
+    s1 += part[b * 2 + 1];
+  }
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  __shared__ float red[2][16];
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = s0;
+    red[1][threadIdx.x >> 6] = s1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f, c = 0.f;
+    for (int q = 0; q < 16; ++q) {
+      a += red[0][q];
+      c += red[1][q];
+    }
+    out[0] = a;
+    out[1] = c;
+  }
+}
+
+// dlogits = gscale / count * (the 4 corner partials around each cell, fixed order), in TO
+template <typename TO>
+__global__ void seg_loss_gather_scaled_kernel(int B, int h, int w, int ncls, const float* __restrict__ part,
+                                              const float* __restrict__ loss_out, const float* __restrict__ gscale,
+                                              TO* __restrict__ dlg) {
+  const long n = (long)B * h * w * ncls;
+  const int tw = w + 1, th = h + 1;
+  const float inv = (gscale ? gscale[0] : 1.f) / fmaxf(loss_out[1], 1.f);
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = e % ncls;
+    const long cell = e / ncls;
+    const int j = cell % w, i = (cell / w) % h, b = cell / ((long)w * h);
+    auto P = [&](int ty, int tx, int slot) { return part[((((long)b * th + ty) * tw + tx) * 4 + slot) * ncls + c]; };
+    stf(dlg + e, inv * (P(i, j, 3) + P(i, j + 1, 2) + P(i + 1, j, 1) + P(i + 1, j + 1, 0)));
+  }
+}
+
+template <typename T>
+int launch_fused_tiles(int S, int B, int h, int w, int ncls, const void* lg, int H, int W, const long* label,
+                       int ignore, float* loss_out, float* part, float* lpart, hipStream_t s) {
+  const long ntiles = (long)B * (h + 1) * (w + 1);
+  const long tiles_per_block = (TILE_NT / 64) * (64 / (S * S));
+  const unsigned nb = cdiv(ntiles, tiles_per_block);
+  if (S == 8)
+    DFM_LAUNCH((seg_loss_fused_tile_kernel<T, 8>), dim3(nb), dim3(TILE_NT), 0, s, B, h, w, ncls, (const T*)lg, H, W,
+               label, ignore, part, lpart, ntiles);
+  else
+    DFM_LAUNCH((seg_loss_fused_tile_kernel<T, 4>), dim3(nb), dim3(TILE_NT), 0, s, B, h, w, ncls, (const T*)lg, H, W,
+               label, ignore, part, lpart, ntiles);
+  DFM_LAUNCH_CHECK();
+  DFM_LAUNCH(seg_loss_sum_wide_kernel, dim3(1), dim3(1024), 0, s, (int)nb, (const float*)lpart, loss_out);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
 template <typename T>
 int launch_bwd_tiles(int S, int B, int h, int w, int ncls, const void* lg, int H, int W, const long* label,
                      int ignore, const float* loss_out, const float* gscale, float* part, float* dlg,
@@ -427,6 +612,62 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
                label, ignore, lse, (float*)workspace);
   DFM_LAUNCH_CHECK();
   DFM_LAUNCH(seg_loss_sum_kernel, dim3(1), dim3(64), 0, s, nblk, (const float*)workspace, loss_out);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+static int fused_scale(int h, int w, int H, int W) {
+  const int S = tile_scale(h, w, H, W);
+  return S == 8 || S == 4 ? S : 0;
+}
+
+extern "C" size_t dfm_seg_loss_grad_partials_size(int B, int h, int w, int ncls, int H, int W) {
+  if (!fused_scale(h, w, H, W)) return 0;
+  const long ntiles = (long)B * (h + 1) * (w + 1);
+  const long nb = (ntiles + 1) / 2;  // upper bound of the blocks (>= 2 tiles per block)
+  return (size_t)(ntiles * 4 * ncls + nb * 2) * sizeof(float);
+}
+
+extern "C" int dfm_seg_loss_fwd_grad(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
+                                     const long* label, int ignore, float* loss_out, float* grad_partials,
+                                     dfm_stream_t stream) {
+  const int S = fused_scale(h, w, H, W);
+  DFM_CHECK_ARG(logits && label && loss_out && grad_partials && ncls <= MAXC && S,
+                "dfm_seg_loss_fwd_grad: bad argument (needs ncls <= 64 and H = S h, W = S w, S in {4, 8})");
+  hipStream_t s = (hipStream_t)stream;
+  float* part = grad_partials;
+  float* lpart = part + (long)B * (h + 1) * (w + 1) * 4 * ncls;
+  if (dtype == DFM_BF16)
+    return launch_fused_tiles<bf16_t>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, part, lpart, s);
+  if (dtype == DFM_F16)
+    return launch_fused_tiles<f16_t>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, part, lpart, s);
+  if (dtype == DFM_F32)
+    return launch_fused_tiles<float>(S, B, h, w, ncls, logits, H, W, label, ignore, loss_out, part, lpart, s);
+  dfm_set_error("dfm_seg_loss_fwd_grad: bad dtype %d", dtype);
+  return DFM_ERR_DTYPE;
+}
+
+extern "C" int dfm_seg_loss_bwd_gather(int dtype_out, int B, int h, int w, int ncls, const float* grad_partials,
+                                       const float* loss_out, const float* gscale, void* dlogits,
+                                       dfm_stream_t stream) {
+  DFM_CHECK_ARG(grad_partials && loss_out && dlogits && ncls > 0 && B > 0 && h > 0 && w > 0,
+                "dfm_seg_loss_bwd_gather: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  const long n = (long)B * h * w * ncls;
+  const dim3 g((unsigned)std::min(8192L, (n + 255) / 256));
+  if (dtype_out == DFM_BF16)
+    DFM_LAUNCH(seg_loss_gather_scaled_kernel<bf16_t>, g, dim3(256), 0, s, B, h, w, ncls, grad_partials, loss_out,
+               gscale, (bf16_t*)dlogits);
+  else if (dtype_out == DFM_F16)
+    DFM_LAUNCH(seg_loss_gather_scaled_kernel<f16_t>, g, dim3(256), 0, s, B, h, w, ncls, grad_partials, loss_out,
+               gscale, (f16_t*)dlogits);
+  else if (dtype_out == DFM_F32)
+    DFM_LAUNCH(seg_loss_gather_scaled_kernel<float>, g, dim3(256), 0, s, B, h, w, ncls, grad_partials, loss_out,
+               gscale, (float*)dlogits);
+  else {
+    dfm_set_error("dfm_seg_loss_bwd_gather: bad dtype %d", dtype_out);
+    return DFM_ERR_DTYPE;
+  }
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }

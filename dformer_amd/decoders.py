@@ -667,17 +667,28 @@ class SegLossFn(torch.autograd.Function):
     def forward(ctx, logits_rows, B, h, w, label, ignore):
         ncls = logits_rows.shape[1]
         label = label.contiguous()
-        out = K.seg_loss_fwd(logits_rows, B, h, w, ncls, label, ignore)
-        ctx.save_for_backward(logits_rows, label, out)
+        H, W = label.shape[-2:]
         ctx.meta = (B, h, w, ncls, ignore)
+        if ctx.needs_input_grad[0] and K.seg_loss_grad_partials_size(B, h, w, ncls, H, W):
+            # training at an integer factor (4, 8): the gradient's partials come out of the same pass
+            out, part = K.seg_loss_fwd_grad(logits_rows, B, h, w, ncls, label, ignore)
+            ctx.save_for_backward(part, out)
+            ctx.fused, ctx.dtype = True, logits_rows.dtype
+        else:
+            out = K.seg_loss_fwd(logits_rows, B, h, w, ncls, label, ignore)
+            ctx.save_for_backward(logits_rows, label, out)
+            ctx.fused = False
         return out[0] / out[1].clamp_min(1.0)
 
     @staticmethod
     def backward(ctx, g):
         K.TAG = "loss.bwd"
-        logits_rows, label, out = ctx.saved_tensors
         B, h, w, ncls, ignore = ctx.meta
         gs = g.reshape(1).float().contiguous()
+        if ctx.fused:
+            part, out = ctx.saved_tensors
+            return K.seg_loss_bwd_gather(part, B, h, w, ncls, out, gs, ctx.dtype), None, None, None, None, None
+        logits_rows, label, out = ctx.saved_tensors
         dl = K.seg_loss_bwd(logits_rows, B, h, w, ncls, label, out, gscale=gs, ignore=ignore)
         if logits_rows.dtype != torch.float32:
             dl = K.cast(dl, logits_rows.dtype)

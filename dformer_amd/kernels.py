@@ -850,6 +850,32 @@ def seg_loss_bwd(logits, B, h, w, ncls, label, loss_out, gscale=None, ignore=255
     return dl
 
 
+def seg_loss_grad_partials_size(B, h, w, ncls, H, W):
+    return lib.dfm_seg_loss_grad_partials_size(B, h, w, ncls, H, W)
+
+
+def seg_loss_fwd_grad(logits, B, h, w, ncls, label, ignore=255):
+    """Training loss + its gradient's unscaled per-tile partials in one pass -> (loss_out, partials)."""
+    H, W = label.shape[-2:]
+    out = torch.empty(2, device=logits.device, dtype=torch.float32)
+    nb = seg_loss_grad_partials_size(B, h, w, ncls, H, W)
+    part = torch.empty(nb // 4, device=logits.device, dtype=torch.float32)
+    check(lib.dfm_seg_loss_fwd_grad(dtype_code(logits), B, h, w, ncls, ptr(logits), H, W, ptr(label), ignore,
+                                    ptr(out), ptr(part), stream()), "dfm_seg_loss_fwd_grad")
+    if ACCOUNT is not None:
+        _acct(0, logits.numel() * _es(logits) + label.numel() * 8)
+    return out, part
+
+
+def seg_loss_bwd_gather(part, B, h, w, ncls, loss_out, gscale, dtype):
+    dl = torch.empty(B * h * w, ncls, device=part.device, dtype=dtype)
+    check(lib.dfm_seg_loss_bwd_gather(dtype_code(dl), B, h, w, ncls, ptr(part), ptr(loss_out), ptr(gscale), ptr(dl),
+                                      stream()), "dfm_seg_loss_bwd_gather")
+    if ACCOUNT is not None:
+        _acct(0, dl.numel() * _es(dl))
+    return dl
+
+
 # -------------------------------------------------------------------------------------- AdamW
 def loss_scale_update(amp, flag, growth, backoff, interval):
     check(lib.dfm_loss_scale_update(ptr(amp), ptr(flag), growth, backoff, interval, stream()),

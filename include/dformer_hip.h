@@ -366,6 +366,17 @@ int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const void* logit
                      const long* label, int ignore, const float* lse, const float* loss_out,
                      const float* gscale, float* dlogits, void* workspace, dfm_stream_t stream);
 
+/* Training: the loss AND its gradient's per-tile partials in one pass (integer factor S in {4, 8}: the
+ * ham head's x8, the MLP decoder's x4 at 480x640): each S x S pixel tile's 2 x 2 low-res logit rows
+ * are read once, loss_out = (sum, count) as dfm_seg_loss_fwd; grad_partials (dfm_seg_loss_grad_partials_size
+ * bytes, 0 = factor unsupported) must survive until dfm_seg_loss_bwd_gather, which writes dlogits
+ * (dtype_out) = gscale / max(count, 1) * the fixed-order sum of the corner partials of each cell. */
+size_t dfm_seg_loss_grad_partials_size(int B, int h, int w, int ncls, int H, int W);
+int dfm_seg_loss_fwd_grad(int dtype, int B, int h, int w, int ncls, const void* logits, int H, int W,
+                          const long* label, int ignore, float* loss_out, float* grad_partials, dfm_stream_t stream);
+int dfm_seg_loss_bwd_gather(int dtype_out, int B, int h, int w, int ncls, const float* grad_partials,
+                            const float* loss_out, const float* gscale, void* dlogits, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- optimizer
  * torch.optim.AdamW step (train.py:210-216) over a flat float32 parameter buffer; optional
  * 16-bit shadow copy (copy_dtype DFM_BF16 / DFM_F16) for the next step's GEMM operands.

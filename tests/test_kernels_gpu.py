@@ -741,6 +741,11 @@ def test_pack_slices():
         out = torch.empty(3, 50, 5 * 64, device=DEV, dtype=odt)
         k.pack_slices(srcs, out)
         assert torch.equal(out, torch.cat([s.to(odt) for s in srcs], -1))
+    # the element-wise path: 12-column slices (not a multiple of 8)
+    odd = [torch.randn(40, 12, device=DEV).to(dt) for dt in (torch.float32, torch.bfloat16, torch.float16)]
+    out = torch.empty(40, 36, device=DEV, dtype=torch.bfloat16)
+    k.pack_slices(odd, out)
+    assert torch.equal(out, torch.cat([s.to(torch.bfloat16) for s in odd], -1))
 
 
 @pytest.mark.parametrize("dt", DTYPES)
@@ -829,3 +834,31 @@ def test_nmf_update_mm_fused(rows):
     assert torch.equal(g16, gnum.to(torch.bfloat16))
     ga2, gnum2, gden2 = Kk.nmf_update_bwd_mm(g, a, num, den, out, eps=eps)  # no folded terms
     assert rel(ga2, g * num * r) < 1e-5 and rel(gden2, -g * out * r) < 1e-5
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (2, 8, 12, 64, 96, 40), (1, 30, 40, 120, 160, 37),
+                                            (2, 7, 9, 28, 36, 64)])
+def test_seg_loss_fwd_grad_fused(dt, B, h, w, H, W, ncls):
+    """dfm_seg_loss_fwd_grad + dfm_seg_loss_bwd_gather (the training loss with its gradient partials
+    from the same pass, factors 8 / 4) vs torch fp32 F.interpolate + cross_entropy(ignore 255) and
+    its autograd gradient, with a loss scale; bitwise reproducible."""
+    k = K()
+    lg = torch.randn(B, h, w, ncls, device=DEV).to(dt)
+    lab = torch.randint(0, ncls, (B, H, W), device=DEV)
+    lab[torch.rand(B, H, W, device=DEV) < 0.1] = 255
+    out, part = k.seg_loss_fwd_grad(lg.view(-1, ncls), B, h, w, ncls, lab)
+    lr = lg.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
+    up = F.interpolate(lr, (H, W), mode="bilinear", align_corners=False)
+    ce = F.cross_entropy(up, lab, reduction="none", ignore_index=255)
+    loss = ce[lab != 255].mean()
+    assert abs((out[0] / out[1]).item() - loss.item()) < 1e-4 * abs(loss.item())
+    (loss * 3.0).backward()
+    gs = torch.full((1,), 3.0, device=DEV)
+    dl = k.seg_loss_bwd_gather(part, B, h, w, ncls, out, gs, torch.float32)
+    assert rel(dl.view(B, h, w, ncls).permute(0, 3, 1, 2), lr.grad) < 1e-3
+    out2, part2 = k.seg_loss_fwd_grad(lg.view(-1, ncls), B, h, w, ncls, lab)
+    dl2 = k.seg_loss_bwd_gather(part2, B, h, w, ncls, out2, gs, torch.float32)
+    assert torch.equal(out, out2) and torch.equal(dl, dl2)
+    dl16 = k.seg_loss_bwd_gather(part, B, h, w, ncls, out, gs, dt)  # written in the logits dtype directly
+    assert rel(dl16.float(), dl) < (1e-6 if dt == torch.float32 else 4e-3)
