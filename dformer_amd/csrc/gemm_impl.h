@@ -48,7 +48,6 @@ struct GemmArgs {
   int ala, alb;    // operand rows 16-byte aligned (vector loads)
   int vec_ok;      // output-side rows 16-byte aligned (vector epilogue)
   int mul_gelu_grad;
-  int stream;      // host: take the M-streaming persistent kernel
   int tiles_n;     // output column tiles (grid.x enumerates tiles_m * tiles_n)
   int tiles_m;     // output row tiles (glds kernel)
   int n_fast;      // glds kernel: consecutive (XCD-local) blocks walk column tiles of one row tile
@@ -677,115 +676,6 @@ __global__ __launch_bounds__(64 * NW, 4) void gemm_group_kernel(GemmGroup g) {
   gemm_tile<T, BM, BN, NW, WAVES_M, BK, AK, BKC, DEPTH>(a, lid % ntile, lid / ntile, smem);
 }
 
-// M-streaming GEMM for large M x short K (K a multiple of BK, 16-byte aligned operands, no
-// split-K, batch 1, no bias-gradient column): a persistent grid walks the tiles (M fastest, so
-// consecutive blocks share the B tile through L2) and requests the next tile's first k-slice
-// before the current tile's epilogue, so operand loads stream underneath the output writes.
-template <typename T, int BM, int BN, int NW, int WAVES_M, int BK, bool AK, bool BKC>
-__global__ __launch_bounds__(64 * NW) void gemm_stream_kernel(GemmArgs a, int tiles_m, long ntiles) {
-  constexpr int NT = 64 * NW;
-  constexpr int WAVES_N = NW / WAVES_M;
-  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int KSTEP = Mf<T>::KSTEP;
-  using GA = TileGeom<T, BM, BK, AK, NT>;
-  using GB = TileGeom<T, BN, BK, BKC, NT>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* const lds_base = reinterpret_cast<T*>(smem);
-#define LDS_A(i) (lds_base + (i) * GA::ELEMS)
-#define LDS_B(i) (lds_base + 2 * GA::ELEMS + (i) * GB::ELEMS)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-  const int nk = a.K / BK;
-  const T* A = (const T*)a.A;
-  const T* Bp = (const T*)a.B;
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0xffffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)Bp, 0, 0xffffffff, 0x00020000);
-
-  long t = blockIdx.x;
-  if (t >= ntiles) return;
-  int bm = (int)(t % tiles_m) * BM, bn = (int)(t / tiles_m) * BN;
-  unsigned offa[GA::NVEC], offb[GB::NVEC];
-  fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
-  fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
-  uint4 ra[GA::NVEC], rb[GB::NVEC];
-  auto load = [&](int kt) {
-    const int k0 = kt * BK;
-    stage_load_fast<T, BM, BK, AK, NT>(ra, rsa, (int)((AK ? k0 : (long)k0 * a.lda) * sizeof(T)), offa);
-    stage_load_fast<T, BN, BK, BKC, NT>(rb, rsb, (int)((BKC ? k0 : (long)k0 * a.ldb) * sizeof(T)), offb);
-  };
-  auto store = [&](int buf) {
-    stage_store<T, BM, BK, AK, NT>(ra, LDS_A(buf));
-    stage_store<T, BN, BK, BKC, NT>(rb, LDS_B(buf));
-  };
-  float4_t acc[TM][TN];
-  auto compute = [&](const T* la, const T* lb) {
-#pragma unroll
-    for (int ks = 0; ks < BK; ks += KSTEP) {
-      if constexpr (sizeof(T) == 2) {
-        bf16x8_t fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = frag_bf16<AK, GA::LD>((const bf16_t*)la, wm * WM + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = frag_bf16<BKC, GB::LD>((const bf16_t*)lb, wn * WN + j * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = mma16<T>(fa[i], fb[j], acc[i][j]);
-      } else {
-        float fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = frag_f32<AK, GA::LD>((const float*)la, wm * WM + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = frag_f32<BKC, GB::LD>((const float*)lb, wn * WN + j * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  };
-
-  load(0);
-  for (;;) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
-    store(0);
-    lds_barrier();
-    int cur = 0;
-    for (int kt = 0; kt + 1 < nk; ++kt) {
-      load(kt + 1);
-      compute(LDS_A(cur), LDS_B(cur));
-      store(cur ^ 1);
-      lds_barrier();
-      cur ^= 1;
-    }
-    compute(LDS_A(cur), LDS_B(cur));
-    // next tile's first slice in flight during this tile's epilogue (a re-read of this tile's
-    // slice, L2-hot, when there is none: every load stays unconditional)
-    const long tn = t + gridDim.x;
-    const bool more = tn < ntiles;
-    const int bm_c = bm, bn_c = bn;
-    if (more) {
-      bm = (int)(tn % tiles_m) * BM;
-      bn = (int)(tn / tiles_m) * BN;
-    }
-    fast_offsets<T, BM, BK, AK, NT>(offa, a.lda, bm, a.M);
-    fast_offsets<T, BN, BK, BKC, NT>(offb, a.ldb, bn, a.N);
-    load(0);
-    lds_barrier();  // operand LDS reads done: the epilogue reuses it
-    gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm_c, bn_c, 0, 0);
-    if (!more) break;
-    t = tn;
-  }
-#undef LDS_A
-#undef LDS_B
-}
-
 // Deterministic split-K combine: each block owns 256/G consecutive outputs and G lanes per output
 // walk the splits in a fixed order (G = 4 when there are many splits, so short outputs x long
 // split counts still fill the chip), then the G partial sums meet in LDS.
@@ -1120,36 +1010,8 @@ int launch_cfg(GemmArgs& a, hipStream_t s) {
   return DFM_OK;
 }
 
-template <typename T, int BM, int BN, int NW, int WM_, int BK, bool AK, bool BKC>
-int launch_stream(GemmArgs& a, hipStream_t s) {
-  using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
-  using GB = TileGeom<T, BN, BK, BKC, 64 * NW>;
-  const size_t lds_op = (size_t)2 * (GA::ELEMS + GB::ELEMS) * sizeof(T);
-  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
-  const size_t lds_c = (size_t)RP * (BN + 4) * sizeof(float);
-  const size_t lds = lds_op > lds_c ? lds_op : lds_c;
-  auto kern = gemm_stream_kernel<T, BM, BN, NW, WM_, BK, AK, BKC>;
-  static int per_cu = -1;
-  if (per_cu < 0) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 64 * NW, lds) != hipSuccess || n < 1) n = 1;
-    per_cu = n;
-  }
-  const int tiles_m = cdiv(a.M, BM);
-  const long ntiles = (long)tiles_m * cdiv(a.Nw, BN);
-  const long grid = std::min(ntiles, (long)256 * per_cu);
-  DFM_LAUNCH(kern, dim3((unsigned)grid), dim3(64 * NW), lds, s, a, tiles_m, ntiles);
-  DFM_LAUNCH_CHECK();
-  return DFM_OK;
-}
-
 template <typename T, int BM, int BN, int NW, int WM_, int BK, int DEPTH>
 int launch_layout(GemmArgs& a, bool ak, bool bk, hipStream_t s) {
-  if constexpr (DEPTH == 1 && BN <= 128 && sizeof(T) == 2) {
-    if (a.stream && ak && bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, true>(a, s);
-    if (a.stream && ak && !bk) return launch_stream<T, BM, BN, NW, WM_, BK, true, false>(a, s);
-  }
   if (ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, true, DEPTH>(a, s);
   if (ak && !bk) return launch_cfg<T, BM, BN, NW, WM_, BK, true, false, DEPTH>(a, s);
   if (!ak && bk) return launch_cfg<T, BM, BN, NW, WM_, BK, false, true, DEPTH>(a, s);
@@ -1209,7 +1071,6 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   constexpr int VEC = Mf<T>::VEC;
   GemmArgs a;
   a.A = A; a.B = B; a.C = C; a.ws = (float*)ws;
-  a.stream = 0;
   a.M = d->M; a.N = d->N; a.K = d->K; a.batch = d->batch > 0 ? d->batch : 1;
   a.Nw = d->N + (d->colsum ? 1 : 0);
   a.ldw = (a.Nw + 7) & ~7;
@@ -1237,13 +1098,9 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
              al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
   const bool ak = d->a_kcontig, bk = d->b_kcontig;
   const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
-  {  // large M x short K, column tiles <= 64: persistent M-streaming kernel (128-wide column tiles
-     // measured slower streamed: 378-380 vs 383 images/s on the DFormer-B step)
-    const int BKsel = small_k ? (sizeof(T) == 2 ? 32 : 16) : (sizeof(T) == 2 ? 64 : 32);
-    const long tiles = (long)cdiv(d->M, BM) * cdiv(a.Nw, BN);
-    a.stream = sizeof(T) == 2 && BN <= 64 && ak && a.splits == 1 && a.batch == 1 && !d->colsum && a.ala && a.alb &&
-               d->K % BKsel == 0 && d->K / BKsel <= 8 && tiles >= 1024;
-  }
+  // (a persistent M-streaming kernel for large M x short K, column tiles <= 64, was measured slower
+  // on the step than one tile per block: 452.7-454.0 vs 455.2 images/s — its static tile walk
+  // finishes late when the concurrent ConvFFN stream holds CUs)
   // bf16 k-contiguous A on the LDS-DMA ring: split-K off (one unsplit 64x64 ring block per tile beats
   // the split + reduction at 4,800 rows x K >= 1024: 16.8 vs 34.8 us, profiles/r04_glds_variants.txt)
   bool glds_ok = std::is_same<T, bf16_t>::value && ak && a.ala && a.alb;
@@ -1268,7 +1125,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // ms/step either way, profiles/r04_glds_variants.txt).
   if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 128);
-    if (glds_ok && route && !a.stream) {
+    if (glds_ok && route) {
       if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
       // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
       // (438.7-438.4 -> 439.0-440.3 images/s on one box; 65-93 vs 81-127 us per launch alone)
