@@ -268,7 +268,8 @@ def main():
         table = census(step)
         dom = max(table, key=lambda n: table[n]["measured_ms"])
     # HIP-graph mode (default at every world size, RCCL collectives included: tests/test_graph_gpu.py
-    # captures the SyncBN / bucket / loss collectives through a one-rank group; DFM_GRAPH=0 disables):
+    # captures the SyncBN / bucket / loss collectives through a one-rank group; DFM_GRAPH=0 disables;
+    # a multi-rank RCCL capture has not run on real N > 1 hardware yet — parity there is unverified):
     # the whole step is captured once and replayed, so ~2.3k kernel launches cost one graph launch
     use_graph = not args.eager and os.environ.get("DFM_GRAPH", "1") != "0"
     if use_graph:
