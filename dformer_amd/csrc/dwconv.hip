@@ -238,8 +238,15 @@ __host__ __device__ inline long w3_units(int B, int nstrips, int nchunks) { retu
 
 template <typename T> struct W3Cfg { static constexpr int EPL = 8 / sizeof(T); };
 
+// Row chunking of the streaming 3x3 kernels. A unit is one TW-column strip x RC rows of one image
+// for one wave's channel vectors; every wave takes one unit. The backward and forward kernels hold
+// 2 waves per SIMD (VGPR-bound), so a launch runs in rounds of 2048 waves on the 256 CUs: the chunk
+// count minimises rounds x (RC + 2 halo rows), chunks of at least 5 rows. Measured over the
+// DFormer-B ConvFFN shapes (tools/dw3_geom_sweep.py, profiles/r04_dw3_geom_sweep.txt): a wave count
+// just past a round boundary cost up to 40 % (30x40x1024 backward 58 vs 42 us at 3200 vs 1920
+// waves); a fixed 3072 / 8192-wave target sat past one on five of the eight shapes.
 template <typename T>
-W3Geom w3_geom(int B, int H, int W, int C) {
+W3Geom w3_geom(int B, int H, int W, int C, int waves_per_simd = 2) {
   constexpr int CPT = W3Cfg<T>::EPL;
   W3Geom g;
   const int G = C / CPT;
@@ -247,12 +254,19 @@ W3Geom w3_geom(int B, int H, int W, int C) {
   g.UPW = 64 / g.LPU;
   g.slices = (G + g.LPU - 1) / g.LPU;
   g.nstrips = (W + W3_TW - 1) / W3_TW;
-  // ~3072 waves in flight (12 per CU at this kernel's register budget): split the rows into chunks
-  // of at least 4 until the units fill them
-  const long target_waves = 3072;
-  long want = (target_waves * g.UPW + (long)B * g.nstrips * g.slices - 1) / ((long)B * g.nstrips * g.slices);
-  want = std::max(1L, std::min(want, (long)(H + 3) / 4));
-  g.RC = (int)((H + want - 1) / want);
+  const long slots = 256L * 4 * waves_per_simd;
+  const int max_chunks = std::max(1, H / 5);
+  long best = -1;
+  for (int n = 1; n <= max_chunks; ++n) {
+    const int rc = (H + n - 1) / n;
+    if (n > 1 && (H + rc - 1) / rc != n) continue;  // same row chunk as a smaller count
+    const long waves = (w3_units(B, g.nstrips, n) + g.UPW - 1) / g.UPW * g.slices;
+    const long cost = (waves + slots - 1) / slots * (rc + 2);
+    if (best < 0 || cost < best) {
+      best = cost;
+      g.RC = rc;
+    }
+  }
   g.nchunks = (H + g.RC - 1) / g.RC;
   g.units = w3_units(B, g.nstrips, g.nchunks);
   const long waves = (g.units + g.UPW - 1) / g.UPW;
@@ -403,7 +417,7 @@ __global__ __launch_bounds__(256) void dw3_stream_wgrad_kernel(int B, int H, int
 template <typename T>
 long w3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, float* part,
                hipStream_t s) {
-  const W3Geom g = w3_geom<T>(B, H, W, C);
+  const W3Geom g = w3_geom<T>(B, H, W, C, 3);
   DFM_LAUNCH(dw3_stream_wgrad_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H,
                      W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, part);
   return g.nsb;
@@ -598,22 +612,7 @@ long w7l_launch(int B, int H, int W, int C, const void* x, long ldx, const void*
 // (+ the fused identity, accumulate and GELU second output). No LDS, no block synchronisation.
 template <typename T>
 W3Geom f3_geom(int B, int H, int W, int C) {
-  constexpr int CPT = W3Cfg<T>::EPL;
-  W3Geom g;
-  const int G = C / CPT;
-  g.LPU = std::min(64, G);
-  g.UPW = 64 / g.LPU;
-  g.slices = (G + g.LPU - 1) / g.LPU;
-  g.nstrips = (W + W3_TW - 1) / W3_TW;
-  const long target_waves = 8192;
-  long want = (target_waves * g.UPW + (long)B * g.nstrips * g.slices - 1) / ((long)B * g.nstrips * g.slices);
-  want = std::max(1L, std::min(want, (long)(H + 7) / 8));
-  g.RC = (int)((H + want - 1) / want);
-  g.nchunks = (H + g.RC - 1) / g.RC;
-  g.units = w3_units(B, g.nstrips, g.nchunks);
-  const long waves = (g.units + g.UPW - 1) / g.UPW;
-  g.nsb = std::max(1L, (waves + 3) / 4);
-  return g;
+  return w3_geom<T>(B, H, W, C, 2);
 }
 
 template <typename T>
@@ -1009,7 +1008,8 @@ extern "C" int dfm_dwconv_bwd_data(int dtype, int B, int H, int W, int C, int k,
 extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k) {
   long nsb = 1;
   if (k == 3)
-    nsb = std::max(w3_geom<float>(B, H, W, C).nsb, w3_geom<bf16_t>(B, H, W, C).nsb);
+    for (int occ = 2; occ <= 3; ++occ)  // fused backward (2 waves / SIMD), weight gradient alone (3)
+      nsb = std::max({nsb, w3_geom<float>(B, H, W, C, occ).nsb, w3_geom<bf16_t>(B, H, W, C, occ).nsb});
   else if (k == 7)
     nsb = std::max(w7l_nsb<float>(B, H, W, C), w7l_nsb<bf16_t>(B, H, W, C));
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);

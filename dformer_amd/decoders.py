@@ -204,6 +204,75 @@ class ResizeCatFn(torch.autograd.Function):
         return (None, None, *grads)
 
 
+class SqueezeFoldFn(torch.autograd.Function):
+    """LightHamHead's resize + cat + squeeze ConvModule (1x1 conv, BN, ReLU; ham_head.py:226-234),
+    folded like MLPFoldFn: bilinear upsampling (align_corners=False) commutes with the 1x1 conv, so
+
+        W cat[c_0, up(c_1), up(c_2)] = W_0 c_0 + up(W_1 c_1) + up(W_2 c_2)
+
+    with W_i the column block of the squeeze weight that the cat order (in_index order, finest
+    first) gives level i. Each level's product runs at its own resolution with K = C_i instead of
+    one K = sum C_i GEMM over the concatenated map. Backward: G_i = up_i^T(dy0), dW_i = G_i^T c_i
+    (column block i of the weight gradient), dc_i = G_i W_i."""
+
+    @staticmethod
+    def forward(ctx, B, hw, bn, sync, w, gamma, beta, *rows):
+        dt = rows[0].dtype
+        H0, W0 = hw[0]
+        E = w.shape[0]
+        Wc = wcast(dt, w).view(E, -1)
+        offs = [0]
+        for r in rows:
+            offs.append(offs[-1] + r.shape[1])
+        assert offs[-1] == Wc.shape[1], "squeeze weight / concatenated channels mismatch"
+        y0 = None
+        for i, r in enumerate(rows):
+            Wi = Wc[:, offs[i]:offs[i + 1]]
+            h, wd = hw[i]
+            if (h, wd) == (H0, W0):
+                y0 = K.linear(r, Wi) if y0 is None else K.linear(r, Wi, out=y0, beta=1.0)
+            else:  # at the level's own resolution, then upsampled into the sum
+                t = K.linear(r, Wi)
+                if y0 is None:
+                    y0 = K.bilinear(t, (h, wd), (H0, W0), B)
+                else:
+                    K.bilinear(t, (h, wd), (H0, W0), B, out=y0, accumulate=True)
+        count = y0.shape[0]
+        if bn.training:
+            mean, rstd, count = bn_batch_stats(y0, bn, sync)
+        else:
+            mean, rstd = bn.running_mean, torch.rsqrt(bn.running_var + bn.eps)
+        y = K.bn_apply(y0, mean, rstd, gamma, beta, act=2)
+        ctx.save_for_backward(y0, y, mean, rstd, gamma, w, *rows)
+        ctx.meta = (B, hw, count, sync, bn, offs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        K.TAG = "decoder.bwd"
+        y0, y, mean, rstd, gamma, w = ctx.saved_tensors[:6]
+        rows = ctx.saved_tensors[6:]
+        B, hw, count, sync, bn, offs = ctx.meta
+        H0, W0 = hw[0]
+        E = w.shape[0]
+        dy = K.relu_bwd(dy.contiguous(), y)
+        st2, dgamma, dbeta = bn_grad_stats(y0, dy, mean, rstd, bn, sync)
+        dy0 = K.bn_bwd_apply(y0, dy, mean, rstd, gamma, st2, count)
+        dW = gslot2(w)
+        if dW is None:
+            dW = torch.empty(E, offs[-1], device=y0.device, dtype=torch.float32)
+        dW = dW.view(E, -1)
+        Wc = wcast(y0.dtype, w).view(E, -1)
+        drows = []
+        with K.wgrad_group():  # the per-level dW_i as one grouped launch
+            for i, r in enumerate(rows):
+                h, wd = hw[i]
+                G = dy0 if (h, wd) == (H0, W0) else K.bilinear_bwd(dy0, (h, wd), (H0, W0), B)
+                K.linear_wgrad(G, r, out=dW[:, offs[i]:offs[i + 1]])
+                drows.append(K.linear_dgrad(G, Wc[:, offs[i]:offs[i + 1]]))
+        return (None, None, None, None, dW.view_as(w), dgamma, dbeta, *drows)
+
+
 class ChannelDropoutLinearFn(torch.autograd.Function):
     """logits = (x * mask[b, c] / keep) @ W^T + b   — Dropout2d + 1x1 conv (decode_head.py:226-231)."""
 
@@ -486,8 +555,8 @@ class LightHamHead(nn.Module):
             r, (b, h, w) = _nhwc_rows(f)
             rows.append(r)
             hw.append((h, w))
-        x = ResizeCatFn.apply(B, hw, *rows)
-        x = self.squeeze.fused(x, act=2, sync=self.syncbn)
+        sq = self.squeeze
+        x = SqueezeFoldFn.apply(B, hw, sq.bn, self.syncbn, sq.conv.weight, sq.bn.weight, sq.bn.bias, *rows)
         H, W = hw[0]
         x = self.hamburger.fused(x, B, H * W, self.syncbn)
         x = self.align.fused(x, act=2, sync=self.syncbn)
