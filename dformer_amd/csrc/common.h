@@ -227,17 +227,29 @@ template <> DFM_INLINE bf16x8_t pack16x8<f16_t>(const float* v) {
 // per 1024-thread block so the nblk partials of a column are read by 16 lanes in parallel.
 //   MODE 0: out0[e]                      MODE 1: e < n0 ? out0[e] : out1[e - n0]
 //   MODE 2: depthwise layout, n0 = k*k+1: i = e % n0, c = e / n0 -> i < n0-1 ? out0[c*(n0-1)+i] : out1[c]
+// one row-lane's share of a column: sum over b = rl, rl + 16, ... < nblk of part[b * n + e], in
+// that order, with 8 loads in flight (the sums are short latency-bound chains)
+DFM_INLINE float ps_lane_sum(const float* __restrict__ part, long n, long e, int nblk, int rl) {
+  float s = 0.f;
+  int b = rl;
+  for (; b + 7 * 16 < nblk; b += 8 * 16) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = part[(long)(b + 16 * i) * n + e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+  }
+  for (; b < nblk; b += 16) s += part[(long)b * n + e];
+  return s;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(1024) void partial_sum_kernel(int nblk, long n, const float* __restrict__ part,
                                                            float* __restrict__ out0, float* __restrict__ out1, long n0,
                                                            int accumulate) {
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const long e = blockIdx.x * 64L + cl;
-  float s = 0.f;
-  if (e < n) {
-#pragma unroll 4
-    for (int b = rl; b < nblk; b += 16) s += part[(long)b * n + e];
-  }
+  const float s = e < n ? ps_lane_sum(part, n, e, nblk, rl) : 0.f;
   __shared__ float red[16][64];
   red[rl][cl] = s;
   __syncthreads();

@@ -915,7 +915,7 @@ template <typename T>
 long b3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, const float* w,
                int id, void* dx, long lddx, int acc, float* part, hipStream_t s) {
   const W3Geom g = w3_geom<T>(B, H, W, C);
-  DFM_LAUNCH(dw3_stream_bwd_kernel<T>, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C,
+  DFM_LAUNCH((dw3_stream_bwd_kernel<T>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C,
                      g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, w, id,
                      (T*)dx, lddx, acc, part);
   return g.nsb;
@@ -956,10 +956,11 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
   DFM_CHECK_ARG(dw_aligned<T>(C, x, ldx) && dw_aligned<T>(C, y, ldy) && (!gout || dw_aligned<T>(C, gout, ldg)),
                 "dwconv: C, row strides and pointers must be 16-byte vector aligned");
   DFM_CHECK_ARG(k == 3 || k == 7, "dwconv: k=%d unsupported", k);
-  // streaming 3x3 wins on the mid-size stages (60x80 / 30x40 planes: 4-17% faster on DFormer-B);
-  // the LDS-tiled kernel stays ahead on the 120x160 and 15x20 planes
+  // streaming 3x3 wins up to 60x80 planes with its round-aware chunking (60x80 / 30x40: 4-17 %
+  // faster on DFormer-B, 15x20 x 2048: 21 vs 24 us); the LDS-tiled kernel stays ahead on the 120x160
+  // planes (302 vs 328 us at 512 channels, profiles/r04_dw3_geom_sweep.txt)
   const long plane = (long)H * W;
-  if (k == 3 && plane >= 1024 && plane <= 6144) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
+  if (k == 3 && plane <= 6144) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
   const int G = C / DwCfg<T>::CPT;
   // channel groups per block: as many as the tile geometry allows without idling lanes
 #define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)

@@ -703,11 +703,7 @@ __global__ __launch_bounds__(1024) void partial_sum_group_kernel(PsGroup g) {
   const DfmPartialSum& ps = g.p[q];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const long e = (blockIdx.x - g.blk0[q]) * 64L + cl;
-  float s = 0.f;
-  if (e < ps.n) {
-#pragma unroll 4
-    for (int b = rl; b < ps.nblk; b += 16) s += ps.part[(long)b * ps.n + e];
-  }
+  const float s = e < ps.n ? ps_lane_sum(ps.part, ps.n, e, ps.nblk, rl) : 0.f;
   __shared__ float red[16][64];
   red[rl][cl] = s;
   __syncthreads();
