@@ -687,10 +687,17 @@ DFM_INLINE void splitk_reduce_block(const GemmArgs& a, long blk) {
   const int o = threadIdx.x % PER, g = threadIdx.x / PER;
   const long idx = blk * PER + o;
   float v = 0.f;
-  if (idx < total) {
+  if (idx < total) {  // splits g, g + G, ... in order, 8 loads in flight
     const float* p = a.ws + idx;
-#pragma unroll 4
-    for (int s = g; s < a.splits; s += G) v += p[(long)s * total];
+    int s = g;
+    for (; s + 7 * G < a.splits; s += 8 * G) {
+      float t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = p[(long)(s + i * G) * total];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v += t[i];
+    }
+    for (; s < a.splits; s += G) v += p[(long)s * total];
   }
   if (G > 1) {
     red[g][o] = v;
