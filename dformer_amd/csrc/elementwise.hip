@@ -97,16 +97,13 @@ __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const
 #pragma unroll
     for (int e = 0; e < V; ++e) aux[c0 + e] = k0[e];
   }
-  for (long r = r0 + rl; r < r1; r += RL) {
-    float xv[V];
-    ldvec<T>(x + r * ldx + c0, xv);
+  // one row's contribution; rows are added in order, four rows' loads in flight at a time
+  auto add_row = [&](long r, float* xv, const float* yv) {
     if (MODE == 1) {
 #pragma unroll
       for (int e = 0; e < V; ++e) xv[e] -= k0[e];
     }
     if (MODE == 0) {
-      float yv[V];
-      if (y) ldvec<T>(y + r * ldy + c0, yv);
       const float sc = p1 ? p1[r / rps] : 1.f;
 #pragma unroll
       for (int e = 0; e < V; ++e) s0[e] += (y ? xv[e] * yv[e] : xv[e]) * sc;
@@ -117,14 +114,30 @@ __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const
         s1[e] += xv[e] * xv[e];
       }
     } else {
-      float gv[V];
-      ldvec<T>(y + r * ldy + c0, gv);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        s0[e] += gv[e];
-        s1[e] += gv[e] * (xv[e] - mu[e]) * rs[e];
+        s0[e] += yv[e];
+        s1[e] += yv[e] * (xv[e] - mu[e]) * rs[e];
       }
     }
+  };
+  constexpr bool HAS_Y = MODE != 1;
+  long r = r0 + rl;
+  for (; r + 3 * RL < r1; r += 4 * RL) {
+    float xv[4][V], yv[4][V];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ldvec<T>(x + (r + u * RL) * ldx + c0, xv[u]);
+      if (HAS_Y && y) ldvec<T>(y + (r + u * RL) * ldy + c0, yv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) add_row(r + u * RL, xv[u], yv[u]);
+  }
+  for (; r < r1; r += RL) {
+    float xv[V], yv[V];
+    ldvec<T>(x + r * ldx + c0, xv);
+    if (HAS_Y && y) ldvec<T>(y + r * ldy + c0, yv);
+    add_row(r, xv, yv);
   }
 #pragma unroll
   for (int e = 0; e < V; ++e) {
