@@ -592,7 +592,9 @@ template <typename T>
 long w7l_nsb(int B, int H, int W, int C) {
   const long ntiles = (long)B * cdiv(H, W7L_TH) * cdiv(W, W7L_TW);
   const long slabs = cdiv(C / DwCfg<T>::CPT, W7L_NG);
-  return std::max(1L, std::min(ntiles, (768 + slabs - 1) / slabs));
+  // one round of blocks: the kernel holds 2 blocks per CU (196 VGPRs), 512 on the chip (768 ran
+  // 1.5 rounds: 459.8-460.7 vs 461.1-461.4 images/s)
+  return std::max(1L, std::min(ntiles, (512 + slabs - 1) / slabs));
 }
 
 template <typename T>
