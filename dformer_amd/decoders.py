@@ -496,6 +496,8 @@ class NMF2D(nn.Module):
         D = x.shape[1]
         bases = self._build_bases(B, D, x.device)
         steps = self.train_steps if self.training else self.eval_steps
+        if not torch.is_grad_enabled() and bases.shape[2] == 64:  # inference: the one-call entry point
+            return K.nmf_fwd(x.view(B, N, D).contiguous(), bases.float().contiguous(), steps, 1e-6).view(B * N, D)
         y = NMF2DFn.apply(x.view(B, N, D), bases, steps, 1e-6)
         return y.view(B * N, D)
 

@@ -808,6 +808,20 @@ def nmf_update_bwd_mm(g, a, num, den, out, A2=None, S=None, Mg=None, eps=1e-6, b
     return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
 
 
+def nmf_fwd(x, bases, steps, eps=1e-6):
+    """NMF2D forward in one library call (dfm_nmf_fwd): x [B, N, D], bases [B, D, 64] float32 -> y [B, N, D]."""
+    Bb, N, D = x.shape
+    R = bases.shape[2]
+    assert x.is_contiguous() and bases.is_contiguous() and bases.dtype == torch.float32
+    nbytes = lib.dfm_nmf_fwd_workspace_size(dtype_code(x), Bb, N, D, R)
+    assert nbytes > 0, "dfm_nmf_fwd: unsupported shape / rank"
+    ws = _ws(nbytes, x.device)
+    y = torch.empty_like(x)
+    check(lib.dfm_nmf_fwd(dtype_code(x), Bb, N, D, R, steps, eps, ptr(x), ptr(bases), ptr(y), ptr(ws), nbytes,
+                          stream()), "dfm_nmf_fwd")
+    return y
+
+
 def softmax_rows(x):
     y = torch.empty_like(x)
     check(lib.dfm_softmax_rows(x.numel() // x.shape[-1], x.shape[-1], ptr(x), ptr(y), stream()), "dfm_softmax_rows")

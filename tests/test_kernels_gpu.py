@@ -836,6 +836,32 @@ def test_nmf_update_mm_fused(rows):
     assert rel(ga2, g * num * r) < 1e-5 and rel(gden2, -g * out * r) < 1e-5
 
 
+@pytest.mark.parametrize("dt,Bb,N,D,steps", [(torch.float32, 2, 300, 512, 6), (torch.bfloat16, 2, 300, 512, 7),
+                                              (torch.bfloat16, 16, 4800, 512, 7), (torch.float16, 3, 77, 96, 2),
+                                              (torch.float32, 1, 64, 64, 0)])
+def test_nmf_fwd_entry_point(dt, Bb, N, D, steps):
+    """dfm_nmf_fwd (the whole NMF2D forward in one call, ham_head.py:60-145) gives the same bits as
+    NMF2DFn's launch-by-launch forward, and stays within fp32 rounding of a torch fp32 restatement."""
+    from dformer_amd.decoders import NMF2DFn
+    Kk = K()
+    g0 = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.rand(Bb, N, D, device=DEV, generator=g0).to(dt)
+    bases = torch.rand(Bb, D, 64, device=DEV, generator=g0)
+    bases = bases / bases.norm(dim=1, keepdim=True)
+    with torch.no_grad():
+        y = Kk.nmf_fwd(x, bases, steps, 1e-6)
+        y_ref = NMF2DFn.apply(x, bases.clone(), steps, 1e-6)
+    assert torch.equal(y, y_ref)
+    if dt == torch.float32:  # torch fp32 restatement of the update loop
+        xf, Bt = x.float(), bases.clone()
+        C = torch.softmax(xf @ Bt, dim=-1)
+        for _ in range(steps):
+            C = C * (xf @ Bt) / (C @ (Bt.transpose(1, 2) @ Bt) + 1e-6)
+            Bt = Bt * (xf.transpose(1, 2) @ C) / (Bt @ (C.transpose(1, 2) @ C) + 1e-6)
+        C = C * (xf @ Bt) / (C @ (Bt.transpose(1, 2) @ Bt) + 1e-6)
+        assert rel(y, C @ Bt.transpose(1, 2)) < 1e-4
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (2, 8, 12, 64, 96, 40), (1, 30, 40, 120, 160, 37),
                                             (2, 7, 9, 28, 36, 64)])
