@@ -3,7 +3,7 @@
 # bench.py reads for roofline.traffic), then configs 2 and 5
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
-T=r04f
+T=${1:-r04f}
 timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/${T}_pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/${T}_pytest_gpu.log | tail -5
 [ $rc -eq 0 ] || exit 11
