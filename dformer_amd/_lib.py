@@ -67,8 +67,12 @@ _SIGS = {
     "dfm_nmf_update_mm": (c_int, [c_int, c_long, c_int, P, P, P, c_float, P, P, P, c_int, P]),
     "dfm_nmf_update_bwd_mm": (c_int, [c_int, c_long, c_int, P, P, P, P, P, P, P, c_float, P, P, c_int, P, P, P,
                                       c_int, P]),
-    "dfm_nmf_fwd_workspace_size": (c_size_t, [c_int, c_int, c_long, c_long, c_int]),
-    "dfm_nmf_fwd": (c_int, [c_int, c_int, c_long, c_long, c_int, c_int, c_float, P, P, P, P, c_long, P]),
+    "dfm_nmf_saved_size": (c_size_t, [c_int, c_int, c_long, c_long, c_int, c_int]),
+    "dfm_nmf_fwd_workspace_size": (c_size_t, [c_int, c_int, c_long, c_long, c_int, c_int]),
+    "dfm_nmf_bwd_workspace_size": (c_size_t, [c_int, c_int, c_long, c_long, c_int, c_int]),
+    "dfm_nmf_fwd": (c_int, [c_int, c_int, c_long, c_long, c_int, c_int, c_float, P, P, P, P, c_long, P, c_long, P]),
+    "dfm_nmf_bwd": (c_int, [c_int, c_int, c_long, c_long, c_int, c_int, c_float, P, P, P, c_long, P, P, P, c_long,
+                            P]),
     "dfm_colsum_workspace": (c_size_t, [c_long, c_int]),
     "dfm_colsum": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P, c_int, P, P]),
     "dfm_cast": (c_int, [c_int, c_int, c_long, P, P, P]),

@@ -309,13 +309,26 @@ class NMF2DFn(torch.autograd.Function):
     x float32: every product in float32. x bfloat16 (the bf16 model; the reference's autocast runs
     these bmm in bf16): the products that stream x (x B, x^T C and their backward twins) and the
     output B C^T take bf16 operands with float32 accumulation; coef / bases, the small R x R
-    products and every multiplicative update stay float32 (nmf_update emits the bf16 operand copy)."""
+    products and every multiplicative update stay float32 (nmf_update emits the bf16 operand copy).
+
+    Rank 64 runs as two library calls (dfm_nmf_fwd keeping every step's factors, dfm_nmf_bwd);
+    entry=False issues the same launches one by one from here (the bit-identity reference of
+    tests/test_kernels_gpu.py::test_nmf_entry_points, and the path for other ranks)."""
 
     @staticmethod
-    def forward(ctx, x, bases, steps, eps):
+    def forward(ctx, x, bases, steps, eps, entry=True):
         x = x.contiguous()
         lp = x.dtype in (torch.bfloat16, torch.float16)
         B0 = bases.contiguous()
+        if entry and B0.shape[2] == 64:
+            # rank 64 (the config's MD_R): the whole loop and its backward are library entry points
+            # (dfm_nmf_fwd / dfm_nmf_bwd) issuing the launches below in the same order
+            B0 = B0.float()
+            y, saved = K.nmf_fwd(x, B0, steps, eps, keep=True)
+            ctx.entry, ctx.steps, ctx.eps = True, steps, eps
+            ctx.save_for_backward(x, B0, saved)
+            return y
+        ctx.entry = False
         f32 = dict(device=x.device, dtype=torch.float32)
 
         def xmm(b16, a_t=False):  # x-streaming product, float32 out
@@ -360,6 +373,10 @@ class NMF2DFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         K.TAG = "decoder.bwd"
+        if ctx.entry:
+            x, B0, saved = ctx.saved_tensors
+            gx = K.nmf_bwd(x, B0, saved, gy.contiguous(), ctx.steps, ctx.eps)
+            return gx, None, None, None, None
         x, B0, coef0 = ctx.saved_tensors
         eps = ctx.eps
         lp = x.dtype in (torch.bfloat16, torch.float16)
@@ -420,7 +437,7 @@ class NMF2DFn(torch.autograd.Function):
         Qc = K.pack_slices(Qs, torch.empty(Bb, D, T * R, device=x.device, dtype=x.dtype))
         gx = K.bmm(Pc, Qc, b_t=True)                              # sum_i P_i Q_i^T, x.dtype
         ctx.hist = ctx.final = None
-        return gx, None, None, None
+        return gx, None, None, None, None
 
     @staticmethod
     def _backward_unfused(ctx, x, gy, gC, gB, upd_bwd, gx_term):
@@ -496,7 +513,7 @@ class NMF2D(nn.Module):
         D = x.shape[1]
         bases = self._build_bases(B, D, x.device)
         steps = self.train_steps if self.training else self.eval_steps
-        if not torch.is_grad_enabled() and bases.shape[2] == 64:  # inference: the one-call entry point
+        if not torch.is_grad_enabled() and bases.shape[2] == 64:  # inference: nothing kept for a backward
             return K.nmf_fwd(x.view(B, N, D).contiguous(), bases.float().contiguous(), steps, 1e-6).view(B * N, D)
         y = NMF2DFn.apply(x.view(B, N, D), bases, steps, 1e-6)
         return y.view(B * N, D)

@@ -808,18 +808,38 @@ def nmf_update_bwd_mm(g, a, num, den, out, A2=None, S=None, Mg=None, eps=1e-6, b
     return (ga, gnum, gden, g16) if bf16_copy else (ga, gnum, gden)
 
 
-def nmf_fwd(x, bases, steps, eps=1e-6):
-    """NMF2D forward in one library call (dfm_nmf_fwd): x [B, N, D], bases [B, D, 64] float32 -> y [B, N, D]."""
+def nmf_fwd(x, bases, steps, eps=1e-6, keep=False):
+    """NMF2D forward in one library call (dfm_nmf_fwd): x [B, N, D], bases [B, D, 64] float32 -> y
+    [B, N, D]; keep=True also returns the saved factors for nmf_bwd (a uint8 buffer)."""
     Bb, N, D = x.shape
     R = bases.shape[2]
     assert x.is_contiguous() and bases.is_contiguous() and bases.dtype == torch.float32
-    nbytes = lib.dfm_nmf_fwd_workspace_size(dtype_code(x), Bb, N, D, R)
+    dt = dtype_code(x)
+    nbytes = lib.dfm_nmf_fwd_workspace_size(dt, Bb, N, D, R, steps)
     assert nbytes > 0, "dfm_nmf_fwd: unsupported shape / rank"
+    saved = None
+    if keep:
+        sb = lib.dfm_nmf_saved_size(dt, Bb, N, D, R, steps)
+        saved = torch.empty(sb, device=x.device, dtype=torch.uint8)
     ws = _ws(nbytes, x.device)
     y = torch.empty_like(x)
-    check(lib.dfm_nmf_fwd(dtype_code(x), Bb, N, D, R, steps, eps, ptr(x), ptr(bases), ptr(y), ptr(ws), nbytes,
-                          stream()), "dfm_nmf_fwd")
-    return y
+    check(lib.dfm_nmf_fwd(dt, Bb, N, D, R, steps, eps, ptr(x), ptr(bases), ptr(y), ptr(saved),
+                          saved.numel() if keep else 0, ptr(ws), nbytes, stream()), "dfm_nmf_fwd")
+    return (y, saved) if keep else y
+
+
+def nmf_bwd(x, bases, saved, gy, steps, eps=1e-6):
+    """Gradient of nmf_fwd's y w.r.t. x (dfm_nmf_bwd) from the factors nmf_fwd(keep=True) saved."""
+    Bb, N, D = x.shape
+    R = bases.shape[2]
+    assert gy.is_contiguous() and gy.dtype == x.dtype
+    dt = dtype_code(x)
+    nbytes = lib.dfm_nmf_bwd_workspace_size(dt, Bb, N, D, R, steps)
+    ws = _ws(nbytes, x.device)
+    gx = torch.empty_like(x)
+    check(lib.dfm_nmf_bwd(dt, Bb, N, D, R, steps, eps, ptr(x), ptr(bases), ptr(saved), saved.numel(), ptr(gy),
+                          ptr(gx), ptr(ws), nbytes, stream()), "dfm_nmf_bwd")
+    return gx
 
 
 def softmax_rows(x):

@@ -344,14 +344,22 @@ int dfm_nmf_update_bwd_mm(int batch, long rows, int R, const float* g, const flo
                           const float* a, const float* num, const float* den, const float* out, float eps,
                           const float* Mg, float* ga, int accumulate_ga, float* gnum, float* gden, void* gnum16,
                           int copy_dtype, dfm_stream_t stream);
-/* The whole NMF2D forward (ham_head.py:60-145: coef = softmax(x B0), `steps` updates of C and B,
- * the final C update, y = C B^T) in one call, rank R = 64, for inference hosts: x [batch][N][D]
- * (dtype), bases [batch][D][R] float32 (not modified), y [batch][N][D] (dtype). Enqueues exactly the
- * launches decoders.NMF2DFn issues (identical results); keeps nothing for a backward.
- * workspace: dfm_nmf_fwd_workspace_size bytes (0 = unsupported shape / rank). */
-size_t dfm_nmf_fwd_workspace_size(int dtype, int batch, long N, long D, int R);
+/* The NMF2D forward and backward (ham_head.py:60-145: coef = softmax(x B0), `steps` updates of C and B,
+ * the final C update, y = C B^T; rank R = 64) as two calls: x [batch][N][D] (dtype), bases
+ * [batch][D][R] float32 (a constant: not modified, no gradient), y / gy / gx [batch][N][D] (dtype).
+ * dfm_nmf_fwd keeps every step's factors in `saved` (dfm_nmf_saved_size bytes) for dfm_nmf_bwd, or
+ * nothing when saved is NULL (inference); the backward returns gx = dL/dx through every update.
+ * Workspaces: dfm_nmf_fwd_workspace_size (sized for saved == NULL, which needs the most) and
+ * dfm_nmf_bwd_workspace_size bytes; sizes 0 = unsupported dtype / shape / rank. */
+size_t dfm_nmf_saved_size(int dtype, int batch, long N, long D, int R, int steps);
+size_t dfm_nmf_fwd_workspace_size(int dtype, int batch, long N, long D, int R, int steps);
+size_t dfm_nmf_bwd_workspace_size(int dtype, int batch, long N, long D, int R, int steps);
 int dfm_nmf_fwd(int dtype, int batch, long N, long D, int R, int steps, float eps, const void* x,
-                const float* bases, void* y, void* workspace, long workspace_bytes, dfm_stream_t stream);
+                const float* bases, void* y, void* saved, long saved_bytes, void* workspace, long workspace_bytes,
+                dfm_stream_t stream);
+int dfm_nmf_bwd(int dtype, int batch, long N, long D, int R, int steps, float eps, const void* x,
+                const float* bases, const void* saved, long saved_bytes, const void* gy, void* gx, void* workspace,
+                long workspace_bytes, dfm_stream_t stream);
 /* row softmax over R (NMF coef init, ham_head.py:48-49) and its backward */
 int dfm_softmax_rows(long rows, int R, const float* x, float* y, dfm_stream_t stream);
 int dfm_softmax_rows_bwd(long rows, int R, const float* y, const float* dy, float* dx, int accumulate,
