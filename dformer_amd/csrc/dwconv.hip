@@ -967,6 +967,10 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
   // channel groups per block: as many as the tile geometry allows without idling lanes
 #define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)
   if (k == 3) {
+    // 64-channel groups (whole 128-byte lines per pixel) on the 120x160 planes: 297-300 vs 307 us at
+    // 512 channels, 128-129 vs 138 at 256 (4 x 32 tiles; 16 x 16 tiles with 8 outputs per thread
+    // hold 169 VGPRs and lose, profiles/r04_dw3_geom_sweep.txt)
+    if (G >= 8) GO(3, 8);
     if (G >= 4) GO(3, 4);
     if (G >= 2) GO(3, 2);
     GO(3, 1);
