@@ -267,11 +267,14 @@ def main():
     if not args.no_census:
         table = census(step)
         dom = max(table, key=lambda n: table[n]["measured_ms"])
-    # HIP-graph mode (default at every world size, RCCL collectives included: tests/test_graph_gpu.py
-    # captures the SyncBN / bucket / loss collectives through a one-rank group; DFM_GRAPH=0 disables;
-    # a multi-rank RCCL capture has not run on real N > 1 hardware yet — parity there is unverified):
-    # the whole step is captured once and replayed, so ~2.3k kernel launches cost one graph launch
-    use_graph = not args.eager and os.environ.get("DFM_GRAPH", "1") != "0"
+    # HIP-graph mode: the whole step is captured once and replayed, so ~1.6k kernel launches cost one
+    # graph launch. Default at world 1 (DFM_GRAPH=0 disables). At world > 1 the step runs EAGERLY unless
+    # DFM_GRAPH=1: a captured multi-rank RCCL step has never run on N > 1 hardware (only the one-rank
+    # RCCL capture of tests/test_graph_gpu.py has, and one capture_end abort was seen there before the
+    # capture waited for the watchdog), and an abort inside a capture cannot be caught and would lose
+    # the whole run. The bench line's "launch" field says which mode ran.
+    graph_env = os.environ.get("DFM_GRAPH", "1" if world == 1 else "0")
+    use_graph = not args.eager and graph_env != "0"
     if use_graph:
         step = GraphedTrainStep(model, opt, rgb, dep, lab)
     torch.cuda.synchronize()

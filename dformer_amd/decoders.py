@@ -76,6 +76,12 @@ def bn_batch_stats(x, bn, sync):
     return mean, rstd, count
 
 
+# test-only probe (tests/test_dp_gpu.py): when a dict, bn_grad_stats records per BN layer (by id) the
+# float64 sums [sum dy*xhat, sum dy, sum |dy*xhat|, sum |dy|] of the rows it reduces, from the same
+# dy / x / mean / rstd its kernel reads
+BN_PROBE = None
+
+
 def bn_grad_stats(x, dy, mean, rstd, bn, sync):
     """BatchNorm backward statistics st2 = (sum dy, sum dy * xhat) of NHWC rows. Returns (st2 for the
     input gradient, dgamma, dbeta). The local statistics ARE this rank's beta / gamma gradients
@@ -84,6 +90,10 @@ def bn_grad_stats(x, dy, mean, rstd, bn, sync):
     straight into the flat gradient slots, laid out [beta | gamma] by train.fused_chains; under
     SyncBN an all-reduced copy feeds the input gradient."""
     out = gslot_rows(bn.bias, bn.weight) if bn is not None and bn.affine else None
+    if BN_PROBE is not None and bn is not None:
+        dyd = dy.double()
+        t = dyd * ((x.double() - mean.double()) * rstd.double())
+        BN_PROBE[id(bn)] = torch.stack([t.sum(0), dyd.sum(0), t.abs().sum(0), dyd.abs().sum(0)])
     st = K.bn_bwd_stats(x, dy, mean, rstd, out=out.view(2, -1) if out is not None else None)
     stg = st
     if sync and collectives_on():

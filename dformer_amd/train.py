@@ -67,12 +67,21 @@ def _chain_order(params, chains):
             tail = [q for q in ch[1:] if id(q) in present and id(q) not in members]
             follow[id(ch[0])] = tail
             members.update(id(q) for q in tail)
-    out = []
-    for p in params:
-        if id(p) in members:
-            continue
+    out, done = [], set()
+
+    def emit(p):  # p, then its chain's tail (a tail member that heads a chain of its own brings that tail)
+        if id(p) in done:
+            return
+        done.add(id(p))
         out.append(p)
-        out.extend(follow.get(id(p), []))
+        for q in follow.get(id(p), []):
+            emit(q)
+
+    for p in params:
+        if id(p) not in members:
+            emit(p)
+    for p in params:  # members reachable from no emitted head (chains that form a cycle)
+        emit(p)
     assert len(out) == len(params), "chain reorder lost or duplicated a parameter"
     return out
 

@@ -119,3 +119,31 @@ def test_frozen_chain_head_keeps_members_in_their_group():
     a, b, c, d = (torch.zeros(1, requires_grad=True) for _ in range(4))
     assert _chain_order([b, c, d], [[a, b, c]]) == [b, c, d]   # head absent: members keep their place
     assert _chain_order([c, d, a], [[a, b, c]]) == [d, a, c]   # head present, b absent: c follows a
+
+
+def test_no_redefined_test_names():
+    """Every test function name is defined once per test module (a redefinition silently shadows
+    the first copy, so pytest would never run it)."""
+    import ast
+    import glob
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    for path in sorted(glob.glob(os.path.join(here, "test_*.py"))):
+        with open(path) as f:
+            tree = ast.parse(f.read(), path)
+        names = [n.name for n in tree.body if isinstance(n, (ast.FunctionDef, ast.ClassDef))]
+        dup = sorted({n for n in names if names.count(n) > 1})
+        assert not dup, f"{os.path.basename(path)} redefines {dup}"
+
+
+def test_chain_order_overlapping_chains():
+    """A chain member that heads a chain of its own brings that chain's tail along; chains forming
+    a cycle and members whose head is absent keep every parameter exactly once."""
+    from dformer_amd.train import _chain_order
+    a, b, c, d, e = (nn.Parameter(torch.zeros(1)) for _ in range(5))
+    order = _chain_order([a, b, c, d, e], [[a, c], [c, e]])
+    assert [id(p) for p in order] == [id(a), id(c), id(e), id(b), id(d)]
+    order = _chain_order([a, b, c], [[a, b], [b, a]])
+    assert sorted(id(p) for p in order) == sorted(id(p) for p in (a, b, c))
+    order = _chain_order([b, c, d], [[a, c, d]])  # head a not present: no regrouping
+    assert [id(p) for p in order] == [id(b), id(c), id(d)]

@@ -874,356 +874,6 @@ def test_nmf_entry_points(dt, Bb, N, D, steps):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (1, 17, 23, 67, 92, 37), (2, 8, 12, 64, 96, 40), (1, 30, 40, 37, 50, 19), (1, 13, 11, 100, 90, 16),
-                                                (1, 24, 20, 96, 80, 40), (2, 10, 14, 20, 28, 64), (1, 7, 9, 56, 72, 3),
-                                                (1, 133, 183, 530, 730, 40), (1, 5, 4, 300, 290, 8)])
-def test_seg_loss(dt, B, h, w, H, W, ncls):
-    k = K()
-    lg = torch.randn(B, h, w, ncls, device=DEV).to(dt)
-    lab = torch.randint(0, ncls, (B, H, W), device=DEV)
-    lab[torch.rand(B, H, W, device=DEV) < 0.1] = 255
-    out = k.seg_loss_fwd(lg.view(-1, ncls), B, h, w, ncls, lab)
-    lr = lg.float().permute(0, 3, 1, 2).contiguous().requires_grad_()
-    up = F.interpolate(lr, (H, W), mode="bilinear", align_corners=False)
-    ce = F.cross_entropy(up, lab, reduction="none", ignore_index=255)
-    loss = ce[lab != 255].mean()
-    assert abs((out[0] / out[1]).item() - loss.item()) < 1e-4 * abs(loss.item())
-    loss.backward()
-    dl = k.seg_loss_bwd(lg.view(-1, ncls), B, h, w, ncls, lab, out)
-    assert rel(dl.view(B, h, w, ncls).permute(0, 3, 1, 2), lr.grad) < 1e-3
-
-
-@pytest.mark.parametrize("B,h,w,H,W", [(2, 15, 20, 120, 160), (2, 30, 40, 120, 160), (2, 60, 80, 120, 160),
-                                       (2, 133, 183, 530, 730), (1, 30, 40, 37, 50), (1, 9, 11, 100, 90)])
-def test_seg_loss_bwd_deterministic(B, h, w, H, W):
-    """every upsampling factor is bitwise reproducible run to run: integer factors (tile partials)
-    and config 5's 133x183 -> 530x730 (separable x-pass / y-pass), builder.py:203,230"""
-    k = K()
-    ncls = 40
-    lg = torch.randn(B, h, w, ncls, device=DEV).to(torch.bfloat16)
-    lab = torch.randint(0, ncls, (B, H, W), device=DEV)
-    lab[:, :5] = 255
-    out = k.seg_loss_fwd(lg.view(-1, ncls), B, h, w, ncls, lab)
-    d1 = k.seg_loss_bwd(lg.view(-1, ncls), B, h, w, ncls, lab, out)
-    d2 = k.seg_loss_bwd(lg.view(-1, ncls), B, h, w, ncls, lab, out)
-    assert torch.equal(d1, d2)
-
-
-def test_adamw_matches_torch():
-    k = K()
-    p = torch.randn(10000, device=DEV)
-    g = torch.randn(10000, device=DEV)
-    m, v = torch.zeros_like(p), torch.zeros_like(p)
-    pr = p.clone().requires_grad_()
-    opt = torch.optim.AdamW([pr], lr=6e-5, betas=(0.9, 0.999), weight_decay=0.01)
-    copy = torch.empty(10000, device=DEV, dtype=torch.bfloat16)
-    for step in range(1, 4):
-        pr.grad = g * step
-        opt.step()
-        k.adamw(p, g * step, m, v, 6e-5, 0.9, 0.999, 1e-8, 0.01, step, 1.0, copy)
-    assert rel(p, pr.detach()) < 1e-6
-    assert rel(copy.float(), p) < 1e-2
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("C", [32, 64, 256, 576])
-def test_residual_bwd_and_ln_dres(dt, C):
-    k = K()
-    rows, B = 4000, 4
-    dout = torch.randn(rows, C, device=DEV).to(dt)
-    f = torch.randn(rows, C, device=DEV).to(dt)
-    ls = torch.rand(C, device=DEV)
-    rs = torch.rand(B, device=DEV)
-    df, dls = k.residual_bwd(dout, f, ls, rs, rows // B)
-    rsx = rs.repeat_interleave(rows // B)[:, None]
-    assert rel(df.float(), dout.float() * ls * rsx) < TOL[dt]
-    assert rel(dls, (dout.float() * f.float() * rsx).sum(0)) < TOL[dt]
-    x = torch.randn(rows, C, device=DEV).to(dt)
-    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
-    _, mean, rstd = k.layernorm(x, g, b)
-    dx_a, _, _ = k.layernorm_bwd(x, f, g, mean, rstd, dres=dout)
-    dx_b, _, _ = k.layernorm_bwd(x, f, g, mean, rstd)
-    assert rel(dx_a.float(), dx_b.float() + dout.float()) < TOL[dt]
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-def test_dgrad_gelu_grad_epilogue(dt):
-    k = K()
-    dy = torch.randn(3000, 64, device=DEV).to(dt)
-    w = torch.randn(64, 512, device=DEV).to(dt)
-    pre = torch.randn(3000, 512, device=DEV).to(dt)
-    out = k.linear_dgrad(dy, w, gelu_grad_of=pre)
-    pr = pre.float().requires_grad_()
-    torch.nn.functional.gelu(pr).backward(dy.float() @ w.float())
-    assert rel(out.float(), pr.grad) < TOL[dt]
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("C", [64, 96, 36])
-def test_dual_mul(dt, C):
-    """(src*m1, src*m2) in one pass, on column slices of wider buffers (vector path) and C % 8 != 0."""
-    k = K()
-    rows = 1000
-    buf = torch.randn(rows, 3 * C + 8, device=DEV).to(dt)
-    src, m1, m2 = buf[:, :C], buf[:, C:2 * C], buf[:, 2 * C:3 * C]
-    outb = torch.empty(rows, 2 * C + 8, device=DEV, dtype=dt)
-    o1, o2 = k.dual_mul(src, m1, m2, out1=outb[:, :C], out2=outb[:, C + 8:2 * C + 8])
-    assert rel(o1.float(), src.float() * m1.float()) < TOL[dt]
-    assert rel(o2.float(), src.float() * m2.float()) < TOL[dt]
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("rows", [19200, 777, 4800])
-def test_wgrad_group(dt, rows):
-    """dfm_gemm_group: the weight gradients queued inside kernels.wgrad_group() (different M / N, bias
-    gradient columns, an accumulating problem, strided operand views) against torch fp32 and against
-    the same GEMMs launched one by one."""
-    k = K()
-    shapes = [(256, 256, True), (640, 256, True), (128, 128, False), (384, 512, True), (64, 96, True),
-              (1024, 256, True), (256, 1024, False), (128, 384, True), (32, 48, True)]
-    dys, xs, refs = [], [], []
-    for n_out, n_in, bias in shapes:
-        dyb = torch.randn(rows, n_out + 8, device=DEV).to(dt)
-        dys.append(dyb[:, 8:])
-        xs.append(torch.randn(rows, n_in, device=DEV).to(dt))
-    base = torch.randn(128, 128, device=DEV)
-    outs = []
-    with k.wgrad_group():
-        for i, (n_out, n_in, bias) in enumerate(shapes):
-            if i == 2:  # accumulate into an existing gradient
-                o = base.clone()
-                k.linear_wgrad(dys[i], xs[i], out=o, accumulate=True)
-                outs.append((o, None))
-            else:
-                outs.append(k.linear_wgrad(dys[i], xs[i], bias_grad=bias) if bias else (k.linear_wgrad(dys[i], xs[i]), None))
-    for i, (n_out, n_in, bias) in enumerate(shapes):
-        ref = dys[i].float().t() @ xs[i].float()
-        if i == 2:
-            ref = ref + base
-        dw, db = outs[i]
-        assert rel(dw, ref) < TOL[dt] * 2, (i, rel(dw, ref))
-        if bias:
-            assert rel(db, dys[i].float().sum(0)) < TOL[dt], i
-        single = k.linear_wgrad(dys[i], xs[i], bias_grad=bias)
-        sw = single[0] if bias else single
-        if i != 2:
-            assert rel(dw, sw) < (1e-5 if dt == torch.float32 else TOL[dt]), i
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-def test_gemm_nmf_backward_input_gradient_descriptor(dt):
-    """The exact descriptor of the NMF backward's input gradient (decoders.py NMF2DFn.backward:
-    gx = Pc Qc^T, M = N_pix 4800, N = D 512, K = T*R 896, batch 16, both operands k-contiguous), the
-    call a round-3 profiling run faulted next to (hipErrorIllegalAddress): through dfm_gemm vs torch
-    fp32, synchronised, plus a re-run into a poisoned output (every element rewritten)."""
-    k = K()
-    B, N, D, KR = 16, 4800, 512, 896
-    pc = torch.randn(B, N, KR, device=DEV).to(dt)
-    qc = torch.randn(B, D, KR, device=DEV).to(dt)
-    gx = k.bmm(pc, qc, b_t=True)
-    torch.cuda.synchronize()
-    ref = torch.bmm(pc.float(), qc.float().transpose(1, 2))
-    assert gx.shape == (B, N, D) and gx.dtype == dt
-    assert rel(gx.float(), ref) < GTOL[dt]
-    out = torch.full_like(gx, float("nan"))
-    k.bmm(pc, qc, b_t=True, out=out)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out.float()).all()
-    assert torch.equal(out, gx)  # deterministic
-
-
-@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("M,N,Kd,ldx", [(19200, 256, 256, 256), (4800 + 37, 200, 1024, 1032), (130, 64, 64, 64),
-                                        (307200 // 16, 512, 64, 64), (777, 1152, 128, 136)])
-def test_gemm_fused_epilogues_step_shapes(dt, M, N, Kd, ldx):
-    """Forward and input-gradient GEMMs at step-like shapes (whichever kernel the routing picks) with
-    every fused epilogue the Block uses: bias + GELU with GELU' stored from a column offset (act 3),
-    the multiplier, the residual with column / row scales, beta accumulation, the GELU'-multiplier
-    of an input gradient; ragged M, N % 64 != 0, strided A, one-slice (K = 64) tiles."""
-    k = K()
-    tol = GTOL[dt]
-    xb = torch.randn(M, ldx, device=DEV).to(dt)
-    x = xb[:, :Kd]
-    w = (torch.randn(N, Kd, device=DEV) / Kd ** 0.5).to(dt)
-    b = torch.randn(N, device=DEV)
-    lin = x.float() @ w.float().t() + b
-    # act 3 from column c0: GELU(v) out, GELU'(v) in preact[:, :N - c0]
-    c0 = (N // 2) // 8 * 8
-    pre = torch.empty(M, N - c0, device=DEV, dtype=dt)
-    y = k.linear(x, w, b, act=3, preact=pre, act_col0=c0)
-    v = lin[:, c0:]
-    cdf = 0.5 * (1 + torch.erf(v / math.sqrt(2)))
-    pdf = torch.exp(-0.5 * v * v) / math.sqrt(2 * math.pi)
-    assert rel(y[:, :c0].float(), lin[:, :c0]) < tol
-    assert rel(y[:, c0:].float(), v * cdf) < tol
-    assert rel(pre.float(), cdf + v * pdf) < 2 * tol
-    # multiplier with preact (the conv-modulation q * a)
-    mul = torch.randn(M, N, device=DEV).to(dt)
-    pre2 = torch.empty(M, N, device=DEV, dtype=dt)
-    y = k.linear(x, w, b, mul=mul, preact=pre2)
-    assert rel(pre2.float(), lin) < tol
-    assert rel(y.float(), lin * mul.float()) < tol
-    # residual + layer scale + per-image row scale (Block residual / DropPath epilogue)
-    res = torch.randn(M, N, device=DEV).to(dt)
-    cs = torch.rand(N, device=DEV)
-    rps = max(1, M // 5)
-    rs = torch.rand((M + rps - 1) // rps, device=DEV)
-    y = k.linear(x, w, b, res=res, colscale=cs, rowscale=rs, rows_per_scale=rps)
-    rsx = rs.repeat_interleave(rps)[:M, None]
-    assert rel(y.float(), res.float() + cs * rsx * lin) < tol
-    # beta accumulate into the output
-    acc = torch.randn(M, N, device=DEV).to(dt)
-    want = acc.float() + lin
-    k.linear(x, w, b, out=acc, beta=1.0)
-    assert rel(acc.float(), want) < tol
-    # input gradient: dx[M, N] = dy[M, Kd] @ wd[Kd, N], plain / GELU'-multiplier / accumulate
-    dy = xb[:, :Kd]
-    wd = (torch.randn(Kd, N, device=DEV) / Kd ** 0.5).to(dt)
-    ref = dy.float() @ wd.float()
-    assert rel(k.linear_dgrad(dy, wd).float(), ref) < tol
-    h = torch.randn(M, N, device=DEV).to(dt)
-    hf = h.float()
-    gg = 0.5 * (1 + torch.erf(hf / math.sqrt(2))) + hf * torch.exp(-0.5 * hf * hf) / math.sqrt(2 * math.pi)
-    assert rel(k.linear_dgrad(dy, wd, gelu_grad_of=h).float(), ref * gg) < tol
-    assert rel(k.linear_dgrad(dy, wd, mul=h).float(), ref * hf) < tol
-    dx = torch.randn(M, N, device=DEV).to(dt)
-    want = dx.float() + ref
-    k.linear_dgrad(dy, wd, out=dx, accumulate=True)
-    assert rel(dx.float(), want) < tol
-
-
-def test_pack_slices():
-    """dfm_pack_slices: n sources of mixed dtypes side by side into one [rows, n*cols] tensor (the NMF
-    backward's rank-R factors), exactly torch.cat of the converted sources."""
-    k = K()
-    srcs = [torch.randn(3, 50, 64, device=DEV).to(dt) for dt in (torch.float32, torch.bfloat16, torch.float32,
-                                                                    torch.float16, torch.float32)]
-    for odt in (torch.bfloat16, torch.float32, torch.float16):
-        out = torch.empty(3, 50, 5 * 64, device=DEV, dtype=odt)
-        k.pack_slices(srcs, out)
-        assert torch.equal(out, torch.cat([s.to(odt) for s in srcs], -1))
-    # the element-wise path: 12-column slices (not a multiple of 8)
-    odd = [torch.randn(40, 12, device=DEV).to(dt) for dt in (torch.float32, torch.bfloat16, torch.float16)]
-    out = torch.empty(40, 36, device=DEV, dtype=torch.bfloat16)
-    k.pack_slices(odd, out)
-    assert torch.equal(out, torch.cat([s.to(torch.bfloat16) for s in odd], -1))
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-def test_deferred_reductions_bit_identical(dt):
-    """Inside wgrad_group the reduction second stages (LN dgamma/dbeta, layer-scale dscale, DW3x3
-    fused and DW7x7 weight gradients) are deferred to one dfm_partial_sum_group launch: the results
-    must equal the immediate two-launch path bit for bit, including a DW7 weight gradient issued on a
-    side stream and joined before the flush (the attention backward's depth branch)."""
-    Kk = K()
-    B, H, W, C = 2, 30, 40, 96
-    P = B * H * W
-    g = torch.Generator(device=DEV).manual_seed(5)
-    x = torch.randn(P, C, device=DEV, generator=g).to(dt)
-    dy = torch.randn(P, C, device=DEV, generator=g).to(dt)
-    f = torch.randn(P, C, device=DEV, generator=g).to(dt)
-    gam = torch.rand(C, device=DEV, generator=g) + 0.5
-    bet = torch.randn(C, device=DEV, generator=g)
-    ls = torch.rand(C, device=DEV, generator=g)
-    rs = torch.rand(B, device=DEV, generator=g)
-    w3 = torch.randn(C, 1, 3, 3, device=DEV, generator=g) / 3
-    xn, mu, rstd = Kk.layernorm(x, gam, bet)
-
-    def run():
-        out = {}
-        out["ln"] = Kk.layernorm_bwd(x, dy, gam, mu, rstd, dres=f)
-        out["res"] = Kk.residual_bwd(dy, f, ls, rs, H * W)
-        out["dw3"] = Kk.dwconv_bwd(x, dy, (B, H, W), w3, 3, add_identity=True)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            out["dw7"] = Kk.dwconv_bwd_weight(x, dy, (B, H, W), 7)
-        torch.cuda.current_stream().wait_stream(side)
-        return out
-
-    ref = run()
-    with Kk.wgrad_group():
-        got = run()
-    torch.cuda.synchronize()
-    for k in ref:
-        for a, b in zip(got[k], ref[k]):
-            assert torch.equal(a, b), k
-
-
-@pytest.mark.parametrize("dt", DTYPES)
-def test_group_scale(dt):
-    """dfm_group_scale: per-group (per-image) channel scale in one launch, in place and strided."""
-    Kk = K()
-    B, rows, C = 4, 300, 96
-    x = torch.randn(B * rows, C, device=DEV).to(dt)
-    sc = torch.rand(B, C, device=DEV)
-    ref = (x.float().view(B, rows, C) * sc[:, None, :]).view(B * rows, C)
-    got = Kk.group_scale(x, sc, rows)
-    assert rel(got.float(), ref) <= TOL[dt] / 4
-    wide = torch.randn(B * rows, C + 32, device=DEV).to(dt)
-    v = wide[:, 16:16 + C]
-    exp = (v.float().view(B, rows, C) * sc[:, None, :]).view(B * rows, C)
-    Kk.group_scale(v, sc, rows, out=v)
-    assert rel(v.float(), exp) <= TOL[dt] / 4
-
-
-@pytest.mark.parametrize("rows", [4800, 77, 512])
-def test_nmf_update_mm_fused(rows):
-    """dfm_nmf_update_mm / _bwd_mm (rank 64, the den products fused) vs torch fp32 compositions of
-    the same update (ham_head.py:120-141) and of its backward with the folded Gram gradient terms."""
-    Kk = K()
-    Bb, R, eps = 3, 64, 1e-6
-    g0 = torch.Generator(device=DEV).manual_seed(9)
-    a = torch.rand(Bb, rows, R, device=DEV, generator=g0) + 0.1
-    num = torch.rand(Bb, rows, R, device=DEV, generator=g0)
-    Bm = torch.rand(Bb, 96, R, device=DEV, generator=g0)
-    M = Bm.transpose(1, 2) @ Bm
-    out, den, o16 = Kk.nmf_update_mm(a, num, M, eps, bf16_copy=True)
-    den_ref = a @ M
-    out_ref = a * num / (den_ref + eps)
-    assert rel(den, den_ref) < 1e-5 and rel(out, out_ref) < 1e-5
-    assert torch.equal(o16, out.to(torch.bfloat16))
-    g = torch.randn(Bb, rows, R, device=DEV, generator=g0)
-    A2 = torch.rand(Bb, rows, R, device=DEV, generator=g0)
-    S = torch.randn(Bb, R, R, device=DEV, generator=g0)
-    ga, gnum, gden, g16 = Kk.nmf_update_bwd_mm(g, a, num, den, out, A2=A2, S=S, Mg=M, eps=eps, bf16_copy=True)
-    ge = g + A2 @ (S + S.transpose(1, 2))
-    r = 1.0 / (den + eps)
-    gden_ref = -ge * out * r
-    assert rel(gnum, ge * a * r) < 1e-5 and rel(gden, gden_ref) < 1e-5
-    assert rel(ga, ge * num * r + gden_ref @ M) < 1e-5
-    assert torch.equal(g16, gnum.to(torch.bfloat16))
-    ga2, gnum2, gden2 = Kk.nmf_update_bwd_mm(g, a, num, den, out, eps=eps)  # no folded terms
-    assert rel(ga2, g * num * r) < 1e-5 and rel(gden2, -g * out * r) < 1e-5
-
-
-@pytest.mark.parametrize("dt,Bb,N,D,steps", [(torch.float32, 2, 300, 512, 6), (torch.bfloat16, 2, 300, 512, 7),
-                                              (torch.bfloat16, 16, 4800, 512, 7), (torch.float16, 3, 77, 96, 2),
-                                              (torch.float32, 1, 64, 64, 0)])
-def test_nmf_fwd_entry_point(dt, Bb, N, D, steps):
-    """dfm_nmf_fwd (the whole NMF2D forward in one call, ham_head.py:60-145) gives the same bits as
-    NMF2DFn's launch-by-launch forward, and stays within fp32 rounding of a torch fp32 restatement."""
-    from dformer_amd.decoders import NMF2DFn
-    Kk = K()
-    g0 = torch.Generator(device=DEV).manual_seed(11)
-    x = torch.rand(Bb, N, D, device=DEV, generator=g0).to(dt)
-    bases = torch.rand(Bb, D, 64, device=DEV, generator=g0)
-    bases = bases / bases.norm(dim=1, keepdim=True)
-    with torch.no_grad():
-        y = Kk.nmf_fwd(x, bases, steps, 1e-6)
-        y_ref = NMF2DFn.apply(x, bases.clone(), steps, 1e-6)
-    assert torch.equal(y, y_ref)
-    if dt == torch.float32:  # torch fp32 restatement of the update loop
-        xf, Bt = x.float(), bases.clone()
-        C = torch.softmax(xf @ Bt, dim=-1)
-        for _ in range(steps):
-            C = C * (xf @ Bt) / (C @ (Bt.transpose(1, 2) @ Bt) + 1e-6)
-            Bt = Bt * (xf.transpose(1, 2) @ C) / (Bt @ (C.transpose(1, 2) @ C) + 1e-6)
-        C = C * (xf @ Bt) / (C @ (Bt.transpose(1, 2) @ Bt) + 1e-6)
-        assert rel(y, C @ Bt.transpose(1, 2)) < 1e-4
-
-
-@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (2, 8, 12, 64, 96, 40), (1, 30, 40, 120, 160, 37),
                                             (2, 7, 9, 28, 36, 64)])
 def test_seg_loss_fwd_grad_fused(dt, B, h, w, H, W, ncls):
