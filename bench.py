@@ -35,7 +35,19 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-METRIC = "images/s training-step, DFormer-B 480×640 bs=16/GPU, 1/2/4/8 MI355X"
+METRIC = "images/s training-step, DFormer-B 480×640 bs=16/GPU, 1/2/4/8 MI355X"  # BASELINE.json config 3 / 4
+
+
+def metric_name(args):
+    """BASELINE.json's metric for its own workload (DFormer-B + ham, 480x640, bs 16 per GPU, bf16);
+    any other configuration (configs 2 and 5) is named by its own workload."""
+    if (args.arch, args.decoder, args.height, args.width, args.batch, args.dtype) == \
+            ("DFormer-Base", "ham", 480, 640, 16, "bf16"):
+        return METRIC
+    return (f"images/s training-step, {args.arch}+{args.decoder} {args.height}×{args.width} bs={args.batch}/GPU, "
+            f"{args.dtype}, MI355X")
+
+
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_PEAK_TFS = {"bf16": 2500.0, "f32": 157.3}  # dense bf16 MFMA; f32-input MFMA (= vector rate)
 # SURVEY §8d: DFormer-B fwd 90.3 GFLOP/img, training step ~3x -> 4.33 TFLOP per bs-16 step
@@ -317,7 +329,7 @@ def main():
     value = images / elapsed
     ms_step = elapsed / args.steps * 1e3
     result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "metric": metric_name(args), "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (random-init weights)",
         "config": {"workload": f"{args.arch}+{args.decoder} train step fwd+bwd+AdamW",

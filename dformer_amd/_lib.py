@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdformer_hip.so")
+# DFM_LIB_PATH: load another build of the library (profiling A/B of compile-time variants only)
+LIB_PATH = os.environ.get("DFM_LIB_PATH") or os.path.join(_HERE, "libdformer_hip.so")
 
 F32, BF16, F16 = 0, 1, 2
 
@@ -39,6 +40,11 @@ class PartialSum(ctypes.Structure):
                 ("layout", c_int), ("accumulate", c_int)]
 
 
+class ConvFFNDesc(ctypes.Structure):
+    """DfmConvFFNDesc: shape of one fused ConvFFN call."""
+    _fields_ = [("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("hidden", c_int), ("ln_eps", c_float)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dfm_last_error": (ctypes.c_char_p, []),
@@ -63,6 +69,10 @@ _SIGS = {
     "dfm_dwconv_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, P, c_long, P, c_long, P, c_int, P, c_long,
                                c_int, P, P, P, P, P]),
     "dfm_partial_sum_group": (c_int, [c_int, P, P]),
+    "dfm_convffn_supported": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)]),
+    "dfm_convffn_fwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 17),
+    "dfm_convffn_bwd_workspace_size": (c_size_t, [c_int, ctypes.POINTER(ConvFFNDesc)]),
+    "dfm_convffn_bwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 25 + [c_size_t, P]),
     "dfm_group_scale": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P]),
     "dfm_nmf_update_mm": (c_int, [c_int, c_long, c_int, P, P, P, c_float, P, P, P, c_int, P]),
     "dfm_nmf_update_bwd_mm": (c_int, [c_int, c_long, c_int, P, P, P, P, P, P, P, c_float, P, P, c_int, P, P, P,

@@ -1,0 +1,1006 @@
+// Fused ConvFFN (K4) for gfx950 — DFormer's MLP (models/encoders/DFormer.py:48-67) inside the Block
+// residual (DFormer.py:173-179):
+//
+//   out = x + rowscale[b] * ls * f,   f = fc2(g) + b2,   g = GELU(hpre),
+//   hpre = DW3x3(h) + bpos + h,       h = fc1(LN(x)) + b1          (rows = NHWC pixels)
+//
+// FORWARD (ffn_fwd_kernel): one workgroup per TH x TW tile of output pixels; the [P, R] hidden
+// activation is produced and consumed on the CU in chunks of HC channels (the depthwise conv is
+// per channel, so a hidden chunk needs only its own channels of h on the tile + 1-pixel halo):
+//   prologue  LN of x on the tile + halo -> Xs (LDS, 16-bit), mean / rstd of the tile saved
+//   per chunk [A] h^T = W1c xn^T + b1 (MFMA 16x16x32), zero outside the image -> Hs (LDS)
+//             [B] every lane computes DW3x3 + bpos + identity and GELU for exactly the 1 pixel x 8
+//                 channels it holds as the B operand of out^T += W2c g^T (MFMA): g goes from the VALU
+//                 straight into the matrix core; the lane's centre tap of h is stored to HBM (the one
+//                 hidden tensor the backward reads)
+//   epilogue  f = acc + b2 (saved for the layer-scale gradient), out = x + rowscale * ls * f.
+// HBM per pixel: read C (x, + halo from L2), write 2C (out, f) + R (h) elements + 8 B; the unfused
+// chain moved 5 hidden tensors (fc1 out, GELU, GELU', and their reads).
+//
+// BACKWARD, hidden part (ffn_bwd_kernel): one workgroup per (strip of tiles, hidden chunk). Per tile:
+//   [A] dg^T = W2c^T df^T on the tile + 1-pixel halo (MFMA; W2c^T held in registers for the strip)
+//   [B] hpre recomputed from h (tile + 2-pixel halo, LDS), GELU / GELU' from one erf evaluation,
+//       dhpre = dg GELU'(hpre) -> LDS; the depthwise weight / bias gradient sums ride in registers
+//       (each lane owns 4 hidden channels for the whole strip)
+//   [C] dh = DW3x3^T(dhpre) + dhpre on the tile -> HBM (for the fc1 input gradient GEMM) and LDS
+//   [D] dW2^T += g^T df, dW1 += dh^T LN(x) (MFMA, K = pixels, operands read with
+//       ds_read_b64_tr_b16 from [pixel][channel] LDS images), accumulated in registers over the strip
+// and writes per-strip partials that one fixed-order grouped sum reduces (deterministic). The fc1
+// input gradient (dh W1), the LayerNorm backward and the residual / layer-scale backward are the
+// library's GEMM / LN / residual entry points, issued by dfm_convffn_bwd.
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+
+namespace {
+
+// ---- 16-bit element helpers (bf16_t / f16_t storage)
+template <typename T> DFM_INLINE float lo16(uint32_t w);
+template <typename T> DFM_INLINE float hi16(uint32_t w);
+template <> DFM_INLINE float lo16<bf16_t>(uint32_t w) { return __uint_as_float(w << 16); }
+template <> DFM_INLINE float hi16<bf16_t>(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+template <> DFM_INLINE float lo16<f16_t>(uint32_t w) { return h2f((uint16_t)(w & 0xffffu)); }
+template <> DFM_INLINE float hi16<f16_t>(uint32_t w) { return h2f((uint16_t)(w >> 16)); }
+template <typename T> DFM_INLINE uint32_t pack2(float a, float b) {
+  return (uint32_t)bits16<T>(a) | ((uint32_t)bits16<T>(b) << 16);
+}
+template <typename T> DFM_INLINE void ld4h(const T* p, float* v) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = lo16<T>(u.x); v[1] = hi16<T>(u.x); v[2] = lo16<T>(u.y); v[3] = hi16<T>(u.y);
+}
+template <typename T> DFM_INLINE void st4h(T* p, const float* v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]));
+}
+template <typename T> DFM_INLINE void unpack8w(const uint4 u, float* v) {
+  v[0] = lo16<T>(u.x); v[1] = hi16<T>(u.x); v[2] = lo16<T>(u.y); v[3] = hi16<T>(u.y);
+  v[4] = lo16<T>(u.z); v[5] = hi16<T>(u.z); v[6] = lo16<T>(u.w); v[7] = hi16<T>(u.w);
+}
+DFM_INLINE bf16x8_t as_frag(uint4 u) { return __builtin_bit_cast(bf16x8_t, u); }
+template <typename T> DFM_INLINE bf16x8_t ldfrag(const T* p) { return as_frag(*reinterpret_cast<const uint4*>(p)); }
+
+// A / B fragment of v_mfma_f32_16x16x32 with K along the ROWS of a [k][n] 16-bit LDS image (pitch
+// in elements, a multiple of 4): lane l gets image[k0 + 8 (l >> 4) + j][n0 + (l & 15)], j < 8, read
+// by two ds_read_b64_tr_b16 (each 16-lane group transposes a 4-row x 16-column block).
+template <typename T>
+DFM_INLINE bf16x8_t tr_frag(const T* img, int pitch, int k0, int n0, int lane) {
+  typedef __attribute__((address_space(3))) short4_t lds_s4;
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const T* a0 = img + (k0 + 8 * (lane >> 4) + q) * pitch + n0 + 4 * p;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0 + 4 * pitch));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  const short8_t s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+struct FfnFwdArgs {
+  int B, H, W, R;
+  float eps;
+  long rps;  // rows per rowscale entry (H * W)
+  int tiles_x, tiles_y;
+  const void* x;
+  const float* lnw;
+  const float* lnb;
+  const void* w1;  // [R][C]
+  const float* b1;
+  const float* wpos;  // [R][9]
+  const float* bpos;
+  const void* w2;  // [C][R]
+  const float* b2;
+  const float* ls;
+  const float* rowscale;  // [B] or NULL
+  void* out;
+  void* f;
+  void* h;  // [P][R] saved for the backward
+  float* mean;
+  float* rstd;
+};
+
+// Forward geometry: 8 x 8 pixel tiles; each of the 4 waves owns every 4th hidden chunk of HC channels
+// and keeps its own partial out^T[C, T] in registers, so the chunk loop has no workgroup barrier:
+// a wave computes h for its chunk (tile + 1 halo, MFMA) into its private LDS buffer and reads it back
+// for the depthwise conv (wave-local LDS hand-off). The four partials are summed in a fixed order at
+// the end (deterministic).
+template <int C, int HC>
+struct FwdGeom {
+  static constexpr int TH = 8, TW = 8, T = TH * TW;
+  static constexpr int EW = TW + 2, T1 = (TH + 2) * EW, T1P = (T1 + 15) / 16 * 16;
+  static constexpr int XP = C + 8, HP = HC + 8;  // LDS pitches (elements): 16-byte rows, staggered banks
+  static constexpr int RB1 = HC / 16, CB1 = T1P / 16, KS1 = C / 32;
+  static constexpr int RB2 = C / 16, CB2 = T / 16, KS2 = HC / 32;
+  static constexpr int XS = T1P * XP, HS = T1P * HP, PS = 10 * HC;  // elements / floats
+  static constexpr int RED = T * C;                                   // floats of one partial
+  static constexpr size_t BODY = (size_t)(XS + 4 * HS) * 2 + (size_t)4 * PS * 4;
+  static constexpr size_t LDS = BODY > (size_t)2 * RED * 4 ? BODY : (size_t)2 * RED * 4;
+  static_assert(T % 16 == 0 && HC % 32 == 0 && C % 32 == 0, "tile geometry");
+};
+
+template <typename T, int C, int HC>
+__global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
+  using G = FwdGeom<C, HC>;
+  constexpr int TH = G::TH, TW = G::TW;
+  extern __shared__ __align__(16) unsigned char smem[];
+  T* Xs = reinterpret_cast<T*>(smem);  // [T1P][XP] LN(x) of tile + halo
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, lq = lane >> 4;
+  T* Hw = Xs + G::XS + wave * G::HS;  // this wave's [T1P][HP] h chunk
+  float* Pw = reinterpret_cast<float*>(Xs + G::XS + 4 * G::HS) + wave * G::PS;  // its taps + bias
+  int t = blockIdx.x;
+  const int tx = t % a.tiles_x;
+  t /= a.tiles_x;
+  const int ty = t % a.tiles_y;
+  const int b = t / a.tiles_y;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int H = a.H, W = a.W, R = a.R;
+  const T* __restrict__ x = static_cast<const T*>(a.x);
+  const T* __restrict__ w1 = static_cast<const T*>(a.w1);
+  const T* __restrict__ w2 = static_cast<const T*>(a.w2);
+  T* __restrict__ hsave = static_cast<T*>(a.h);
+
+  // ---- prologue: LayerNorm of the tile + 1-pixel halo (DFormer.py:58, eps 1e-6) into Xs; all of a
+  //      thread's rows are loaded before any is normalised (one round trip)
+  {
+    constexpr int GL = C / 8 < 64 ? C / 8 : 64, RPP = 256 / GL, NV = C / 8 / GL;
+    constexpr int NR = (G::T1P + RPP - 1) / RPP;
+    const int gl = tid % GL;
+    float4 lg[NV][2], lb[NV][2];
+#pragma unroll
+    for (int nv = 0; nv < NV; ++nv) {
+      const int c = 8 * (gl + nv * GL);
+      lg[nv][0] = *reinterpret_cast<const float4*>(a.lnw + c);
+      lg[nv][1] = *reinterpret_cast<const float4*>(a.lnw + c + 4);
+      lb[nv][0] = *reinterpret_cast<const float4*>(a.lnb + c);
+      lb[nv][1] = *reinterpret_cast<const float4*>(a.lnb + c + 4);
+    }
+    uint4 raw[NR][NV];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int e = r * RPP + tid / GL;
+      const int yy = y0 + e / G::EW - 1, xx = x0 + e % G::EW - 1;
+      const bool in = e < G::T1 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const long p = ((long)b * H + yy) * W + xx;
+#pragma unroll
+      for (int nv = 0; nv < NV; ++nv)
+        raw[r][nv] = in ? *reinterpret_cast<const uint4*>(x + p * C + 8 * (gl + nv * GL)) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int e = r * RPP + tid / GL;
+      const int ey = e / G::EW, ex = e % G::EW;
+      const int yy = y0 + ey - 1, xx = x0 + ex - 1;
+      const bool in = e < G::T1 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      float v[NV][8];
+      float s = 0.f;
+#pragma unroll
+      for (int nv = 0; nv < NV; ++nv) {
+        unpack8w<T>(raw[r][nv], v[nv]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[nv][j];
+      }
+      const float mu = group_sum<GL>(s) / C;
+      float q = 0.f;
+#pragma unroll
+      for (int nv = 0; nv < NV; ++nv)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = in ? v[nv][j] - mu : 0.f;
+          q += d * d;
+        }
+      const float rs = rsqrtf(group_sum<GL>(q) / C + a.eps);
+      if (e < G::T1P) {
+#pragma unroll
+        for (int nv = 0; nv < NV; ++nv) {
+          const float gw[8] = {lg[nv][0].x, lg[nv][0].y, lg[nv][0].z, lg[nv][0].w,
+                               lg[nv][1].x, lg[nv][1].y, lg[nv][1].z, lg[nv][1].w};
+          const float bw[8] = {lb[nv][0].x, lb[nv][0].y, lb[nv][0].z, lb[nv][0].w,
+                               lb[nv][1].x, lb[nv][1].y, lb[nv][1].z, lb[nv][1].w};
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = in ? (v[nv][j] - mu) * rs * gw[j] + bw[j] : 0.f;
+          st8<T>(Xs + e * G::XP + 8 * (gl + nv * GL), o);
+        }
+        if (in && gl == 0 && ey >= 1 && ey <= TH && ex >= 1 && ex <= TW) {
+          const long p = ((long)b * H + yy) * W + xx;
+          a.mean[p] = mu;
+          a.rstd[p] = rs;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  float4_t acc[G::CB2][G::RB2];  // this wave's partial out^T over its chunks
+#pragma unroll
+  for (int i = 0; i < G::CB2; ++i)
+#pragma unroll
+    for (int r = 0; r < G::RB2; ++r) acc[i][r] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nch = R / HC;
+  for (int ch = wave; ch < nch; ch += 4) {
+    const int c0 = ch * HC;
+    // taps (identity folded into the centre) + bias of the chunk -> this wave's Pw
+    for (int i = lane; i < G::PS; i += 64) {
+      const int tap = i / HC, j = i % HC;
+      Pw[i] = tap < 9 ? a.wpos[(long)(c0 + j) * 9 + tap] + (tap == 4 ? 1.f : 0.f) : a.bpos[c0 + j];
+    }
+    // [A] h^T[HC, T1P] = W1c[HC, C] xn^T  (+ b1; zero outside the image) -> Hw[pixel][channel]
+#pragma unroll
+    for (int rb = 0; rb < G::RB1; ++rb) {
+      bf16x8_t wa[G::KS1];
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks) wa[ks] = ldfrag(w1 + (long)(c0 + 16 * rb + l15) * C + 32 * ks + 8 * lq);
+      const float4 bias = *reinterpret_cast<const float4*>(a.b1 + c0 + 16 * rb + 4 * lq);
+#pragma unroll
+      for (int cb = 0; cb < G::CB1; ++cb) {
+        const int e = 16 * cb + l15;
+        float4_t hacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < G::KS1; ++ks) hacc = mma16<T>(wa[ks], ldfrag(Xs + e * G::XP + 32 * ks + 8 * lq), hacc);
+        const int ey = e / G::EW, ex = e % G::EW;
+        const int yy = y0 + ey - 1, xx = x0 + ex - 1;
+        const bool in = e < G::T1 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        float hv[4] = {hacc[0] + bias.x, hacc[1] + bias.y, hacc[2] + bias.z, hacc[3] + bias.w};
+        if (!in) hv[0] = hv[1] = hv[2] = hv[3] = 0.f;
+        st4h<T>(Hw + e * G::HP + 16 * rb + 4 * lq, hv);
+      }
+    }
+    // wave-local hand-off: this wave's own LDS writes are complete once lgkmcnt drains
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // [B] g = GELU(DW3x3(h) + bpos + h) for (1 pixel, 8 channels) per lane = its B fragment of
+    //     out^T[C, T] += W2c[C, HC] g^T
+    bf16x8_t wb[G::RB2][G::KS2];
+#pragma unroll
+    for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+      for (int ks = 0; ks < G::KS2; ++ks) wb[r][ks] = ldfrag(w2 + (long)(16 * r + l15) * R + c0 + 32 * ks + 8 * lq);
+#pragma unroll
+    for (int cb = 0; cb < G::CB2; ++cb) {
+      const int p = 16 * cb + l15, py = p / TW, px = p % TW;
+      const int yy = y0 + py, xx = x0 + px;
+      const bool in = yy < H && xx < W;
+#pragma unroll
+      for (int ks = 0; ks < G::KS2; ++ks) {
+        const int cc = 32 * ks + 8 * lq;
+        float hp[8];
+        {
+          const float4 p0 = *reinterpret_cast<const float4*>(Pw + 9 * HC + cc);
+          const float4 p1 = *reinterpret_cast<const float4*>(Pw + 9 * HC + cc + 4);
+          hp[0] = p0.x; hp[1] = p0.y; hp[2] = p0.z; hp[3] = p0.w;
+          hp[4] = p1.x; hp[5] = p1.y; hp[6] = p1.z; hp[7] = p1.w;
+        }
+        const T* hb = Hw + (py * G::EW + px) * G::HP + cc;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          const uint4 u = *reinterpret_cast<const uint4*>(hb + ((tap / 3) * G::EW + tap % 3) * G::HP);
+          if (tap == 4 && in) *reinterpret_cast<uint4*>(hsave + (((long)b * H + yy) * W + xx) * R + c0 + cc) = u;
+          float hv[8];
+          unpack8w<T>(u, hv);
+          const float4 q0 = *reinterpret_cast<const float4*>(Pw + tap * HC + cc);
+          const float4 q1 = *reinterpret_cast<const float4*>(Pw + tap * HC + cc + 4);
+          const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hp[j] = fmaf(wv[j], hv[j], hp[j]);
+        }
+        float g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = gelu_f(hp[j]);
+        const bf16x8_t gf = pack16x8<T>(g);
+#pragma unroll
+        for (int r = 0; r < G::RB2; ++r) acc[cb][r] = mma16<T>(wb[r][ks], gf, acc[cb][r]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the next chunk's phase A rewrites Hw / Pw: this wave's reads of them must have completed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // ---- fixed-order sum of the 4 partials: (w0 + w2) + (w1 + w3) in LDS (the body buffers are dead)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // 2 x [T * C] floats, element (cb, r, lane, j)
+  auto slot = [&](int buf, int cb, int r, int j) { return buf * G::RED + ((cb * G::RB2 + r) * 4 + j) * 64 + lane; };
+  if (wave >= 2) {
+#pragma unroll
+    for (int cb = 0; cb < G::CB2; ++cb)
+#pragma unroll
+      for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[slot(wave - 2, cb, r, j)] = acc[cb][r][j];
+  }
+  __syncthreads();
+  if (wave < 2) {
+#pragma unroll
+    for (int cb = 0; cb < G::CB2; ++cb)
+#pragma unroll
+      for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[cb][r][j] += red[slot(wave, cb, r, j)];
+  }
+  __syncthreads();
+  if (wave == 1) {
+#pragma unroll
+    for (int cb = 0; cb < G::CB2; ++cb)
+#pragma unroll
+      for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[slot(0, cb, r, j)] = acc[cb][r][j];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  // ---- epilogue (wave 0): f = acc + b2; out = x + rowscale * ls * f   (4 channels x 1 pixel per block)
+  T* __restrict__ out = static_cast<T*>(a.out);
+  T* __restrict__ fo = static_cast<T*>(a.f);
+#pragma unroll
+  for (int cb = 0; cb < G::CB2; ++cb) {
+    const int p = 16 * cb + l15, py = p / TW, px = p % TW;
+    const int yy = y0 + py, xx = x0 + px;
+    const bool in = yy < H && xx < W;
+    const long pg = ((long)b * H + (in ? yy : 0)) * W + (in ? xx : 0);
+    const float rsc = a.rowscale ? a.rowscale[pg / a.rps] : 1.f;
+#pragma unroll
+    for (int r = 0; r < G::RB2; ++r) {
+      const int c = 16 * r + 4 * lq;
+      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + c);
+      const float4 ll = *reinterpret_cast<const float4*>(a.ls + c);
+      float v[4] = {acc[cb][r][0] + red[slot(0, cb, r, 0)] + bb.x, acc[cb][r][1] + red[slot(0, cb, r, 1)] + bb.y,
+                    acc[cb][r][2] + red[slot(0, cb, r, 2)] + bb.z, acc[cb][r][3] + red[slot(0, cb, r, 3)] + bb.w};
+      if (!in) continue;
+      float xv[4];
+      ld4h<T>(x + pg * C + c, xv);
+      st4h<T>(fo + pg * C + c, v);
+      const float lv[4] = {ll.x, ll.y, ll.z, ll.w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = xv[j] + lv[j] * rsc * v[j];
+      st4h<T>(out + pg * C + c, o);
+    }
+  }
+}
+
+// ============================================================================ backward (hidden part)
+struct FfnBwdArgs {
+  int B, H, W, R;
+  int tiles_x, tiles_y, ntiles;
+  int nstrip, tiles_per_strip;
+  const void* x;
+  const float* mean;
+  const float* rstd;
+  const float* lnw;
+  const float* lnb;
+  const void* h;   // [P][R] saved by the forward
+  const void* df;  // [P][C] gradient of f (dout * rowscale * ls)
+  const void* w2;  // [C][R]
+  const float* wpos;
+  const float* bpos;
+  void* dh;          // [P][R]
+  float* part_w2;    // [nstrip][C * R]   dW2[c][r]
+  float* part_w1;    // [nstrip][R * C]   dW1[r][c]
+  float* part_b1;    // [nstrip][R]
+  float* part_pos;   // [nstrip][R * 10] dwpos (9 taps) | dbpos
+  float* part_b2;    // [nstrip][C]
+};
+
+
+// Backward geometry: 8 x 8 pixel tiles. The h chunk (tile + 2 halo) and df (tile + 1 halo) of the
+// NEXT tile are DMA'd (global_load_lds, no registers) into the idle half of double-buffered LDS
+// images while this tile is computed; x of this tile is loaded to registers at its start and
+// normalised into LDS late in the tile. The h image has padded 80-byte rows (a DMA writes lane-
+// linearly: every fifth 16-byte slot of a row is a pad slot the DMA fills from a zero page), so
+// the 9 tap reads of a pixel are one base address plus constant offsets; the df image has unpadded
+// 16-byte pieces XOR-swizzled by row (swz) for conflict-free reads.
+template <int C, int HC>
+struct BwdGeom {
+  static constexpr int TH = 8, TW = 8, T = TH * TW;
+  static constexpr int EW1 = TW + 2, T1 = (TH + 2) * EW1, T1P = (T1 + 15) / 16 * 16;
+  static constexpr int EW2 = TW + 4, T2 = (TH + 4) * EW2;
+  static constexpr int RB = HC / 16, CB1 = T1P / 16, KS1 = C / 32;
+  static constexpr int NCB1 = (CB1 * RB + 3) / 4;  // phase-A/B column blocks per wave
+  static constexpr int CB3 = C / 16, KS3 = T / 32;
+  static constexpr int NCB3 = (CB3 * RB + 3) / 4;  // phase-D column blocks per wave
+  static constexpr int NQ = HC / 8, ITEMS = T * NQ, NI = (ITEMS + 255) / 256;  // phase-C items
+  static constexpr int HP = HC + 8, XP = C + 8;   // padded pitches (elements)
+  static constexpr int HSL = HP / 8, PC = C / 8;  // 16-byte slots per h row, pieces per df / x row
+  static constexpr int NSH = T2 * HSL, NSD = T1P * PC;  // DMA slots per tile
+  static constexpr int NXV = (T * PC + 255) / 256;      // x vectors per thread
+  static constexpr int HS = T2 * HP, DS = T1P * C, XS = T * XP, DH = T1P * HP, GS = T * HP;  // elements
+  static constexpr size_t LDS = (size_t)(2 * HS + 2 * DS + XS + DH + 2 * GS) * 2 + (size_t)(10 * HC + 2 * C) * 4;
+  static_assert(HC % 32 == 0 && C % 32 == 0 && 4 % RB == 0 && 256 % NQ == 0 && 256 % PC == 0, "geometry");
+  static_assert((size_t)HS * 2 * 2 >= (size_t)256 * 8 * 4, "end-of-strip reduction space");
+};
+
+// 16-byte piece p of image row r sits at position p ^ swz(r) of that row
+template <int NPR> DFM_INLINE int swz(int r) {
+  if constexpr (NPR >= 8) return r & 7;
+  else if constexpr (NPR == 4) return (r >> 2) & 3;
+  else return 0;
+}
+// element offset of (row, element e) in an unpadded swizzled image of NPR 16-byte pieces per row
+template <int NPR> DFM_INLINE int sw_off(int row, int e) {
+  return row * NPR * 8 + (((e >> 3) ^ swz<NPR>(row)) << 3) + (e & 7);
+}
+// MFMA fragment, K along the rows of a swizzled image (row(k): the image row of k)
+template <int NPR, typename RowF>
+DFM_INLINE bf16x8_t tr_frag_sw(const bf16_t* img, int k0, int n0, int lane, RowF rowf) {
+  typedef __attribute__((address_space(3))) short4_t lds_s4;
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int k = k0 + 8 * (lane >> 4) + q;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + sw_off<NPR>(rowf(k), n0 + 4 * p)));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(img + sw_off<NPR>(rowf(k + 4), n0 + 4 * p)));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  const short8_t s = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, s);
+}
+
+__device__ __attribute__((aligned(16))) const unsigned int g_ffn_zero[4] = {0u, 0u, 0u, 0u};
+
+template <typename T, int C, int HC>
+__global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
+  using G = BwdGeom<C, HC>;
+  constexpr int TH = G::TH, TW = G::TW, HP = G::HP;
+  extern __shared__ __align__(16) unsigned char smem[];
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);  // 2 x [T2][HP]  h chunk, tile + 2 halo (padded)
+  bf16_t* Ds = Hs + 2 * G::HS;                     // 2 x [T1P][C]  df, tile + 1 halo (swizzled)
+  bf16_t* Xs = Ds + 2 * G::DS;                     // [T][XP]      LN(x) of the tile
+  bf16_t* Dh = Xs + G::XS;                         // [T1P][HP]    dhpre, tile + 1 halo
+  bf16_t* Gs = Dh + G::DH;                         // [T][HP]      g of the tile
+  bf16_t* DHs = Gs + G::GS;                        // [T][HP]      dh of the tile
+  float* Ps = reinterpret_cast<float*>(DHs + G::GS);  // [10][HC] taps (identity in the centre) + bias
+  float* Lw = Ps + 10 * HC;                           // LayerNorm weight | bias
+  float* red = reinterpret_cast<float*>(smem);        // end of strip only (Hs region)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, lq = lane >> 4;
+  const int H = a.H, W = a.W, R = a.R;
+  const int nch = R / HC;
+  const int xcd = blockIdx.x & 7, j8 = blockIdx.x >> 3;
+  const int chunk = j8 % nch;
+  const int strip = (j8 / nch) * 8 + xcd;
+  if (strip >= a.nstrip) return;
+  const int c0 = chunk * HC;
+  const T* __restrict__ hg = static_cast<const T*>(a.h);
+  const T* __restrict__ dfg = static_cast<const T*>(a.df);
+  const T* __restrict__ xg = static_cast<const T*>(a.x);
+  const T* __restrict__ w2 = static_cast<const T*>(a.w2);
+  T* __restrict__ dhg = static_cast<T*>(a.dh);
+  const void* zero = (const void*)g_ffn_zero;
+
+  for (int i = tid; i < 10 * HC; i += 256) {
+    const int tap = i / HC, j = i % HC;
+    Ps[i] = tap < 9 ? a.wpos[(long)(c0 + j) * 9 + tap] + (tap == 4 ? 1.f : 0.f) : a.bpos[c0 + j];
+  }
+  for (int i = tid; i < 2 * C; i += 256) Lw[i] = i < C ? a.lnw[i] : a.lnb[i - C];
+  const int rb = wave % G::RB;
+  const int chl = 16 * rb + 4 * lq;  // the lane's 4 hidden channels (within the chunk) in [A] / [B]
+  bf16x8_t wa[G::KS1];  // W2c^T[HC, C] as A fragments: row = hidden channel 16 rb + l15, k = c
+#pragma unroll
+  for (int ks = 0; ks < G::KS1; ++ks) {
+    typedef __attribute__((ext_vector_type(8))) unsigned short us8;
+    us8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(unsigned short, w2[(long)(32 * ks + 8 * lq + j) * R + c0 + 16 * rb + l15]);
+    wa[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  float dwp[4][9], dbp[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    dbp[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dwp[j][k] = 0.f;
+  }
+  float db1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) db1[j] = 0.f;
+  float4_t aw2[G::NCB3], aw1[G::NCB3];
+#pragma unroll
+  for (int i = 0; i < G::NCB3; ++i) aw2[i] = aw1[i] = float4_t{0.f, 0.f, 0.f, 0.f};
+  constexpr int RS2 = 256 / C;
+  float db2 = 0.f;
+
+  const int t_begin = strip * a.tiles_per_strip;
+  const int t_end = min(a.ntiles, t_begin + a.tiles_per_strip);
+  auto tile_xy = [&](int tile, int& b, int& y0, int& x0) {
+    const int tx = tile % a.tiles_x, r = tile / a.tiles_x;
+    x0 = tx * TW;
+    y0 = (r % a.tiles_y) * TH;
+    b = r / a.tiles_y;
+  };
+  // DMA the h chunk and df of `tile` into buffer `buf` (wave-instruction wi writes slots 64 wi ..;
+  // lanes past an image's end are inactive; out-of-image pixels and pad slots read a zero page)
+  auto issue = [&](int tile, int buf) {
+    int b, y0, x0;
+    tile_xy(tile, b, y0, x0);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // opaque: the per-lane address math is redone here, not kept live
+    unsigned char* hbase = smem + buf * G::HS * 2;
+    for (int wi = wave; wi * 64 < G::NSH; wi += 4) {
+      const int q = wi * 64 + ln;
+      if (q < G::NSH) {
+        const int row = q / G::HSL, slot = q - row * G::HSL;
+        const int yy = y0 + row / G::EW2 - 2, xx = x0 + row % G::EW2 - 2;
+        const void* src = zero;
+        if (slot < HC / 8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          src = hg + (((long)b * H + yy) * W + xx) * R + c0 + 8 * slot;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                         (void __attribute__((address_space(3)))*)(hbase + wi * 1024), 16, 0, 0);
+      }
+    }
+    unsigned char* dbase = smem + (2 * G::HS + buf * G::DS) * 2;
+    for (int wi = wave; wi * 64 < G::NSD; wi += 4) {
+      const int q = wi * 64 + ln;
+      if (q < G::NSD) {
+        const int row = q / G::PC, pos = q - row * G::PC, piece = pos ^ swz<G::PC>(row);
+        const int yy = y0 + row / G::EW1 - 1, xx = x0 + row % G::EW1 - 1;
+        const void* src = zero;
+        if (row < G::T1 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          src = dfg + (((long)b * H + yy) * W + xx) * C + 8 * piece;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                         (void __attribute__((address_space(3)))*)(dbase + wi * 1024), 16, 0, 0);
+      }
+    }
+  };
+
+  if (t_begin < t_end) issue(t_begin, 0);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int cur = (tile - t_begin) & 1;
+    int b, y0, x0;
+    tile_xy(tile, b, y0, x0);
+    const bf16_t* Hc = Hs + cur * G::HS;
+    const bf16_t* Dc = Ds + cur * G::DS;
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): this tile's DMAs (and everything older)
+    __builtin_amdgcn_s_barrier();
+    // x of this tile + the forward's LN statistics (registers; normalised into Xs after [B])
+    uint4 xv[G::NXV];
+    float xmu[G::NXV], xrs[G::NXV];
+#pragma unroll
+    for (int k = 0; k < G::NXV; ++k) {
+      const int q = tid + 256 * k, pi = q / G::PC;
+      const bool in = (G::T * G::PC % 256 == 0 || pi < G::T) && y0 + pi / TW < H && x0 + pi % TW < W;
+      const long p = ((long)b * H + y0 + pi / TW) * W + x0 + pi % TW;
+      xv[k] = in ? *reinterpret_cast<const uint4*>(xg + p * C + 8 * (q % G::PC)) : make_uint4(0, 0, 0, 0);
+      xmu[k] = in ? a.mean[p] : 0.f;
+      xrs[k] = in ? a.rstd[p] : 0.f;
+    }
+#ifndef FFN_EXP_NO_DMA
+    if (tile + 1 < t_end) issue(tile + 1, cur ^ 1);  // in flight under this tile
+#endif
+    // ---- [A] dg^T = W2c^T df^T (tile + 1 halo), [B] hpre, GELU / GELU' (one erf), dhpre -> Dh,
+    //      g (tile) -> Gs, dwpos / dbpos sums; one column block at a time
+#ifndef FFN_EXP_NO_B
+#pragma unroll 1
+    for (int i = 0; i < G::NCB1; ++i) {
+      const int cb = wave / G::RB + i * (4 / G::RB);
+      if ((G::CB1 * G::RB) % 4 != 0 && cb >= G::CB1) break;
+      const int e = 16 * cb + l15;
+      float4_t dg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < G::KS1; ++ks)
+        dg = mma16<T>(wa[ks], ldfrag(Dc + sw_off<G::PC>(e, 32 * ks + 8 * lq)), dg);
+      if (e < G::T1) {
+        const int ey = e / G::EW1, ex = e % G::EW1;
+        const bf16_t* hb = Hc + (ey * G::EW2 + ex) * HP + chl;  // tap (0, 0); tap t at + off(t)
+        float hv[9][4];
+        float hp[4];
+        {
+          const float4 bp = *reinterpret_cast<const float4*>(Ps + 9 * HC + chl);
+          hp[0] = bp.x; hp[1] = bp.y; hp[2] = bp.z; hp[3] = bp.w;
+        }
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+          ld4h<T>(reinterpret_cast<const T*>(hb + ((tap / 3) * G::EW2 + tap % 3) * HP), hv[tap]);
+          const float4 wt = *reinterpret_cast<const float4*>(Ps + tap * HC + chl);
+          hp[0] = fmaf(wt.x, hv[tap][0], hp[0]);
+          hp[1] = fmaf(wt.y, hv[tap][1], hp[1]);
+          hp[2] = fmaf(wt.z, hv[tap][2], hp[2]);
+          hp[3] = fmaf(wt.w, hv[tap][3], hp[3]);
+        }
+        float g[4], dhp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float cdf, pdf;
+          normal_cdf_pdf(hp[j], cdf, pdf);
+          g[j] = hp[j] * cdf;
+          dhp[j] = Num<T>::to_f(Num<T>::from_f(dg[j] * fmaf(hp[j], pdf, cdf)));  // rounded as stored
+        }
+        st4h<T>(reinterpret_cast<T*>(Dh + e * HP + chl), dhp);
+        if (ey >= 1 && ey <= TH && ex >= 1 && ex <= TW) {
+          const int pi = (ey - 1) * TW + ex - 1;
+          const bool in = y0 + ey - 1 < H && x0 + ex - 1 < W;
+          if (!in) g[0] = g[1] = g[2] = g[3] = 0.f;
+          st4h<T>(reinterpret_cast<T*>(Gs + pi * HP + chl), g);
+          if (in) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              dbp[j] += dhp[j];
+#pragma unroll
+              for (int tap = 0; tap < 9; ++tap) dwp[j][tap] = fmaf(dhp[j], hv[tap][j], dwp[j][tap]);
+            }
+          }
+        }
+      }
+    }
+#endif
+    // ---- LN(x) of the tile (the forward's statistics) -> Xs
+#pragma unroll
+    for (int k = 0; k < G::NXV; ++k) {
+      const int q = tid + 256 * k, pi = q / G::PC, c = 8 * (q % G::PC);
+      if (G::T * G::PC % 256 != 0 && pi >= G::T) break;
+      float v[8], o[8];
+      unpack8w<T>(xv[k], v);
+      const float4 w0 = *reinterpret_cast<const float4*>(Lw + c), w1 = *reinterpret_cast<const float4*>(Lw + c + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(Lw + C + c), b1 = *reinterpret_cast<const float4*>(Lw + C + c + 4);
+      const float wl[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float bl[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = xrs[k] != 0.f ? (v[j] - xmu[k]) * xrs[k] * wl[j] + bl[j] : 0.f;
+      st8<T>(reinterpret_cast<T*>(Xs + pi * G::XP + c), o);
+    }
+    lds_barrier();
+    // ---- [C] dh = DW3x3^T(dhpre) + dhpre on the tile -> HBM and DHs; db1
+#ifndef FFN_EXP_NO_C
+#pragma unroll
+    for (int it = 0; it < G::NI; ++it) {
+      const int item = tid + 256 * it;
+      if (G::ITEMS % 256 != 0 && item >= G::ITEMS) break;
+      const int pi = item / G::NQ, cc = 8 * (item % G::NQ);
+      const int py = pi / TW, px = pi % TW;
+      const bool in = y0 + py < H && x0 + px < W;
+      const bf16_t* db = Dh + ((py + 2) * G::EW1 + px + 2) * HP + cc;  // dhpre at q - off(tap 0)
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {  // transposed conv: dh[q] = sum_tap w[tap] dhpre[q - off(tap)]
+        float dv[8];
+        unpack8w<T>(*reinterpret_cast<const uint4*>(db - ((tap / 3) * G::EW1 + tap % 3) * HP), dv);
+        const float4 q0 = *reinterpret_cast<const float4*>(Ps + tap * HC + cc);
+        const float4 q1 = *reinterpret_cast<const float4*>(Ps + tap * HC + cc + 4);
+        const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = fmaf(wv[j], dv[j], d[j]);
+      }
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (in) {
+        u = make_uint4(pack2<T>(d[0], d[1]), pack2<T>(d[2], d[3]), pack2<T>(d[4], d[5]), pack2<T>(d[6], d[7]));
+        float r[8];
+        unpack8w<T>(u, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) db1[j] += r[j];
+        *reinterpret_cast<uint4*>(dhg + (((long)b * H + y0 + py) * W + x0 + px) * R + c0 + cc) = u;
+      }
+      *reinterpret_cast<uint4*>(DHs + pi * HP + cc) = u;
+    }
+#endif
+    // ---- [D1] dW2^T[HC, C] += g^T df (K = tile pixels: df rows of the tile's interior); db2 (chunk 0)
+    auto int_row = [](int k) { return (k / TW + 1) * G::EW1 + k % TW + 1; };
+#pragma unroll
+    for (int i = 0; i < G::NCB3; ++i) {
+      const int cb = wave / G::RB + i * (4 / G::RB);
+      if ((G::CB3 * G::RB) % 4 != 0 && cb >= G::CB3) break;
+#pragma unroll
+      for (int ks = 0; ks < G::KS3; ++ks)
+        aw2[i] = mma16<T>(tr_frag(Gs, HP, 32 * ks, 16 * rb, lane), tr_frag_sw<G::PC>(Dc, 32 * ks, 16 * cb, lane, int_row),
+                          aw2[i]);
+    }
+    if (chunk == 0) {
+      const int c = tid % C;
+      for (int pi = tid / C; pi < G::T; pi += RS2)
+        db2 += Num<T>::to_f(reinterpret_cast<const T*>(Dc)[sw_off<G::PC>(int_row(pi), c)]);
+    }
+    lds_barrier();
+    // ---- [D2] dW1[HC, C] += dh^T LN(x)
+#pragma unroll
+    for (int i = 0; i < G::NCB3; ++i) {
+      const int cb = wave / G::RB + i * (4 / G::RB);
+      if ((G::CB3 * G::RB) % 4 != 0 && cb >= G::CB3) break;
+#pragma unroll
+      for (int ks = 0; ks < G::KS3; ++ks)
+        aw1[i] = mma16<T>(tr_frag(DHs, HP, 32 * ks, 16 * rb, lane), tr_frag(Xs, G::XP, 32 * ks, 16 * cb, lane), aw1[i]);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  // ---- per-strip partials (plain stores; one fixed-order grouped sum over the strips follows)
+  const long S = strip;
+#pragma unroll
+  for (int i = 0; i < G::NCB3; ++i) {
+    const int cb = wave / G::RB + i * (4 / G::RB);
+    if ((G::CB3 * G::RB) % 4 != 0 && cb >= G::CB3) break;
+    const int c = 16 * cb + l15;
+    *reinterpret_cast<float4*>(a.part_w2 + S * C * R + (long)c * R + c0 + chl) =
+        make_float4(aw2[i][0], aw2[i][1], aw2[i][2], aw2[i][3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a.part_w1[S * R * C + (long)(c0 + chl + j) * C + c] = aw1[i][j];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) dwp[j][tap] = group_sum<16>(dwp[j][tap]);
+    dbp[j] = group_sum<16>(dbp[j]);
+  }
+  if (l15 == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) red[((wave * 4 + lq) * 4 + j) * 10 + tap] = dwp[j][tap];
+      red[((wave * 4 + lq) * 4 + j) * 10 + 9] = dbp[j];
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < HC * 10; i += 256) {
+    const int cl = i / 10, k = i % 10;  // channel within the chunk, tap (9 = bias)
+    const int r = cl / 16, lqq = (cl % 16) / 4, jj = cl % 4;
+    float s = 0.f;
+    for (int w = r; w < 4; w += G::RB) s += red[((w * 4 + lqq) * 4 + jj) * 10 + k];
+    a.part_pos[S * R * 10 + (long)(c0 + cl) * 10 + k] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = db1[j];
+  __syncthreads();
+  if (tid < HC) {
+    const int kq = tid / 8, j = tid % 8;
+    float s = 0.f;
+    for (int t2 = kq; t2 < 256; t2 += G::NQ) s += red[t2 * 8 + j];
+    a.part_b1[S * R + c0 + tid] = s;
+  }
+  if (chunk == 0) {
+    __syncthreads();
+    red[tid] = db2;
+    __syncthreads();
+    if (tid < C) {
+      float s = 0.f;
+      for (int t2 = tid; t2 < 256; t2 += C) s += red[t2];
+      a.part_b2[S * C + tid] = s;
+    }
+  }
+}
+
+// ============================================================================ host side
+template <int C> struct FfnCfg;  // tile shapes per channel count (forward; the backward tiles 8 x 8)
+template <> struct FfnCfg<32> {
+  static constexpr int FHC = 32, FTH = 8, FTW = 16, BHC = 32;
+};
+template <> struct FfnCfg<64> {
+  static constexpr int FHC = 32, FTH = 8, FTW = 16, BHC = 32;
+};
+template <> struct FfnCfg<128> {
+  static constexpr int FHC = 32, FTH = 4, FTW = 16, BHC = 32;
+};
+template <> struct FfnCfg<256> {
+  static constexpr int FHC = 32, FTH = 4, FTW = 16, BHC = 32;
+};
+
+bool ffn_shape_ok(int C, int R) {
+  return (C == 32 || C == 64) && R % 32 == 0 && R >= 32;
+}
+
+template <typename T, int C>
+int ffn_fwd_launch(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
+  using Cf = FfnCfg<C>;
+  using G = FwdGeom<C, Cf::FHC>;
+  auto kern = ffn_fwd_kernel<T, C, Cf::FHC>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    attr = true;
+  }
+  a.tiles_x = (int)cdiv(d->W, G::TW);
+  a.tiles_y = (int)cdiv(d->H, G::TH);
+  const long grid = (long)d->B * a.tiles_x * a.tiles_y;
+  DFM_LAUNCH(kern, dim3((unsigned)grid), dim3(256), G::LDS, s, a);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+struct BwdPlan {
+  int tiles_x, tiles_y, ntiles, nstrip, tps, nch;
+  size_t lds;
+};
+
+template <int C>
+BwdPlan ffn_bwd_plan(const DfmConvFFNDesc* d) {
+  using Cf = FfnCfg<C>;
+  BwdPlan p;
+  using G = BwdGeom<C, Cf::BHC>;
+  p.tiles_x = (int)cdiv(d->W, G::TW);
+  p.tiles_y = (int)cdiv(d->H, G::TH);
+  p.ntiles = d->B * p.tiles_x * p.tiles_y;
+  p.nch = d->hidden / Cf::BHC;
+  // strips: about 2 workgroups per CU over (strip, chunk), a multiple of 8 strips (one XCD each)
+  int ns = (512 + p.nch - 1) / p.nch;
+  ns = std::max(8, std::min((ns + 7) / 8 * 8, (p.ntiles + 7) / 8 * 8));
+  p.tps = (p.ntiles + ns - 1) / ns;
+  p.nstrip = (p.ntiles + p.tps - 1) / p.tps;
+  p.lds = G::LDS;
+  return p;
+}
+
+BwdPlan bwd_plan(const DfmConvFFNDesc* d) {
+  switch (d->C) {
+    case 32: return ffn_bwd_plan<32>(d);
+    case 64: return ffn_bwd_plan<64>(d);
+    case 128: return ffn_bwd_plan<128>(d);
+    default: return ffn_bwd_plan<256>(d);
+  }
+}
+
+template <typename T, int C>
+int ffn_bwd_launch(const BwdPlan& p, FfnBwdArgs a, hipStream_t s) {
+  using Cf = FfnCfg<C>;
+  auto kern = ffn_bwd_kernel<T, C, Cf::BHC>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
+    attr = true;
+  }
+  a.tiles_x = p.tiles_x;
+  a.tiles_y = p.tiles_y;
+  a.ntiles = p.ntiles;
+  a.nstrip = p.nstrip;
+  a.tiles_per_strip = p.tps;
+  const long grid = (long)(p.nstrip + 7) / 8 * 8 * p.nch;
+  DFM_LAUNCH(kern, dim3((unsigned)grid), dim3(256), p.lds, s, a);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+#define FFN_C_SWITCH(C, FN, ...)            \
+  [&]() -> int {                            \
+    switch (C) {                            \
+      case 32: return FN<T, 32>(__VA_ARGS__);  \
+      case 64: return FN<T, 64>(__VA_ARGS__);  \
+      case 128: return FN<T, 128>(__VA_ARGS__); \
+      default: return FN<T, 256>(__VA_ARGS__); \
+    }                                       \
+  }()
+
+struct BwdWs {
+  size_t df, dh, du, pw2, pw1, pb1, ppos, pb2, res, ln, gemm, total;
+};
+
+DfmGemmDesc du_desc(const DfmConvFFNDesc* d) {
+  // du[P, C] = dh[P, R] W1[R, C]   (nn.Linear fc1 input gradient: A k-contiguous, B row-contiguous)
+  DfmGemmDesc g{};
+  const long P = (long)d->B * d->H * d->W;
+  g.M = (int)P;
+  g.N = d->C;
+  g.K = d->hidden;
+  g.batch = 1;
+  g.a_kcontig = 1;
+  g.b_kcontig = 0;
+  g.lda = d->hidden;
+  g.ldb = d->C;
+  g.ldc = d->C;
+  g.alpha = 1.f;
+  g.beta = 0.f;
+  g.rows_per_scale = 1;
+  return g;
+}
+
+BwdWs bwd_ws(int dtype, const DfmConvFFNDesc* d) {
+  const size_t es = dtype == DFM_F32 ? 4 : 2;
+  const long P = (long)d->B * d->H * d->W;
+  const BwdPlan p = bwd_plan(d);
+  BwdWs w{};
+  auto al = [](size_t v) { return (v + 255) / 256 * 256; };
+  w.df = al(es * P * d->C);
+  w.dh = al(es * P * d->hidden);
+  w.du = al(es * P * d->C);
+  w.pw2 = al((size_t)p.nstrip * d->C * d->hidden * 4);
+  w.pw1 = w.pw2;
+  w.pb1 = al((size_t)p.nstrip * d->hidden * 4);
+  w.ppos = al((size_t)p.nstrip * d->hidden * 10 * 4);
+  w.pb2 = al((size_t)p.nstrip * d->C * 4);
+  w.res = al(dfm_residual_bwd_workspace(P, d->C));
+  w.ln = al(dfm_layernorm_bwd_workspace(P, d->C));
+  DfmGemmDesc g = du_desc(d);
+  w.gemm = al(dfm_gemm_workspace_size(&g));
+  w.total = w.df + w.dh + w.du + w.pw2 + w.pw1 + w.pb1 + w.ppos + w.pb2 + w.res + w.ln + w.gemm;
+  return w;
+}
+
+}  // namespace
+
+extern "C" int dfm_convffn_supported(int dtype, const DfmConvFFNDesc* d) {
+  return d && (dtype == DFM_BF16 || dtype == DFM_F16) && d->B > 0 && d->H > 0 && d->W > 0 &&
+         ffn_shape_ok(d->C, d->hidden);
+}
+
+extern "C" int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x, const float* ln_w,
+                               const float* ln_b, const void* w1, const float* b1, const float* wpos,
+                               const float* bpos, const void* w2, const float* b2, const float* ls,
+                               const float* rowscale, void* out, void* f, void* h, float* mean, float* rstd,
+                               dfm_stream_t stream) {
+  DFM_CHECK_ARG(dfm_convffn_supported(dtype, d), "dfm_convffn_fwd: unsupported dtype %d / shape (C %d, hidden %d)",
+                dtype, d ? d->C : -1, d ? d->hidden : -1);
+  DFM_CHECK_ARG(x && ln_w && ln_b && w1 && b1 && wpos && bpos && w2 && b2 && ls && out && f && h && mean && rstd,
+                "dfm_convffn_fwd: null argument");
+  FfnFwdArgs a{};
+  a.B = d->B; a.H = d->H; a.W = d->W; a.R = d->hidden;
+  a.eps = d->ln_eps;
+  a.rps = (long)d->H * d->W;
+  a.x = x; a.lnw = ln_w; a.lnb = ln_b; a.w1 = w1; a.b1 = b1; a.wpos = wpos; a.bpos = bpos;
+  a.w2 = w2; a.b2 = b2; a.ls = ls; a.rowscale = rowscale;
+  a.out = out; a.f = f; a.h = h; a.mean = mean; a.rstd = rstd;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFM_BF16) {
+    using T = bf16_t;
+    return FFN_C_SWITCH(d->C, ffn_fwd_launch, d, a, s);
+  }
+  using T = f16_t;
+  return FFN_C_SWITCH(d->C, ffn_fwd_launch, d, a, s);
+}
+
+extern "C" size_t dfm_convffn_bwd_workspace_size(int dtype, const DfmConvFFNDesc* d) {
+  if (!dfm_convffn_supported(dtype, d)) return 0;
+  return bwd_ws(dtype, d).total;
+}
+
+extern "C" int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const void* x, const void* h,
+                               const void* f, const float* mean, const float* rstd, const float* ln_w,
+                               const float* ln_b, const void* w1, const float* wpos, const float* bpos,
+                               const void* w2, const float* ls, const float* rowscale, void* dx, float* dln_w,
+                               float* dln_b, float* dw1, float* db1, float* dwpos, float* dbpos, float* dw2,
+                               float* db2, float* dls, void* workspace, size_t workspace_bytes, dfm_stream_t stream) {
+  DFM_CHECK_ARG(dfm_convffn_supported(dtype, d), "dfm_convffn_bwd: unsupported dtype %d / shape (C %d, hidden %d)",
+                dtype, d ? d->C : -1, d ? d->hidden : -1);
+  DFM_CHECK_ARG(dout && x && h && f && mean && rstd && ln_w && ln_b && w1 && wpos && bpos && w2 && ls && dx &&
+                    dln_w && dln_b && dw1 && db1 && dwpos && dbpos && dw2 && db2 && dls && workspace,
+                "dfm_convffn_bwd: null argument");
+  const BwdWs w = bwd_ws(dtype, d);
+  DFM_CHECK_ARG(workspace_bytes >= w.total, "dfm_convffn_bwd: workspace %zu < %zu bytes", workspace_bytes, w.total);
+  hipStream_t s = (hipStream_t)stream;
+  const long P = (long)d->B * d->H * d->W;
+  const int C = d->C, R = d->hidden;
+  char* ws = (char*)workspace;
+  void* df = ws; ws += w.df;
+  void* dh = ws; ws += w.dh;
+  void* du = ws; ws += w.du;
+  float* pw2 = (float*)ws; ws += w.pw2;
+  float* pw1 = (float*)ws; ws += w.pw1;
+  float* pb1 = (float*)ws; ws += w.pb1;
+  float* ppos = (float*)ws; ws += w.ppos;
+  float* pb2 = (float*)ws; ws += w.pb2;
+  void* wres = ws; ws += w.res;
+  void* wln = ws; ws += w.ln;
+  void* wgemm = ws;
+  DfmPartialSum sums[8];
+  int ns = 0;
+  // residual / layer-scale backward: df = dout * ls * rowscale, dls = sum dout * f * rowscale
+  int rc = dfm_residual_bwd(dtype, P, C, dout, C, f, C, ls, rowscale, (long)d->H * d->W, df, C, dls, wres, &sums[ns],
+                            stream);
+  if (rc != DFM_OK) return rc;
+  if (sums[ns].part) ++ns;
+  // hidden part
+  const BwdPlan p = bwd_plan(d);
+  FfnBwdArgs a{};
+  a.B = d->B; a.H = d->H; a.W = d->W; a.R = R;
+  a.x = x; a.mean = mean; a.rstd = rstd; a.lnw = ln_w; a.lnb = ln_b; a.h = h; a.df = df; a.w2 = w2;
+  a.wpos = wpos; a.bpos = bpos; a.dh = dh;
+  a.part_w2 = pw2; a.part_w1 = pw1; a.part_b1 = pb1; a.part_pos = ppos; a.part_b2 = pb2;
+  if (dtype == DFM_BF16) {
+    using T = bf16_t;
+    rc = FFN_C_SWITCH(C, ffn_bwd_launch, p, a, s);
+  } else {
+    using T = f16_t;
+    rc = FFN_C_SWITCH(C, ffn_bwd_launch, p, a, s);
+  }
+  if (rc != DFM_OK) return rc;
+  sums[ns++] = DfmPartialSum{pw2, dw2, nullptr, (long)C * R, 0, p.nstrip, 0, 0};
+  sums[ns++] = DfmPartialSum{pw1, dw1, nullptr, (long)R * C, 0, p.nstrip, 0, 0};
+  sums[ns++] = DfmPartialSum{pb1, db1, nullptr, (long)R, 0, p.nstrip, 0, 0};
+  sums[ns++] = DfmPartialSum{ppos, dwpos, dbpos, (long)R * 10, 10, p.nstrip, 2, 0};
+  sums[ns++] = DfmPartialSum{pb2, db2, nullptr, (long)C, 0, p.nstrip, 0, 0};
+  // fc1 input gradient du = dh W1, then the LayerNorm backward with the residual's dout
+  DfmGemmDesc g = du_desc(d);
+  g.workspace_bytes = (long)w.gemm;
+  rc = dfm_gemm(dtype, &g, dh, w1, du, wgemm, stream);
+  if (rc != DFM_OK) return rc;
+  rc = dfm_layernorm_bwd(dtype, P, C, x, C, du, C, ln_w, mean, rstd, dout, C, dx, C, 0, dln_w, dln_b, wln, &sums[ns],
+                         stream);
+  if (rc != DFM_OK) return rc;
+  if (sums[ns].part) ++ns;
+  return dfm_partial_sum_group(ns, sums, stream);
+}

@@ -176,6 +176,11 @@ def _cat1(*vs):
 
 
 # ====================================================================== ConvFFN (+ residual)
+# bf16 / fp16 ConvFFNs whose shape has fused kernels run dfm_convffn_fwd / _bwd (csrc/convffn.hip);
+# False routes every ConvFFN through the op-level chain below (tests compare the two)
+FUSED_FFN = False
+
+
 class ConvFFNFn(torch.autograd.Function):
     """out = x + rowscale * ls * fc2(GELU(DW3x3(h) + h)),  h = fc1(LN(x))   on [P, C] rows.
 
@@ -192,6 +197,12 @@ class ConvFFNFn(torch.autograd.Function):
         dt = x.dtype
         W1, W2 = wcast(dt, w1), wcast(dt, w2)
         ctx.tag = K.TAG
+        ctx.fused = FUSED_FFN and K.convffn_supported(dt, shape, C, w1.shape[0])
+        if ctx.fused:  # one kernel: LN, fc1, DW3x3 + identity, GELU, fc2, residual; h is the saved hidden
+            out, f, h, mu, rs = K.convffn_fwd(x, shape, ln_w, ln_b, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
+            ctx.shape = shape
+            ctx.save_for_backward(x, h, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls)
+            return out
         xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
         ctx.shape = shape
         h = K.linear(xn, W1, b1)
@@ -207,6 +218,19 @@ class ConvFFNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         K.TAG = ctx.tag + ".bwd"
+        if ctx.fused:
+            x, h, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
+            dt = x.dtype
+            slots = [gslot(ln_w), gslot(ln_b), gslot2(w1), gslot(b1), gslot(wpos), gslot(bpos), gslot2(w2), gslot(b2),
+                     gslot(ls)]
+            slots = [None if t is None else t.view(sh) for t, sh in
+                     zip(slots, [(-1,), (-1,), tuple(w1.shape), (-1,), (w1.shape[0], 9), (-1,), tuple(w2.shape), (-1,),
+                                 (-1,)])]
+            dx, dlnw, dlnb, dW1, db1, dwpos, dbpos, dW2, db2, dls = K.convffn_bwd(
+                dout.contiguous(), x, h, f, mu, rs, ctx.shape, ln_w, ln_b, wcast(dt, w1), wpos, bpos, wcast(dt, w2), ls,
+                rowscale, grads=slots)
+            return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
+                    dls)
         with wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
             x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
             B, H, W = ctx.shape

@@ -317,6 +317,82 @@ def residual_bwd(dout, f, colscale, rowscale=None, rows_per_scale=1, df=None):
     return df, dls
 
 
+# ----------------------------------------------------------------------------- fused ConvFFN (K4)
+def _acct_named(parts, peak="bf16"):
+    """Account one entry point that launched several kernels: parts = [(name substring, flops, bytes)];
+    each launched kernel is charged the first unused part whose substring its name contains."""
+    n = lib.dfm_trace_take(_FUNCS, 64)
+    used = [False] * len(parts)
+    for i in range(min(n, 64)):
+        f = _FUNCS[i]
+        nm = kernel_name(f)
+        fl = by = 0.0
+        for j, (sub, pf, pb) in enumerate(parts):
+            if not used[j] and sub in nm:
+                used[j], fl, by = True, pf, pb
+                break
+        ACCOUNT.append(((f,), float(fl), float(by), peak, TAG))
+
+
+def _ffn_desc(shape, C, hidden, eps):
+    B, H, W = shape
+    return _lib.ConvFFNDesc(B, H, W, C, hidden, eps)
+
+
+def convffn_supported(dtype, shape, C, hidden):
+    if dtype not in (torch.bfloat16, torch.float16):
+        return False
+    d = _ffn_desc(shape, C, hidden, 1e-6)
+    code = _lib.BF16 if dtype == torch.bfloat16 else _lib.F16
+    return bool(lib.dfm_convffn_supported(code, ctypes.byref(d)))
+
+
+def convffn_fwd(x, shape, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, eps=1e-6):
+    """Fused ConvFFN + Block residual (DFormer.py:48-67, 176-179). Returns (out, f, h, mean, rstd):
+    out = x + rowscale * ls * f, f = fc2 pre-residual output, h = fc1 output, LN statistics."""
+    P, C = x.shape
+    R = w1.shape[0]
+    d = _ffn_desc(shape, C, R, eps)
+    out, f = torch.empty_like(x), torch.empty_like(x)
+    h = torch.empty(P, R, device=x.device, dtype=x.dtype)
+    mean = torch.empty(P, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(P, device=x.device, dtype=torch.float32)
+    check(lib.dfm_convffn_fwd(dtype_code(x), ctypes.byref(d), ptr(x), ptr(ln_w), ptr(ln_b), ptr(w1), ptr(b1),
+                              ptr(wpos), ptr(bpos), ptr(w2), ptr(b2), ptr(ls), ptr(rowscale), ptr(out), ptr(f),
+                              ptr(h), ptr(mean), ptr(rstd), stream()), "dfm_convffn_fwd")
+    if ACCOUNT is not None:
+        es = _es(x)
+        _acct(4.0 * P * C * R + 18.0 * P * R, es * P * (3 * C + R) + 8 * P + es * 2 * C * R)
+    return out, f, h, mean, rstd
+
+
+def convffn_bwd(dout, x, h, f, mean, rstd, shape, ln_w, ln_b, w1, wpos, bpos, w2, ls, rowscale=None, eps=1e-6,
+                grads=None):
+    """Backward of convffn_fwd. Returns (dx, dln_w, dln_b, dw1, db1, dwpos, dbpos, dw2, db2, dls); the
+    parameter gradients go to the tensors of `grads` (same order, None = allocate; float32, overwritten)."""
+    P, C = x.shape
+    R = w1.shape[0]
+    d = _ffn_desc(shape, C, R, eps)
+    code = dtype_code(x)
+    dev = x.device
+    shapes = [(C,), (C,), (R, C), (R,), (R, 9), (R,), (C, R), (C,), (C,)]
+    grads = list(grads) if grads is not None else [None] * 9
+    outs = [g if g is not None else torch.empty(sh, device=dev, dtype=torch.float32) for g, sh in zip(grads, shapes)]
+    dx = torch.empty_like(x)
+    nbytes = lib.dfm_convffn_bwd_workspace_size(code, ctypes.byref(d))
+    ws = _ws(nbytes, dev)
+    check(lib.dfm_convffn_bwd(code, ctypes.byref(d), ptr(dout), ptr(x), ptr(h), ptr(f), ptr(mean), ptr(rstd),
+                              ptr(ln_w), ptr(ln_b), ptr(w1), ptr(wpos), ptr(bpos), ptr(w2), ptr(ls), ptr(rowscale),
+                              ptr(dx), *[ptr(o) for o in outs], ptr(ws), nbytes, stream()), "dfm_convffn_bwd")
+    if ACCOUNT is not None:
+        es = _es(x)
+        _acct_named([("residual", 0.0, 3.0 * es * P * C),
+                     ("ffn_bwd", 6.0 * P * C * R + 36.0 * P * R, es * P * (2 * R + 2 * C) + 8 * P),
+                     ("gemm", 2.0 * P * C * R, es * (P * R + P * C + R * C)),
+                     ("ln_bwd", 0.0, es * P * C * 4 + 8 * P)])
+    return (dx, *outs)
+
+
 # ---------------------------------------------------------------------------- depthwise conv
 def dwconv(x, shape, w, bias, k, add_identity=False, out=None, gelu_out=None, out_gelu_grad=False):
     """x: [B*H*W, C] view (NHWC rows); w float32 [C,1,k,k] or [C,k,k]. gelu_out: also GELU(y);

@@ -39,8 +39,9 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 8 (round 4: DfmGemmDesc.workspace_bytes + stride / leading-dimension validation;
-                              deferred reduction second stages, dfm_partial_sum_group) */
+int dfm_abi_version(void); /* 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
+                              second stages (dfm_partial_sum_group); 7: DfmGemmDesc.workspace_bytes + stride /
+                              leading-dimension validation */
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -185,6 +186,36 @@ int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const vo
 int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const void* dy,
                    long lddy, const float* w, int add_identity, void* dx, long lddx, int accumulate, float* dw,
                    float* db, void* workspace, DfmPartialSum* defer, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- fused ConvFFN (K4)
+ * DFormer.py:48-67 (MLP: LN -> fc1 -> DW3x3 + identity -> GELU -> fc2) inside Block's residual
+ * (DFormer.py:176-179):  out = x + rowscale[p / (H*W)] * ls * f,
+ *   f = fc2(GELU(DW3x3(h) + bpos + h)) + b2,  h = fc1(LN(x)) + b1.
+ * x, out, f, dx, dout: [B*H*W][C] contiguous NHWC rows (dtype); h: [B*H*W][hidden] (dtype), written
+ * by the forward for the backward (the only hidden-sized tensor either pass moves through HBM);
+ * w1 [hidden][C], w2 [C][hidden] (dtype); ln_w, ln_b, b1, bpos, b2, ls: float32; wpos [hidden][9]
+ * float32; rowscale float32 [B] (DropPath keep mask / keep probability) or NULL; mean / rstd float32
+ * [B*H*W] (the LayerNorm statistics, written by the forward). dtype bf16 or f16 (float32 runs the
+ * unfused entry points); dfm_convffn_supported says whether (C, hidden) has fused kernels.
+ * The backward writes dx (LayerNorm backward + the residual's dout) and every parameter gradient
+ * (float32, overwritten: dw1 [hidden][C], dw2 [C][hidden], dwpos [hidden][9], dls = layer-scale),
+ * reducing them in a fixed order (bit-reproducible); workspace from dfm_convffn_bwd_workspace_size. */
+typedef struct DfmConvFFNDesc {
+  int B, H, W, C, hidden;
+  float ln_eps;
+} DfmConvFFNDesc;
+int dfm_convffn_supported(int dtype, const DfmConvFFNDesc* d);
+int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x, const float* ln_w, const float* ln_b,
+                    const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
+                    const float* b2, const float* ls, const float* rowscale, void* out, void* f, void* h,
+                    float* mean, float* rstd, dfm_stream_t stream);
+size_t dfm_convffn_bwd_workspace_size(int dtype, const DfmConvFFNDesc* d);
+int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const void* x, const void* h,
+                    const void* f, const float* mean, const float* rstd, const float* ln_w, const float* ln_b,
+                    const void* w1, const float* wpos, const float* bpos, const void* w2, const float* ls,
+                    const float* rowscale, void* dx, float* dln_w, float* dln_b, float* dw1, float* db1,
+                    float* dwpos, float* dbpos, float* dw2, float* db2, float* dls, void* workspace,
+                    size_t workspace_bytes, dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)

@@ -83,6 +83,15 @@ def bench_stage(st, branch="mlp"):
         ("wgrad fc2+fc1", lambda: _wg(df, g, dh, xn), P * (C + hid + hid + C) * E),
         ("ln_bwd", lambda: K.layernorm_bwd(x, xn, lnw, mu, rstd, dres=dout), P * C * E * 4),
     ]
+    if K.convffn_supported(bf, (B, H, W), C, hid):  # the fused ConvFFN entry points on the same operands
+        fo = K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs)
+        rows += [
+            ("FUSED fwd", lambda: K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs),
+             P * (3 * C + hid) * E),
+            ("FUSED bwd", lambda: K.convffn_bwd(dout, x, fo[2], fo[1], fo[3], fo[4], (B, H, W), lnw, lnb, w1, wpos,
+                                                bpos, w2, ls, rs),
+             P * (3 * C + 2 * C + 3 * hid + 5 * C) * E),
+        ]
     res = []
     for name, fn, nb in rows:
         us = timed(fn)
@@ -107,6 +116,15 @@ def main():
     for st in stages:
         for br in ("mlp", "mlp_e2"):
             allr += bench_stage(st, br)
+    for st in stages:
+        for br in ("mlp", "mlp_e2"):
+            rr = [r for r in allr if r["stage"] == st and r["branch"] == br]
+            unf = [r["us"] for r in rr if not r["kernel"].startswith("FUSED")]
+            fus = {r["kernel"]: r["us"] for r in rr if r["kernel"].startswith("FUSED")}
+            if fus:
+                print(f"s{st}.{br:6s} unfused fwd {sum(unf[:4]):7.1f} us bwd {sum(unf[4:]):7.1f} us | fused fwd "
+                      f"{fus['FUSED fwd']:7.1f} us bwd {fus['FUSED bwd']:7.1f} us")
+    allr = [r for r in allr if not r["kernel"].startswith("FUSED")]
     tot = sum(r["us"] for r in allr)
     ideal = sum(r["bytes"] for r in allr) / HBM * 1e6
     print(f"total {tot:.1f} us, HBM ideal at 6.3 TB/s {ideal:.1f} us ({ideal / tot:.2f})")
