@@ -45,6 +45,32 @@ class ConvFFNDesc(ctypes.Structure):
     _fields_ = [("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("hidden", c_int), ("ln_eps", c_float)]
 
 
+class BlockDesc(ctypes.Structure):
+    """DfmBlockDesc: one encoder Block (dfm_block_fwd / dfm_block_bwd)."""
+    _fields_ = [("B", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("heads", c_int), ("window", c_int),
+                ("hidden", c_int), ("drop_depth", c_int), ("fused_ffn", c_int), ("ln_eps", c_float)]
+
+
+# the DFM_BP_* indices of dfm_block_fwd's parameter array: the reference Block's state_dict keys
+# (DFormer.py:70-181) in the header's enum order
+BLOCK_PARAM_NAMES = (
+    "attn.norm.weight", "attn.norm.bias", "attn.norm_e.weight", "attn.norm_e.bias",
+    "attn.q.weight", "attn.q.bias", "attn.q_cut.weight", "attn.q_cut.bias", "attn.l.weight", "attn.l.bias",
+    "attn.conv.weight", "attn.conv.bias", "attn.a.weight", "attn.a.bias", "attn.e_fore.weight", "attn.e_fore.bias",
+    "attn.e_conv.weight", "attn.e_conv.bias", "attn.e_back.weight", "attn.e_back.bias", "attn.kv.weight",
+    "attn.kv.bias", "attn.short_cut_linear.weight", "attn.short_cut_linear.bias", "attn.proj.weight",
+    "attn.proj.bias", "attn.proj_e.weight", "attn.proj_e.bias",
+    "layer_scale_1", "layer_scale_1_e", "layer_scale_2", "layer_scale_2_e",
+    "mlp.norm.weight", "mlp.norm.bias", "mlp.fc1.weight", "mlp.fc1.bias", "mlp.pos.weight", "mlp.pos.bias",
+    "mlp.fc2.weight", "mlp.fc2.bias",
+    "mlp_e2.norm.weight", "mlp_e2.norm.bias", "mlp_e2.fc1.weight", "mlp_e2.fc1.bias", "mlp_e2.pos.weight",
+    "mlp_e2.pos.bias", "mlp_e2.fc2.weight", "mlp_e2.fc2.bias")
+# entries passed in the activation dtype (nn.Linear weights); every other entry is float32
+BLOCK_GEMM_WEIGHTS = frozenset(n for n in BLOCK_PARAM_NAMES if n.endswith(".weight") and any(
+    k in n for k in (".q.", ".q_cut.", ".l.", ".a.", ".e_fore.", ".e_back.", ".kv.", ".short_cut_linear.", ".proj.",
+                     ".proj_e.", ".fc1.", ".fc2.")))
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dfm_last_error": (ctypes.c_char_p, []),
@@ -70,9 +96,14 @@ _SIGS = {
                                c_int, P, P, P, P, P]),
     "dfm_partial_sum_group": (c_int, [c_int, P, P]),
     "dfm_convffn_supported": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)]),
-    "dfm_convffn_fwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 17),
+    "dfm_convffn_fwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 18),
     "dfm_convffn_bwd_workspace_size": (c_size_t, [c_int, ctypes.POINTER(ConvFFNDesc)]),
-    "dfm_convffn_bwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 25 + [c_size_t, P]),
+    "dfm_convffn_bwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 26 + [c_size_t, P]),
+    "dfm_block_saved_size": (c_size_t, [c_int, ctypes.POINTER(BlockDesc)]),
+    "dfm_block_workspace_size": (c_size_t, [c_int, ctypes.POINTER(BlockDesc)]),
+    "dfm_block_fwd": (c_int, [c_int, ctypes.POINTER(BlockDesc), P, P, P, P, P, P, P, c_size_t, P, c_size_t, P]),
+    "dfm_block_bwd": (c_int, [c_int, ctypes.POINTER(BlockDesc), P, P, P, P, P, c_size_t, P, P, P, P, P, P, c_size_t,
+                              P]),
     "dfm_group_scale": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, c_long, P]),
     "dfm_nmf_update_mm": (c_int, [c_int, c_long, c_int, P, P, P, c_float, P, P, P, c_int, P]),
     "dfm_nmf_update_bwd_mm": (c_int, [c_int, c_long, c_int, P, P, P, P, P, P, P, c_float, P, P, c_int, P, P, P,

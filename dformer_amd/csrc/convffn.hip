@@ -92,19 +92,22 @@ struct FfnFwdArgs {
   const float* rowscale;  // [B] or NULL
   void* out;
   void* f;
-  void* h;  // [P][R] saved for the backward
+  void* h;   // [P][R] saved for the backward
+  void* xn;  // [P][C] LN(x), or NULL
   float* mean;
   float* rstd;
 };
 
-// Forward geometry: 8 x 8 pixel tiles; each of the 4 waves owns every 4th hidden chunk of HC channels
+// Forward geometry: TH x TW pixel tiles with T * C = 4096 (a wave's partial out^T is 64 fp32 registers
+// per lane: 8 x 16 tiles at C = 32, 8 x 8 at 64, 4 x 8 at 128, 4 x 4 at 256); each of the 4 waves owns
+// every 4th hidden chunk of HC channels
 // and keeps its own partial out^T[C, T] in registers, so the chunk loop has no workgroup barrier:
 // a wave computes h for its chunk (tile + 1 halo, MFMA) into its private LDS buffer and reads it back
 // for the depthwise conv (wave-local LDS hand-off). The four partials are summed in a fixed order at
 // the end (deterministic).
-template <int C, int HC>
+template <int C, int HC, int TH_, int TW_>
 struct FwdGeom {
-  static constexpr int TH = 8, TW = 8, T = TH * TW;
+  static constexpr int TH = TH_, TW = TW_, T = TH * TW;
   static constexpr int EW = TW + 2, T1 = (TH + 2) * EW, T1P = (T1 + 15) / 16 * 16;
   static constexpr int XP = C + 8, HP = HC + 8;  // LDS pitches (elements): 16-byte rows, staggered banks
   static constexpr int RB1 = HC / 16, CB1 = T1P / 16, KS1 = C / 32;
@@ -116,9 +119,9 @@ struct FwdGeom {
   static_assert(T % 16 == 0 && HC % 32 == 0 && C % 32 == 0, "tile geometry");
 };
 
-template <typename T, int C, int HC>
+template <typename T, int C, int HC, int TH_, int TW_>
 __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
-  using G = FwdGeom<C, HC>;
+  using G = FwdGeom<C, HC, TH_, TW_>;
   constexpr int TH = G::TH, TW = G::TW;
   extern __shared__ __align__(16) unsigned char smem[];
   T* Xs = reinterpret_cast<T*>(smem);  // [T1P][XP] LN(x) of tile + halo
@@ -200,10 +203,18 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
           for (int j = 0; j < 8; ++j) o[j] = in ? (v[nv][j] - mu) * rs * gw[j] + bw[j] : 0.f;
           st8<T>(Xs + e * G::XP + 8 * (gl + nv * GL), o);
         }
-        if (in && gl == 0 && ey >= 1 && ey <= TH && ex >= 1 && ex <= TW) {
+        if (in && ey >= 1 && ey <= TH && ex >= 1 && ex <= TW) {
           const long p = ((long)b * H + yy) * W + xx;
-          a.mean[p] = mu;
-          a.rstd[p] = rs;
+          if (gl == 0) {
+            a.mean[p] = mu;
+            a.rstd[p] = rs;
+          }
+          if (a.xn) {
+#pragma unroll
+            for (int nv = 0; nv < NV; ++nv)
+              *reinterpret_cast<uint4*>(static_cast<T*>(a.xn) + p * C + 8 * (gl + nv * GL)) =
+                  *reinterpret_cast<const uint4*>(Xs + e * G::XP + 8 * (gl + nv * GL));
+          }
         }
       }
     }
@@ -217,19 +228,58 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
     for (int r = 0; r < G::RB2; ++r) acc[i][r] = float4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nch = R / HC;
+  // the next chunk's taps (+ W1 fragments when they are few) are loaded into registers under this
+  // chunk's depthwise / GELU phase; the chunk's W2 fragments under its fc1 phase
+  constexpr int NTP = (G::PS + 63) / 64;
+  constexpr bool PREW1 = G::RB1 * G::KS1 <= 4;
+  float tp[NTP];
+  bf16x8_t wpf[PREW1 ? G::RB1 : 1][PREW1 ? G::KS1 : 1];
+  auto load_taps = [&](int c0) {  // unconditional loads (clamped index): no branch for the wait to settle in
+#pragma unroll
+    for (int k = 0; k < NTP; ++k) {
+      const int i = min(lane + 64 * k, G::PS - 1);
+      const int tap = i / HC, j = i % HC;
+      const float wv = a.wpos[(long)(c0 + j) * 9 + min(tap, 8)];
+      const float bv = a.bpos[c0 + j];
+      tp[k] = tap < 9 ? wv + (tap == 4 ? 1.f : 0.f) : bv;
+    }
+  };
+  auto load_w1 = [&](int c0) {
+    if constexpr (PREW1) {
+#pragma unroll
+      for (int rb = 0; rb < G::RB1; ++rb)
+#pragma unroll
+        for (int ks = 0; ks < G::KS1; ++ks) wpf[rb][ks] = ldfrag(w1 + (long)(c0 + 16 * rb + l15) * C + 32 * ks + 8 * lq);
+    }
+  };
+  // W2c fragments of the chunk: loaded one chunk ahead, under the previous chunk's GELU phase (when
+  // the double set fits in registers: C <= 128), else at the chunk's start
+  constexpr bool PREW2 = G::RB2 * G::KS2 <= 8;
+  bf16x8_t wb[G::RB2][G::KS2], wbn[PREW2 ? G::RB2 : 1][PREW2 ? G::KS2 : 1];
+  auto load_w2 = [&](int c0, auto& dst) {
+#pragma unroll
+    for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+      for (int ks = 0; ks < G::KS2; ++ks) dst[r][ks] = ldfrag(w2 + (long)(16 * r + l15) * R + c0 + 32 * ks + 8 * lq);
+  };
+  if (wave < nch) {
+    load_taps(wave * HC);
+    load_w1(wave * HC);
+    if constexpr (PREW2) load_w2(wave * HC, wb);
+  }
   for (int ch = wave; ch < nch; ch += 4) {
     const int c0 = ch * HC;
-    // taps (identity folded into the centre) + bias of the chunk -> this wave's Pw
-    for (int i = lane; i < G::PS; i += 64) {
-      const int tap = i / HC, j = i % HC;
-      Pw[i] = tap < 9 ? a.wpos[(long)(c0 + j) * 9 + tap] + (tap == 4 ? 1.f : 0.f) : a.bpos[c0 + j];
-    }
+    if constexpr (!PREW2) load_w2(c0, wb);
+#pragma unroll
+    for (int k = 0; k < NTP; ++k)
+      if (G::PS % 64 == 0 || lane + 64 * k < G::PS) Pw[lane + 64 * k] = tp[k];
     // [A] h^T[HC, T1P] = W1c[HC, C] xn^T  (+ b1; zero outside the image) -> Hw[pixel][channel]
 #pragma unroll
     for (int rb = 0; rb < G::RB1; ++rb) {
       bf16x8_t wa[G::KS1];
 #pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks) wa[ks] = ldfrag(w1 + (long)(c0 + 16 * rb + l15) * C + 32 * ks + 8 * lq);
+      for (int ks = 0; ks < G::KS1; ++ks)
+        wa[ks] = PREW1 ? wpf[PREW1 ? rb : 0][PREW1 ? ks : 0] : ldfrag(w1 + (long)(c0 + 16 * rb + l15) * C + 32 * ks + 8 * lq);
       const float4 bias = *reinterpret_cast<const float4*>(a.b1 + c0 + 16 * rb + 4 * lq);
 #pragma unroll
       for (int cb = 0; cb < G::CB1; ++cb) {
@@ -248,18 +298,29 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
     // wave-local hand-off: this wave's own LDS writes are complete once lgkmcnt drains
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    // [B] g = GELU(DW3x3(h) + bpos + h) for (1 pixel, 8 channels) per lane = its B fragment of
-    //     out^T[C, T] += W2c[C, HC] g^T
-    bf16x8_t wb[G::RB2][G::KS2];
-#pragma unroll
-    for (int r = 0; r < G::RB2; ++r)
-#pragma unroll
-      for (int ks = 0; ks < G::KS2; ++ks) wb[r][ks] = ldfrag(w2 + (long)(16 * r + l15) * R + c0 + 32 * ks + 8 * lq);
+    if (ch + 4 < nch) {
+      load_taps(c0 + 4 * HC);
+      load_w1(c0 + 4 * HC);
+      if constexpr (PREW2) load_w2(c0 + 4 * HC, wbn);
+    }
+    // the tile's h (the centre tap) is saved first: the stores then complete under the GELU phase
+    // instead of being waited on by the next chunk's first load-use (one counter covers both)
 #pragma unroll
     for (int cb = 0; cb < G::CB2; ++cb) {
       const int p = 16 * cb + l15, py = p / TW, px = p % TW;
       const int yy = y0 + py, xx = x0 + px;
-      const bool in = yy < H && xx < W;
+#pragma unroll
+      for (int ks = 0; ks < G::KS2; ++ks) {
+        const int cc = 32 * ks + 8 * lq;
+        const uint4 u = *reinterpret_cast<const uint4*>(Hw + ((py + 1) * G::EW + px + 1) * G::HP + cc);
+        if (yy < H && xx < W) *reinterpret_cast<uint4*>(hsave + (((long)b * H + yy) * W + xx) * R + c0 + cc) = u;
+      }
+    }
+    // [B] g = GELU(DW3x3(h) + bpos + h) for (1 pixel, 8 channels) per lane = its B fragment of
+    //     out^T[C, T] += W2c[C, HC] g^T
+#pragma unroll
+    for (int cb = 0; cb < G::CB2; ++cb) {
+      const int p = 16 * cb + l15, py = p / TW, px = p % TW;
 #pragma unroll
       for (int ks = 0; ks < G::KS2; ++ks) {
         const int cc = 32 * ks + 8 * lq;
@@ -274,7 +335,6 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const uint4 u = *reinterpret_cast<const uint4*>(hb + ((tap / 3) * G::EW + tap % 3) * G::HP);
-          if (tap == 4 && in) *reinterpret_cast<uint4*>(hsave + (((long)b * H + yy) * W + xx) * R + c0 + cc) = u;
           float hv[8];
           unpack8w<T>(u, hv);
           const float4 q0 = *reinterpret_cast<const float4*>(Pw + tap * HC + cc);
@@ -294,6 +354,14 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
     }
     // the next chunk's phase A rewrites Hw / Pw: this wave's reads of them must have completed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (PREW2) {
+      if (ch + 4 < nch) {
+#pragma unroll
+        for (int r = 0; r < G::RB2; ++r)
+#pragma unroll
+          for (int ks = 0; ks < G::KS2; ++ks) wb[r][ks] = wbn[r < G::RB2 ? r : 0][ks];
+      }
+    }
   }
 
   // ---- fixed-order sum of the 4 partials: (w0 + w2) + (w1 + w3) in LDS (the body buffers are dead)
@@ -363,11 +431,6 @@ struct FfnBwdArgs {
   int B, H, W, R;
   int tiles_x, tiles_y, ntiles;
   int nstrip, tiles_per_strip;
-  const void* x;
-  const float* mean;
-  const float* rstd;
-  const float* lnw;
-  const float* lnb;
   const void* h;   // [P][R] saved by the forward
   const void* df;  // [P][C] gradient of f (dout * rowscale * ls)
   const void* w2;  // [C][R]
@@ -375,39 +438,9 @@ struct FfnBwdArgs {
   const float* bpos;
   void* dh;          // [P][R]
   float* part_w2;    // [nstrip][C * R]   dW2[c][r]
-  float* part_w1;    // [nstrip][R * C]   dW1[r][c]
-  float* part_b1;    // [nstrip][R]
-  float* part_pos;   // [nstrip][R * 10] dwpos (9 taps) | dbpos
   float* part_b2;    // [nstrip][C]
 };
 
-
-// Backward geometry: 8 x 8 pixel tiles. The h chunk (tile + 2 halo) and df (tile + 1 halo) of the
-// NEXT tile are DMA'd (global_load_lds, no registers) into the idle half of double-buffered LDS
-// images while this tile is computed; x of this tile is loaded to registers at its start and
-// normalised into LDS late in the tile. The h image has padded 80-byte rows (a DMA writes lane-
-// linearly: every fifth 16-byte slot of a row is a pad slot the DMA fills from a zero page), so
-// the 9 tap reads of a pixel are one base address plus constant offsets; the df image has unpadded
-// 16-byte pieces XOR-swizzled by row (swz) for conflict-free reads.
-template <int C, int HC>
-struct BwdGeom {
-  static constexpr int TH = 8, TW = 8, T = TH * TW;
-  static constexpr int EW1 = TW + 2, T1 = (TH + 2) * EW1, T1P = (T1 + 15) / 16 * 16;
-  static constexpr int EW2 = TW + 4, T2 = (TH + 4) * EW2;
-  static constexpr int RB = HC / 16, CB1 = T1P / 16, KS1 = C / 32;
-  static constexpr int NCB1 = (CB1 * RB + 3) / 4;  // phase-A/B column blocks per wave
-  static constexpr int CB3 = C / 16, KS3 = T / 32;
-  static constexpr int NCB3 = (CB3 * RB + 3) / 4;  // phase-D column blocks per wave
-  static constexpr int NQ = HC / 8, ITEMS = T * NQ, NI = (ITEMS + 255) / 256;  // phase-C items
-  static constexpr int HP = HC + 8, XP = C + 8;   // padded pitches (elements)
-  static constexpr int HSL = HP / 8, PC = C / 8;  // 16-byte slots per h row, pieces per df / x row
-  static constexpr int NSH = T2 * HSL, NSD = T1P * PC;  // DMA slots per tile
-  static constexpr int NXV = (T * PC + 255) / 256;      // x vectors per thread
-  static constexpr int HS = T2 * HP, DS = T1P * C, XS = T * XP, DH = T1P * HP, GS = T * HP;  // elements
-  static constexpr size_t LDS = (size_t)(2 * HS + 2 * DS + XS + DH + 2 * GS) * 2 + (size_t)(10 * HC + 2 * C) * 4;
-  static_assert(HC % 32 == 0 && C % 32 == 0 && 4 % RB == 0 && 256 % NQ == 0 && 256 % PC == 0, "geometry");
-  static_assert((size_t)HS * 2 * 2 >= (size_t)256 * 8 * 4, "end-of-strip reduction space");
-};
 
 // 16-byte piece p of image row r sits at position p ^ swz(r) of that row
 template <int NPR> DFM_INLINE int swz(int r) {
@@ -432,22 +465,44 @@ DFM_INLINE bf16x8_t tr_frag_sw(const bf16_t* img, int k0, int n0, int lane, RowF
   return __builtin_bit_cast(bf16x8_t, s);
 }
 
-__device__ __attribute__((aligned(16))) const unsigned int g_ffn_zero[4] = {0u, 0u, 0u, 0u};
+// ============================================================================ backward, dhpre pass
+// ffn_dhpre_kernel: one workgroup per (strip of tiles, hidden chunk); per tile (8 x 8; 4 x 8 at C = 256):
+//   [A] dg^T = W2c^T df^T on the tile (MFMA; W2c^T in registers for the strip)
+//   [B] hpre = DW3x3(h) + bpos + h from h on tile + 1 halo (LDS), GELU / GELU' from one erf,
+//       dhpre = dg GELU'(hpre) -> HBM (16-bit, as the op-level chain stores it); g -> LDS
+//   [D] dW2^T += g^T df (MFMA, K = pixels, ds_read_b64_tr_b16), accumulated over the strip
+// h and df of the NEXT tile are DMA'd into double-buffered LDS images while this tile is computed.
+// The depthwise input / weight gradients (dfm_dwconv_bwd) and the fc1 GEMMs follow in
+// dfm_convffn_bwd. No halo pixel's GELU is recomputed.
+template <int C, int HC, int TH_, int TW_>
+struct DhGeom {
+  static constexpr int TH = TH_, TW = TW_, T = TH * TW;
+  static constexpr int EW1 = TW + 2, T1 = (TH + 2) * EW1;
+  static constexpr int RB = HC / 16, CBT = T / 16, KS1 = C / 32;
+  static constexpr int NPAIR = (CBT * RB + 3) / 4;  // (row block, column block) pairs per wave in [A] / [B]
+  static constexpr int CB3 = C / 16, KS3 = T / 32;
+  static constexpr int NCB3 = (CB3 * RB + 3) / 4;
+  static constexpr int HP = HC + 8, HSL = HP / 8, PC = C / 8;
+  static constexpr int NSH = T1 * HSL, NSD = T * PC;  // DMA slots per tile
+  static constexpr int HS = T1 * HP, DS = T * C, GS = T * HP;  // elements
+  static constexpr size_t LDS = (size_t)(2 * HS + 2 * DS + GS) * 2 + (size_t)(10 * HC) * 4;
+  static_assert(HC % 32 == 0 && C % 32 == 0 && 4 % RB == 0 && (CBT * RB) % 4 == 0, "geometry");
+};
 
-template <typename T, int C, int HC>
-__global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
-  using G = BwdGeom<C, HC>;
+// zero page for LDS-DMA slots outside the image: 64 x 16 bytes indexed by lane, so the requests spread
+// over L2 channels instead of all hitting one line
+__device__ __attribute__((aligned(16))) const unsigned int g_ffn_zero16[256] = {};
+
+template <typename T, int C, int HC, int TH_, int TW_>
+__global__ __launch_bounds__(256, 2) void ffn_dhpre_kernel(FfnBwdArgs a) {
+  using G = DhGeom<C, HC, TH_, TW_>;
   constexpr int TH = G::TH, TW = G::TW, HP = G::HP;
   extern __shared__ __align__(16) unsigned char smem[];
-  bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);  // 2 x [T2][HP]  h chunk, tile + 2 halo (padded)
-  bf16_t* Ds = Hs + 2 * G::HS;                     // 2 x [T1P][C]  df, tile + 1 halo (swizzled)
-  bf16_t* Xs = Ds + 2 * G::DS;                     // [T][XP]      LN(x) of the tile
-  bf16_t* Dh = Xs + G::XS;                         // [T1P][HP]    dhpre, tile + 1 halo
-  bf16_t* Gs = Dh + G::DH;                         // [T][HP]      g of the tile
-  bf16_t* DHs = Gs + G::GS;                        // [T][HP]      dh of the tile
-  float* Ps = reinterpret_cast<float*>(DHs + G::GS);  // [10][HC] taps (identity in the centre) + bias
-  float* Lw = Ps + 10 * HC;                           // LayerNorm weight | bias
-  float* red = reinterpret_cast<float*>(smem);        // end of strip only (Hs region)
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);  // 2 x [T1][HP]  h chunk, tile + 1 halo (padded rows)
+  bf16_t* Ds = Hs + 2 * G::HS;                     // 2 x [T][C]    df of the tile (swizzled pieces)
+  bf16_t* Gs = Ds + 2 * G::DS;                     // [T][HP]       g of the tile
+  float* Ps = reinterpret_cast<float*>(Gs + G::GS);  // [10][HC] taps (identity in the centre) + bias
+  float* red = reinterpret_cast<float*>(smem);       // end of strip only
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, lq = lane >> 4;
   const int H = a.H, W = a.W, R = a.R;
@@ -459,16 +514,14 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
   const int c0 = chunk * HC;
   const T* __restrict__ hg = static_cast<const T*>(a.h);
   const T* __restrict__ dfg = static_cast<const T*>(a.df);
-  const T* __restrict__ xg = static_cast<const T*>(a.x);
   const T* __restrict__ w2 = static_cast<const T*>(a.w2);
-  T* __restrict__ dhg = static_cast<T*>(a.dh);
-  const void* zero = (const void*)g_ffn_zero;
+  T* __restrict__ dhp_g = static_cast<T*>(a.dh);  // dhpre out
+  const void* zero = (const void*)g_ffn_zero16;
 
   for (int i = tid; i < 10 * HC; i += 256) {
     const int tap = i / HC, j = i % HC;
     Ps[i] = tap < 9 ? a.wpos[(long)(c0 + j) * 9 + tap] + (tap == 4 ? 1.f : 0.f) : a.bpos[c0 + j];
   }
-  for (int i = tid; i < 2 * C; i += 256) Lw[i] = i < C ? a.lnw[i] : a.lnb[i - C];
   const int rb = wave % G::RB;
   const int chl = 16 * rb + 4 * lq;  // the lane's 4 hidden channels (within the chunk) in [A] / [B]
   bf16x8_t wa[G::KS1];  // W2c^T[HC, C] as A fragments: row = hidden channel 16 rb + l15, k = c
@@ -481,19 +534,9 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
       v[j] = __builtin_bit_cast(unsigned short, w2[(long)(32 * ks + 8 * lq + j) * R + c0 + 16 * rb + l15]);
     wa[ks] = __builtin_bit_cast(bf16x8_t, v);
   }
-  float dwp[4][9], dbp[4];
+  float4_t aw2[G::NCB3];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    dbp[j] = 0.f;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) dwp[j][k] = 0.f;
-  }
-  float db1[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) db1[j] = 0.f;
-  float4_t aw2[G::NCB3], aw1[G::NCB3];
-#pragma unroll
-  for (int i = 0; i < G::NCB3; ++i) aw2[i] = aw1[i] = float4_t{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < G::NCB3; ++i) aw2[i] = float4_t{0.f, 0.f, 0.f, 0.f};
   constexpr int RS2 = 256 / C;
   float db2 = 0.f;
 
@@ -505,8 +548,6 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
     y0 = (r % a.tiles_y) * TH;
     b = r / a.tiles_y;
   };
-  // DMA the h chunk and df of `tile` into buffer `buf` (wave-instruction wi writes slots 64 wi ..;
-  // lanes past an image's end are inactive; out-of-image pixels and pad slots read a zero page)
   auto issue = [&](int tile, int buf) {
     int b, y0, x0;
     tile_xy(tile, b, y0, x0);
@@ -517,10 +558,10 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
       const int q = wi * 64 + ln;
       if (q < G::NSH) {
         const int row = q / G::HSL, slot = q - row * G::HSL;
-        const int yy = y0 + row / G::EW2 - 2, xx = x0 + row % G::EW2 - 2;
-        const void* src = zero;
-        if (slot < HC / 8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
-          src = hg + (((long)b * H + yy) * W + xx) * R + c0 + 8 * slot;
+        const int yy = y0 + row / G::EW1 - 1, xx = x0 + row % G::EW1 - 1;
+        const void* src = static_cast<const unsigned char*>(zero) + 16 * ln;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)  // a pad slot re-reads the pixel's first piece
+          src = hg + (((long)b * H + yy) * W + xx) * R + c0 + 8 * (slot < HC / 8 ? slot : 0);
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                          (void __attribute__((address_space(3)))*)(hbase + wi * 1024), 16, 0, 0);
       }
@@ -530,10 +571,9 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
       const int q = wi * 64 + ln;
       if (q < G::NSD) {
         const int row = q / G::PC, pos = q - row * G::PC, piece = pos ^ swz<G::PC>(row);
-        const int yy = y0 + row / G::EW1 - 1, xx = x0 + row % G::EW1 - 1;
-        const void* src = zero;
-        if (row < G::T1 && yy >= 0 && yy < H && xx >= 0 && xx < W)
-          src = dfg + (((long)b * H + yy) * W + xx) * C + 8 * piece;
+        const int yy = y0 + row / TW, xx = x0 + row % TW;
+        const void* src = static_cast<const unsigned char*>(zero) + 16 * ln;
+        if (yy < H && xx < W) src = dfg + (((long)b * H + yy) * W + xx) * C + 8 * piece;
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
                                          (void __attribute__((address_space(3)))*)(dbase + wi * 1024), 16, 0, 0);
       }
@@ -547,161 +587,67 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
     tile_xy(tile, b, y0, x0);
     const bf16_t* Hc = Hs + cur * G::HS;
     const bf16_t* Dc = Ds + cur * G::DS;
-    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): this tile's DMAs (and everything older)
+    __builtin_amdgcn_s_waitcnt(0);  // this tile's DMAs (and everything older)
     __builtin_amdgcn_s_barrier();
-    // x of this tile + the forward's LN statistics (registers; normalised into Xs after [B])
-    uint4 xv[G::NXV];
-    float xmu[G::NXV], xrs[G::NXV];
-#pragma unroll
-    for (int k = 0; k < G::NXV; ++k) {
-      const int q = tid + 256 * k, pi = q / G::PC;
-      const bool in = (G::T * G::PC % 256 == 0 || pi < G::T) && y0 + pi / TW < H && x0 + pi % TW < W;
-      const long p = ((long)b * H + y0 + pi / TW) * W + x0 + pi % TW;
-      xv[k] = in ? *reinterpret_cast<const uint4*>(xg + p * C + 8 * (q % G::PC)) : make_uint4(0, 0, 0, 0);
-      xmu[k] = in ? a.mean[p] : 0.f;
-      xrs[k] = in ? a.rstd[p] : 0.f;
-    }
-#ifndef FFN_EXP_NO_DMA
     if (tile + 1 < t_end) issue(tile + 1, cur ^ 1);  // in flight under this tile
-#endif
-    // ---- [A] dg^T = W2c^T df^T (tile + 1 halo), [B] hpre, GELU / GELU' (one erf), dhpre -> Dh,
-    //      g (tile) -> Gs, dwpos / dbpos sums; one column block at a time
-#ifndef FFN_EXP_NO_B
+    // ---- [A] + [B], one (row block, column block) pair at a time
 #pragma unroll 1
-    for (int i = 0; i < G::NCB1; ++i) {
+    for (int i = 0; i < G::NPAIR; ++i) {
       const int cb = wave / G::RB + i * (4 / G::RB);
-      if ((G::CB1 * G::RB) % 4 != 0 && cb >= G::CB1) break;
-      const int e = 16 * cb + l15;
+      const int pi = 16 * cb + l15, py = pi / TW, px = pi % TW;  // tile pixel of this lane
       float4_t dg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < G::KS1; ++ks)
-        dg = mma16<T>(wa[ks], ldfrag(Dc + sw_off<G::PC>(e, 32 * ks + 8 * lq)), dg);
-      if (e < G::T1) {
-        const int ey = e / G::EW1, ex = e % G::EW1;
-        const bf16_t* hb = Hc + (ey * G::EW2 + ex) * HP + chl;  // tap (0, 0); tap t at + off(t)
-        float hv[9][4];
-        float hp[4];
-        {
-          const float4 bp = *reinterpret_cast<const float4*>(Ps + 9 * HC + chl);
-          hp[0] = bp.x; hp[1] = bp.y; hp[2] = bp.z; hp[3] = bp.w;
-        }
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          ld4h<T>(reinterpret_cast<const T*>(hb + ((tap / 3) * G::EW2 + tap % 3) * HP), hv[tap]);
-          const float4 wt = *reinterpret_cast<const float4*>(Ps + tap * HC + chl);
-          hp[0] = fmaf(wt.x, hv[tap][0], hp[0]);
-          hp[1] = fmaf(wt.y, hv[tap][1], hp[1]);
-          hp[2] = fmaf(wt.z, hv[tap][2], hp[2]);
-          hp[3] = fmaf(wt.w, hv[tap][3], hp[3]);
-        }
-        float g[4], dhp[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float cdf, pdf;
-          normal_cdf_pdf(hp[j], cdf, pdf);
-          g[j] = hp[j] * cdf;
-          dhp[j] = Num<T>::to_f(Num<T>::from_f(dg[j] * fmaf(hp[j], pdf, cdf)));  // rounded as stored
-        }
-        st4h<T>(reinterpret_cast<T*>(Dh + e * HP + chl), dhp);
-        if (ey >= 1 && ey <= TH && ex >= 1 && ex <= TW) {
-          const int pi = (ey - 1) * TW + ex - 1;
-          const bool in = y0 + ey - 1 < H && x0 + ex - 1 < W;
-          if (!in) g[0] = g[1] = g[2] = g[3] = 0.f;
-          st4h<T>(reinterpret_cast<T*>(Gs + pi * HP + chl), g);
-          if (in) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              dbp[j] += dhp[j];
-#pragma unroll
-              for (int tap = 0; tap < 9; ++tap) dwp[j][tap] = fmaf(dhp[j], hv[tap][j], dwp[j][tap]);
-            }
-          }
-        }
+      for (int ks = 0; ks < G::KS1; ++ks) dg = mma16<T>(wa[ks], ldfrag(Dc + sw_off<G::PC>(pi, 32 * ks + 8 * lq)), dg);
+      const bf16_t* hb = Hc + (py * G::EW1 + px) * HP + chl;  // tap (0, 0); tap t at + off(t)
+      float hp[4];
+      {
+        const float4 bp = *reinterpret_cast<const float4*>(Ps + 9 * HC + chl);
+        hp[0] = bp.x; hp[1] = bp.y; hp[2] = bp.z; hp[3] = bp.w;
       }
-    }
-#endif
-    // ---- LN(x) of the tile (the forward's statistics) -> Xs
 #pragma unroll
-    for (int k = 0; k < G::NXV; ++k) {
-      const int q = tid + 256 * k, pi = q / G::PC, c = 8 * (q % G::PC);
-      if (G::T * G::PC % 256 != 0 && pi >= G::T) break;
-      float v[8], o[8];
-      unpack8w<T>(xv[k], v);
-      const float4 w0 = *reinterpret_cast<const float4*>(Lw + c), w1 = *reinterpret_cast<const float4*>(Lw + c + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(Lw + C + c), b1 = *reinterpret_cast<const float4*>(Lw + C + c + 4);
-      const float wl[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      const float bl[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      for (int tap = 0; tap < 9; ++tap) {
+        float hv[4];
+        ld4h<T>(reinterpret_cast<const T*>(hb + ((tap / 3) * G::EW1 + tap % 3) * HP), hv);
+        const float4 wt = *reinterpret_cast<const float4*>(Ps + tap * HC + chl);
+        hp[0] = fmaf(wt.x, hv[0], hp[0]);
+        hp[1] = fmaf(wt.y, hv[1], hp[1]);
+        hp[2] = fmaf(wt.z, hv[2], hp[2]);
+        hp[3] = fmaf(wt.w, hv[3], hp[3]);
+      }
+      float g[4], dhp[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = xrs[k] != 0.f ? (v[j] - xmu[k]) * xrs[k] * wl[j] + bl[j] : 0.f;
-      st8<T>(reinterpret_cast<T*>(Xs + pi * G::XP + c), o);
-    }
-    lds_barrier();
-    // ---- [C] dh = DW3x3^T(dhpre) + dhpre on the tile -> HBM and DHs; db1
-#ifndef FFN_EXP_NO_C
-#pragma unroll
-    for (int it = 0; it < G::NI; ++it) {
-      const int item = tid + 256 * it;
-      if (G::ITEMS % 256 != 0 && item >= G::ITEMS) break;
-      const int pi = item / G::NQ, cc = 8 * (item % G::NQ);
-      const int py = pi / TW, px = pi % TW;
+      for (int j = 0; j < 4; ++j) {
+        float cdf, pdf;
+        normal_cdf_pdf(hp[j], cdf, pdf);
+        g[j] = hp[j] * cdf;
+        dhp[j] = dg[j] * fmaf(hp[j], pdf, cdf);
+      }
       const bool in = y0 + py < H && x0 + px < W;
-      const bf16_t* db = Dh + ((py + 2) * G::EW1 + px + 2) * HP + cc;  // dhpre at q - off(tap 0)
-      float d[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = 0.f;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {  // transposed conv: dh[q] = sum_tap w[tap] dhpre[q - off(tap)]
-        float dv[8];
-        unpack8w<T>(*reinterpret_cast<const uint4*>(db - ((tap / 3) * G::EW1 + tap % 3) * HP), dv);
-        const float4 q0 = *reinterpret_cast<const float4*>(Ps + tap * HC + cc);
-        const float4 q1 = *reinterpret_cast<const float4*>(Ps + tap * HC + cc + 4);
-        const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = fmaf(wv[j], dv[j], d[j]);
-      }
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (in) {
-        u = make_uint4(pack2<T>(d[0], d[1]), pack2<T>(d[2], d[3]), pack2<T>(d[4], d[5]), pack2<T>(d[6], d[7]));
-        float r[8];
-        unpack8w<T>(u, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) db1[j] += r[j];
-        *reinterpret_cast<uint4*>(dhg + (((long)b * H + y0 + py) * W + x0 + px) * R + c0 + cc) = u;
-      }
-      *reinterpret_cast<uint4*>(DHs + pi * HP + cc) = u;
+      if (in) st4h<T>(dhp_g + (((long)b * H + y0 + py) * W + x0 + px) * R + c0 + chl, dhp);
+      else g[0] = g[1] = g[2] = g[3] = 0.f;
+      st4h<T>(reinterpret_cast<T*>(Gs + pi * HP + chl), g);
     }
-#endif
-    // ---- [D1] dW2^T[HC, C] += g^T df (K = tile pixels: df rows of the tile's interior); db2 (chunk 0)
-    auto int_row = [](int k) { return (k / TW + 1) * G::EW1 + k % TW + 1; };
-#pragma unroll
-    for (int i = 0; i < G::NCB3; ++i) {
-      const int cb = wave / G::RB + i * (4 / G::RB);
-      if ((G::CB3 * G::RB) % 4 != 0 && cb >= G::CB3) break;
-#pragma unroll
-      for (int ks = 0; ks < G::KS3; ++ks)
-        aw2[i] = mma16<T>(tr_frag(Gs, HP, 32 * ks, 16 * rb, lane), tr_frag_sw<G::PC>(Dc, 32 * ks, 16 * cb, lane, int_row),
-                          aw2[i]);
-    }
-    if (chunk == 0) {
+    if (chunk == 0) {  // db2 = sum df over the strip
       const int c = tid % C;
       for (int pi = tid / C; pi < G::T; pi += RS2)
-        db2 += Num<T>::to_f(reinterpret_cast<const T*>(Dc)[sw_off<G::PC>(int_row(pi), c)]);
+        db2 += Num<T>::to_f(reinterpret_cast<const T*>(Dc)[sw_off<G::PC>(pi, c)]);
     }
     lds_barrier();
-    // ---- [D2] dW1[HC, C] += dh^T LN(x)
+    // ---- [D] dW2^T[HC, C] += g^T df (K = tile pixels)
+    auto id_row = [](int k) { return k; };
 #pragma unroll
     for (int i = 0; i < G::NCB3; ++i) {
       const int cb = wave / G::RB + i * (4 / G::RB);
       if ((G::CB3 * G::RB) % 4 != 0 && cb >= G::CB3) break;
 #pragma unroll
       for (int ks = 0; ks < G::KS3; ++ks)
-        aw1[i] = mma16<T>(tr_frag(DHs, HP, 32 * ks, 16 * rb, lane), tr_frag(Xs, G::XP, 32 * ks, 16 * cb, lane), aw1[i]);
+        aw2[i] = mma16<T>(tr_frag(Gs, HP, 32 * ks, 16 * rb, lane), tr_frag_sw<G::PC>(Dc, 32 * ks, 16 * cb, lane, id_row),
+                          aw2[i]);
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-
-  // ---- per-strip partials (plain stores; one fixed-order grouped sum over the strips follows)
+  // ---- per-strip partials
   const long S = strip;
 #pragma unroll
   for (int i = 0; i < G::NCB3; ++i) {
@@ -710,43 +656,8 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
     const int c = 16 * cb + l15;
     *reinterpret_cast<float4*>(a.part_w2 + S * C * R + (long)c * R + c0 + chl) =
         make_float4(aw2[i][0], aw2[i][1], aw2[i][2], aw2[i][3]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a.part_w1[S * R * C + (long)(c0 + chl + j) * C + c] = aw1[i][j];
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) dwp[j][tap] = group_sum<16>(dwp[j][tap]);
-    dbp[j] = group_sum<16>(dbp[j]);
-  }
-  if (l15 == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) red[((wave * 4 + lq) * 4 + j) * 10 + tap] = dwp[j][tap];
-      red[((wave * 4 + lq) * 4 + j) * 10 + 9] = dbp[j];
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < HC * 10; i += 256) {
-    const int cl = i / 10, k = i % 10;  // channel within the chunk, tap (9 = bias)
-    const int r = cl / 16, lqq = (cl % 16) / 4, jj = cl % 4;
-    float s = 0.f;
-    for (int w = r; w < 4; w += G::RB) s += red[((w * 4 + lqq) * 4 + jj) * 10 + k];
-    a.part_pos[S * R * 10 + (long)(c0 + cl) * 10 + k] = s;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 8; ++j) red[tid * 8 + j] = db1[j];
-  __syncthreads();
-  if (tid < HC) {
-    const int kq = tid / 8, j = tid % 8;
-    float s = 0.f;
-    for (int t2 = kq; t2 < 256; t2 += G::NQ) s += red[t2 * 8 + j];
-    a.part_b1[S * R + c0 + tid] = s;
   }
   if (chunk == 0) {
-    __syncthreads();
     red[tid] = db2;
     __syncthreads();
     if (tid < C) {
@@ -758,29 +669,29 @@ __global__ __launch_bounds__(256, 2) void ffn_bwd_kernel(FfnBwdArgs a) {
 }
 
 // ============================================================================ host side
-template <int C> struct FfnCfg;  // tile shapes per channel count (forward; the backward tiles 8 x 8)
+template <int C> struct FfnCfg;  // hidden chunk and tile shapes per channel count
 template <> struct FfnCfg<32> {
-  static constexpr int FHC = 32, FTH = 8, FTW = 16, BHC = 32;
+  static constexpr int FHC = 32, FTH = 8, FTW = 16, BHC = 32, DTH = 8, DTW = 8;
 };
 template <> struct FfnCfg<64> {
-  static constexpr int FHC = 32, FTH = 8, FTW = 16, BHC = 32;
+  static constexpr int FHC = 32, FTH = 8, FTW = 8, BHC = 32, DTH = 8, DTW = 8;
 };
 template <> struct FfnCfg<128> {
-  static constexpr int FHC = 32, FTH = 4, FTW = 16, BHC = 32;
+  static constexpr int FHC = 32, FTH = 4, FTW = 8, BHC = 32, DTH = 8, DTW = 8;
 };
 template <> struct FfnCfg<256> {
-  static constexpr int FHC = 32, FTH = 4, FTW = 16, BHC = 32;
+  static constexpr int FHC = 32, FTH = 4, FTW = 4, BHC = 32, DTH = 4, DTW = 8;
 };
 
 bool ffn_shape_ok(int C, int R) {
-  return (C == 32 || C == 64) && R % 32 == 0 && R >= 32;
+  return (C == 32 || C == 64 || C == 128 || C == 256) && R % 128 == 0;
 }
 
-template <typename T, int C>
-int ffn_fwd_launch(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
+template <typename T, int C, int TH, int TW>
+int ffn_fwd_launch_t(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
   using Cf = FfnCfg<C>;
-  using G = FwdGeom<C, Cf::FHC>;
-  auto kern = ffn_fwd_kernel<T, C, Cf::FHC>;
+  using G = FwdGeom<C, Cf::FHC, TH, TW>;
+  auto kern = ffn_fwd_kernel<T, C, Cf::FHC, TH, TW>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
@@ -794,22 +705,40 @@ int ffn_fwd_launch(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
   return DFM_OK;
 }
 
+// DFM_FFN_FWD_SMALL=1 (A/B): half-size forward tiles (T * C = 2048: 32 accumulator registers, higher occupancy)
+static bool ffn_fwd_small() {
+  static int v = [] {
+    const char* e = getenv("DFM_FFN_FWD_SMALL");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v != 0;
+}
+
+template <typename T, int C>
+int ffn_fwd_launch(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
+  using Cf = FfnCfg<C>;
+  if constexpr (C <= 128) {
+    if (ffn_fwd_small()) return ffn_fwd_launch_t<T, C, (C == 32 ? 8 : 4), (C == 128 ? 4 : 8)>(d, a, s);
+  }
+  return ffn_fwd_launch_t<T, C, Cf::FTH, Cf::FTW>(d, a, s);
+}
+
 struct BwdPlan {
   int tiles_x, tiles_y, ntiles, nstrip, tps, nch;
   size_t lds;
 };
 
 template <int C>
-BwdPlan ffn_bwd_plan(const DfmConvFFNDesc* d) {
+BwdPlan ffn_dh_plan(const DfmConvFFNDesc* d) {
   using Cf = FfnCfg<C>;
+  using G = DhGeom<C, Cf::BHC, Cf::DTH, Cf::DTW>;
   BwdPlan p;
-  using G = BwdGeom<C, Cf::BHC>;
   p.tiles_x = (int)cdiv(d->W, G::TW);
   p.tiles_y = (int)cdiv(d->H, G::TH);
   p.ntiles = d->B * p.tiles_x * p.tiles_y;
   p.nch = d->hidden / Cf::BHC;
-  // strips: about 2 workgroups per CU over (strip, chunk), a multiple of 8 strips (one XCD each)
-  int ns = (512 + p.nch - 1) / p.nch;
+  // about 4 workgroups per CU over (strip, chunk): the tile loop's DMA waits overlap across them
+  int ns = (1024 + p.nch - 1) / p.nch;
   ns = std::max(8, std::min((ns + 7) / 8 * 8, (p.ntiles + 7) / 8 * 8));
   p.tps = (p.ntiles + ns - 1) / ns;
   p.nstrip = (p.ntiles + p.tps - 1) / p.tps;
@@ -817,19 +746,19 @@ BwdPlan ffn_bwd_plan(const DfmConvFFNDesc* d) {
   return p;
 }
 
-BwdPlan bwd_plan(const DfmConvFFNDesc* d) {
+BwdPlan dh_plan(const DfmConvFFNDesc* d) {
   switch (d->C) {
-    case 32: return ffn_bwd_plan<32>(d);
-    case 64: return ffn_bwd_plan<64>(d);
-    case 128: return ffn_bwd_plan<128>(d);
-    default: return ffn_bwd_plan<256>(d);
+    case 32: return ffn_dh_plan<32>(d);
+    case 64: return ffn_dh_plan<64>(d);
+    case 128: return ffn_dh_plan<128>(d);
+    default: return ffn_dh_plan<256>(d);
   }
 }
 
 template <typename T, int C>
-int ffn_bwd_launch(const BwdPlan& p, FfnBwdArgs a, hipStream_t s) {
+int ffn_dh_launch(const BwdPlan& p, FfnBwdArgs a, hipStream_t s) {
   using Cf = FfnCfg<C>;
-  auto kern = ffn_bwd_kernel<T, C, Cf::BHC>;
+  auto kern = ffn_dhpre_kernel<T, C, Cf::BHC, Cf::DTH, Cf::DTW>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds);
@@ -857,7 +786,7 @@ int ffn_bwd_launch(const BwdPlan& p, FfnBwdArgs a, hipStream_t s) {
   }()
 
 struct BwdWs {
-  size_t df, dh, du, pw2, pw1, pb1, ppos, pb2, res, ln, gemm, total;
+  size_t df, dh, du, pw2, pb2, res, ln, gemm, dhp, dw, wg, total;
 };
 
 DfmGemmDesc du_desc(const DfmConvFFNDesc* d) {
@@ -879,25 +808,48 @@ DfmGemmDesc du_desc(const DfmConvFFNDesc* d) {
   return g;
 }
 
+DfmGemmDesc w1_desc(const DfmConvFFNDesc* d) {
+  // dW1[R, C] = dh^T xn (+ db1 = column sums of dh): K = pixels, both operands row-contiguous
+  DfmGemmDesc g{};
+  const long P = (long)d->B * d->H * d->W;
+  g.M = d->hidden;
+  g.N = d->C;
+  g.K = (int)P;
+  g.batch = 1;
+  g.a_kcontig = 0;
+  g.b_kcontig = 0;
+  g.lda = d->hidden;
+  g.ldb = d->C;
+  g.ldc = d->C;
+  g.alpha = 1.f;
+  g.beta = 0.f;
+  g.c_f32 = 1;
+  g.rows_per_scale = 1;
+  return g;
+}
+
 BwdWs bwd_ws(int dtype, const DfmConvFFNDesc* d) {
   const size_t es = dtype == DFM_F32 ? 4 : 2;
   const long P = (long)d->B * d->H * d->W;
-  const BwdPlan p = bwd_plan(d);
   BwdWs w{};
   auto al = [](size_t v) { return (v + 255) / 256 * 256; };
   w.df = al(es * P * d->C);
   w.dh = al(es * P * d->hidden);
   w.du = al(es * P * d->C);
-  w.pw2 = al((size_t)p.nstrip * d->C * d->hidden * 4);
-  w.pw1 = w.pw2;
-  w.pb1 = al((size_t)p.nstrip * d->hidden * 4);
-  w.ppos = al((size_t)p.nstrip * d->hidden * 10 * 4);
-  w.pb2 = al((size_t)p.nstrip * d->C * 4);
   w.res = al(dfm_residual_bwd_workspace(P, d->C));
   w.ln = al(dfm_layernorm_bwd_workspace(P, d->C));
   DfmGemmDesc g = du_desc(d);
   w.gemm = al(dfm_gemm_workspace_size(&g));
-  w.total = w.df + w.dh + w.du + w.pw2 + w.pw1 + w.pb1 + w.ppos + w.pb2 + w.res + w.ln + w.gemm;
+  // dhpre (+ dW2 / db2 strip partials), depthwise weight-gradient partials, fc1 weight-gradient GEMM
+  const BwdPlan q = dh_plan(d);
+  w.pw2 = al((size_t)q.nstrip * d->C * d->hidden * 4);
+  w.pb2 = al((size_t)q.nstrip * d->C * 4);
+  w.dhp = al(es * P * d->hidden);
+  w.dw = al(dfm_dwconv_bwd_weight_workspace(d->B, d->H, d->W, d->hidden, 3));
+  DfmGemmDesc gw = w1_desc(d);
+  gw.colsum = reinterpret_cast<float*>(16);  // sized with its bias-gradient column (only nullness is read)
+  w.wg = al(dfm_gemm_workspace_size(&gw));
+  w.total = w.df + w.dh + w.du + w.pw2 + w.pb2 + w.res + w.ln + w.gemm + w.dhp + w.dw + w.wg;
   return w;
 }
 
@@ -911,8 +863,8 @@ extern "C" int dfm_convffn_supported(int dtype, const DfmConvFFNDesc* d) {
 extern "C" int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x, const float* ln_w,
                                const float* ln_b, const void* w1, const float* b1, const float* wpos,
                                const float* bpos, const void* w2, const float* b2, const float* ls,
-                               const float* rowscale, void* out, void* f, void* h, float* mean, float* rstd,
-                               dfm_stream_t stream) {
+                               const float* rowscale, void* out, void* f, void* h, void* xn, float* mean,
+                               float* rstd, dfm_stream_t stream) {
   DFM_CHECK_ARG(dfm_convffn_supported(dtype, d), "dfm_convffn_fwd: unsupported dtype %d / shape (C %d, hidden %d)",
                 dtype, d ? d->C : -1, d ? d->hidden : -1);
   DFM_CHECK_ARG(x && ln_w && ln_b && w1 && b1 && wpos && bpos && w2 && b2 && ls && out && f && h && mean && rstd,
@@ -923,7 +875,7 @@ extern "C" int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x
   a.rps = (long)d->H * d->W;
   a.x = x; a.lnw = ln_w; a.lnb = ln_b; a.w1 = w1; a.b1 = b1; a.wpos = wpos; a.bpos = bpos;
   a.w2 = w2; a.b2 = b2; a.ls = ls; a.rowscale = rowscale;
-  a.out = out; a.f = f; a.h = h; a.mean = mean; a.rstd = rstd;
+  a.out = out; a.f = f; a.h = h; a.xn = xn; a.mean = mean; a.rstd = rstd;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) {
     using T = bf16_t;
@@ -939,14 +891,15 @@ extern "C" size_t dfm_convffn_bwd_workspace_size(int dtype, const DfmConvFFNDesc
 }
 
 extern "C" int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const void* x, const void* h,
-                               const void* f, const float* mean, const float* rstd, const float* ln_w,
-                               const float* ln_b, const void* w1, const float* wpos, const float* bpos,
-                               const void* w2, const float* ls, const float* rowscale, void* dx, float* dln_w,
-                               float* dln_b, float* dw1, float* db1, float* dwpos, float* dbpos, float* dw2,
-                               float* db2, float* dls, void* workspace, size_t workspace_bytes, dfm_stream_t stream) {
+                               const void* xn, const void* f, const float* mean, const float* rstd,
+                               const float* ln_w, const float* ln_b, const void* w1, const float* wpos,
+                               const float* bpos, const void* w2, const float* ls, const float* rowscale, void* dx,
+                               float* dln_w, float* dln_b, float* dw1, float* db1, float* dwpos, float* dbpos,
+                               float* dw2, float* db2, float* dls, void* workspace, size_t workspace_bytes,
+                               dfm_stream_t stream) {
   DFM_CHECK_ARG(dfm_convffn_supported(dtype, d), "dfm_convffn_bwd: unsupported dtype %d / shape (C %d, hidden %d)",
                 dtype, d ? d->C : -1, d ? d->hidden : -1);
-  DFM_CHECK_ARG(dout && x && h && f && mean && rstd && ln_w && ln_b && w1 && wpos && bpos && w2 && ls && dx &&
+  DFM_CHECK_ARG(dout && x && h && xn && f && mean && rstd && ln_w && ln_b && w1 && wpos && bpos && w2 && ls && dx &&
                     dln_w && dln_b && dw1 && db1 && dwpos && dbpos && dw2 && db2 && dls && workspace,
                 "dfm_convffn_bwd: null argument");
   const BwdWs w = bwd_ws(dtype, d);
@@ -959,40 +912,47 @@ extern "C" int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* d
   void* dh = ws; ws += w.dh;
   void* du = ws; ws += w.du;
   float* pw2 = (float*)ws; ws += w.pw2;
-  float* pw1 = (float*)ws; ws += w.pw1;
-  float* pb1 = (float*)ws; ws += w.pb1;
-  float* ppos = (float*)ws; ws += w.ppos;
   float* pb2 = (float*)ws; ws += w.pb2;
   void* wres = ws; ws += w.res;
   void* wln = ws; ws += w.ln;
-  void* wgemm = ws;
-  DfmPartialSum sums[8];
+  void* wgemm = ws; ws += w.gemm;
+  void* dhp = ws; ws += w.dhp;
+  void* wdw = ws; ws += w.dw;
+  void* wwg = ws;
+  DfmPartialSum sums[12];
   int ns = 0;
   // residual / layer-scale backward: df = dout * ls * rowscale, dls = sum dout * f * rowscale
   int rc = dfm_residual_bwd(dtype, P, C, dout, C, f, C, ls, rowscale, (long)d->H * d->W, df, C, dls, wres, &sums[ns],
                             stream);
   if (rc != DFM_OK) return rc;
   if (sums[ns].part) ++ns;
-  // hidden part
-  const BwdPlan p = bwd_plan(d);
   FfnBwdArgs a{};
   a.B = d->B; a.H = d->H; a.W = d->W; a.R = R;
-  a.x = x; a.mean = mean; a.rstd = rstd; a.lnw = ln_w; a.lnb = ln_b; a.h = h; a.df = df; a.w2 = w2;
-  a.wpos = wpos; a.bpos = bpos; a.dh = dh;
-  a.part_w2 = pw2; a.part_w1 = pw1; a.part_b1 = pb1; a.part_pos = ppos; a.part_b2 = pb2;
+  a.h = h; a.df = df; a.w2 = w2;
+  a.wpos = wpos; a.bpos = bpos;
+  a.part_w2 = pw2; a.part_b2 = pb2;
+  // dhpre (+ dW2, db2) -> depthwise input / weight gradients -> fc1 weight gradient (+ db1)
+  const BwdPlan p = dh_plan(d);
+  a.dh = dhp;
   if (dtype == DFM_BF16) {
     using T = bf16_t;
-    rc = FFN_C_SWITCH(C, ffn_bwd_launch, p, a, s);
+    rc = FFN_C_SWITCH(C, ffn_dh_launch, p, a, s);
   } else {
     using T = f16_t;
-    rc = FFN_C_SWITCH(C, ffn_bwd_launch, p, a, s);
+    rc = FFN_C_SWITCH(C, ffn_dh_launch, p, a, s);
   }
   if (rc != DFM_OK) return rc;
   sums[ns++] = DfmPartialSum{pw2, dw2, nullptr, (long)C * R, 0, p.nstrip, 0, 0};
-  sums[ns++] = DfmPartialSum{pw1, dw1, nullptr, (long)R * C, 0, p.nstrip, 0, 0};
-  sums[ns++] = DfmPartialSum{pb1, db1, nullptr, (long)R, 0, p.nstrip, 0, 0};
-  sums[ns++] = DfmPartialSum{ppos, dwpos, dbpos, (long)R * 10, 10, p.nstrip, 2, 0};
   sums[ns++] = DfmPartialSum{pb2, db2, nullptr, (long)C, 0, p.nstrip, 0, 0};
+  rc = dfm_dwconv_bwd(dtype, d->B, d->H, d->W, R, 3, h, R, dhp, R, wpos, 1, dh, R, 0, dwpos, dbpos, wdw, &sums[ns],
+                      stream);
+  if (rc != DFM_OK) return rc;
+  if (sums[ns].part) ++ns;
+  DfmGemmDesc gw = w1_desc(d);
+  gw.colsum = db1;
+  gw.workspace_bytes = (long)w.wg;
+  rc = dfm_gemm(dtype, &gw, dh, xn, dw1, wwg, stream);
+  if (rc != DFM_OK) return rc;
   // fc1 input gradient du = dh W1, then the LayerNorm backward with the residual's dout
   DfmGemmDesc g = du_desc(d);
   g.workspace_bytes = (long)w.gemm;

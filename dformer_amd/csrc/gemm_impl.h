@@ -766,7 +766,7 @@ template <int N>
 DFM_INLINE void wait_vm() { __builtin_amdgcn_s_waitcnt(vmcnt_imm(N)); }
 DFM_INLINE void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8)); }
 
-template <int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
+template <typename T, int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
 __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int WAVES_N = NW / WAVES_M;
@@ -802,12 +802,12 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
   const int nfull = (kend - kbeg) / GBK;  // >= 2 whenever the host picks this kernel, except short splits
   const int ones_r = a.colsum != nullptr ? a.N : -1;
 
-  const bf16_t* A = (const bf16_t*)a.A + (long)b * a.sa;
-  const bf16_t* Bp = (const bf16_t*)a.B + (long)b * a.sb;
+  const T* A = (const T*)a.A + (long)b * a.sa;
+  const T* Bp = (const T*)a.B + (long)b * a.sb;
 
   // per DMA j of this lane: source of slice 0, per-slice step (elements), LDS offset in a stage,
   // and (virtual ones column) the element of the chunk to overwrite with 1.0 after it lands
-  const bf16_t* src[J];
+  const T* src[J];
   long step[J];
   int dst[J], ones_e[J];
 #pragma unroll
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[h][i], fb[h][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = mma16<T>(fa[h][i], fb[h][j], acc[i][j]);
   };
   auto compute = [&](int stage) {
     bf16x8_t fa[2][TM], fb[2][TN];
@@ -936,12 +936,12 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
       uint4 v;
       if (isA) {
         IA::at(gq, row, chunk);
-        v = AK ? load_vec<bf16_t, true>(A, a.lda, bm + row, k0 + chunk * 8, a.M, kend, true, -1)
-               : load_vec<bf16_t, false>(A, a.lda, bm + chunk * 8, k0 + row, a.M, kend, true, -1);
+        v = AK ? load_vec<T, true>(A, a.lda, bm + row, k0 + chunk * 8, a.M, kend, true, -1)
+               : load_vec<T, false>(A, a.lda, bm + chunk * 8, k0 + row, a.M, kend, true, -1);
       } else {
         IB::at(gq, row, chunk);
-        v = BKC ? load_vec<bf16_t, true>(Bp, a.ldb, bn + row, k0 + chunk * 8, a.N, kend, true, ones_r)
-                : load_vec<bf16_t, false>(Bp, a.ldb, bn + chunk * 8, k0 + row, a.N, kend, true, ones_r);
+        v = BKC ? load_vec<T, true>(Bp, a.ldb, bn + row, k0 + chunk * 8, a.N, kend, true, ones_r)
+                : load_vec<T, false>(Bp, a.ldb, bn + chunk * 8, k0 + row, a.N, kend, true, ones_r);
       }
       *reinterpret_cast<uint4*>(smem + dst[j] + lane * 16) = v;
     }
@@ -949,16 +949,16 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
     compute(0);
     __syncthreads();
   }
-  gemm_epilogue<bf16_t, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
+  gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
 }
 
-template <int BM, int BN, int NW, int WM_, bool AK, bool BKC, int NS, int MINB>
+template <typename T, int BM, int BN, int NW, int WM_, bool AK, bool BKC, int NS, int MINB>
 int launch_glds(GemmArgs& a, hipStream_t s) {
   using IA = GImg<BM, AK>;
   using IB = GImg<BN, BKC>;
   constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
   const size_t lds = std::max((size_t)NS * (IA::BYTES + IB::BYTES), (size_t)RP * (BN + 4) * sizeof(float));
-  auto kern = gemm_glds_kernel<BM, BN, NW, WM_, AK, BKC, NS, MINB>;
+  auto kern = gemm_glds_kernel<T, BM, BN, NW, WM_, AK, BKC, NS, MINB>;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -973,18 +973,18 @@ int launch_glds(GemmArgs& a, hipStream_t s) {
   if (a.splits > 1) {
     const long total = (long)a.batch * a.M * a.ldw;
     if (a.splits >= 8)
-      DFM_LAUNCH((splitk_reduce_kernel<bf16_t, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
+      DFM_LAUNCH((splitk_reduce_kernel<T, 4>), dim3(cdiv(total, 64)), dim3(256), 0, s, a);
     else
-      DFM_LAUNCH((splitk_reduce_kernel<bf16_t, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
+      DFM_LAUNCH((splitk_reduce_kernel<T, 1>), dim3(cdiv(total, 256)), dim3(256), 0, s, a);
     DFM_LAUNCH_CHECK();
   }
   return DFM_OK;
 }
 
-template <int BM, int BN, int NW, int WM_, int NS, int MINB>
+template <typename T, int BM, int BN, int NW, int WM_, int NS, int MINB>
 int glds_ak(GemmArgs& a, bool bk, hipStream_t s) {
-  if (bk) return launch_glds<BM, BN, NW, WM_, true, true, NS, MINB>(a, s);
-  return launch_glds<BM, BN, NW, WM_, true, false, NS, MINB>(a, s);
+  if (bk) return launch_glds<T, BM, BN, NW, WM_, true, true, NS, MINB>(a, s);
+  return launch_glds<T, BM, BN, NW, WM_, true, false, NS, MINB>(a, s);
 }
 
 template <typename T, int BM, int BN, int NW, int WM_, int BK, bool AK, bool BKC, int DEPTH>
@@ -1110,7 +1110,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // finishes late when the concurrent ConvFFN stream holds CUs)
   // bf16 k-contiguous A on the LDS-DMA ring: split-K off (one unsplit 64x64 ring block per tile beats
   // the split + reduction at 4,800 rows x K >= 1024: 16.8 vs 34.8 us, profiles/r04_glds_variants.txt)
-  bool glds_ok = std::is_same<T, bf16_t>::value && ak && a.ala && a.alb;
+  bool glds_ok = sizeof(T) == 2 && ak && a.ala && a.alb;
   if (glds_ok && d->split_k < 1) a.splits = 1;
   glds_ok = glds_ok && (d->K + a.splits - 1) / a.splits >= 2 * GBK;  // >= 2 whole k-slices per split
   // tall short-K GEMMs with more than one 128-column slice (gemm_wide.h): measured per shape on the
@@ -1130,14 +1130,14 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // tiles chosen per shape (128x128 from 65,536 rows, 128x64 / 64x128 elsewhere: 1 ms less GEMM time
   // per step replayed in isolation, tools/gemm_variants.py) measured flat on the step (37.45-37.59
   // ms/step either way, profiles/r04_glds_variants.txt).
-  if constexpr (std::is_same<T, bf16_t>::value) {  // the LDS-DMA ring kernel is bf16-only
+  if constexpr (sizeof(T) == 2) {  // the LDS-DMA ring kernel: bf16 and fp16
     const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 128);
     if (glds_ok && route) {
-      if (BN == 32) return glds_ak<128, 32, 4, 4, 2, 3>(a, bk, s);
+      if (BN == 32) return glds_ak<T, 128, 32, 4, 4, 2, 3>(a, bk, s);
       // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
       // (438.7-438.4 -> 439.0-440.3 images/s on one box; 65-93 vs 81-127 us per launch alone)
-      if (a.splits == 1 && d->M >= 65536 && a.Nw >= 512 && d->K >= 512) return glds_ak<128, 128, 8, 2, 2, 2>(a, bk, s);
-      return glds_ak<64, 64, 4, 2, 2, 4>(a, bk, s);
+      if (a.splits == 1 && d->M >= 65536 && a.Nw >= 512 && d->K >= 512) return glds_ak<T, 128, 128, 8, 2, 2, 2>(a, bk, s);
+      return glds_ak<T, 64, 64, 4, 2, 2, 4>(a, bk, s);
     }
   }
   if (small_k) {

@@ -25,7 +25,7 @@ void dfm_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* dfm_last_error(void) { return g_err; }
-extern "C" int dfm_abi_version(void) { return 10; }  // 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
+extern "C" int dfm_abi_version(void) { return 11; }  // 11: dfm_block_fwd / _bwd; 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
 
 // ---------------------------------------------------------------- launch tracer
 // dfm_trace_flags is read by DFM_LAUNCH (common.h) before every kernel launch; 0 = tracer off and

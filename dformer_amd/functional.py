@@ -9,6 +9,7 @@ Reference semantics (file:line in Originofamonia/DFormer):
   ConvFFNFn     MLP.forward + Block residual/layer-scale/DropPath   DFormer.py:48-67, 173-179
   AttentionFn   Attention.forward + Block residuals                 DFormer.py:70-145, 168-179
 """
+import os
 import weakref
 
 import torch
@@ -177,8 +178,9 @@ def _cat1(*vs):
 
 # ====================================================================== ConvFFN (+ residual)
 # bf16 / fp16 ConvFFNs whose shape has fused kernels run dfm_convffn_fwd / _bwd (csrc/convffn.hip);
-# False routes every ConvFFN through the op-level chain below (tests compare the two)
-FUSED_FFN = False
+# False routes every ConvFFN through the op-level chain below (tests compare the two; DFM_FUSED_FFN=0|1
+# sets the default for A/B runs)
+FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
 
 
 class ConvFFNFn(torch.autograd.Function):
@@ -199,9 +201,9 @@ class ConvFFNFn(torch.autograd.Function):
         ctx.tag = K.TAG
         ctx.fused = FUSED_FFN and K.convffn_supported(dt, shape, C, w1.shape[0])
         if ctx.fused:  # one kernel: LN, fc1, DW3x3 + identity, GELU, fc2, residual; h is the saved hidden
-            out, f, h, mu, rs = K.convffn_fwd(x, shape, ln_w, ln_b, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
+            out, f, h, xn, mu, rs = K.convffn_fwd(x, shape, ln_w, ln_b, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
             ctx.shape = shape
-            ctx.save_for_backward(x, h, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls)
+            ctx.save_for_backward(x, h, xn, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls)
             return out
         xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
         ctx.shape = shape
@@ -219,7 +221,7 @@ class ConvFFNFn(torch.autograd.Function):
     def backward(ctx, dout):
         K.TAG = ctx.tag + ".bwd"
         if ctx.fused:
-            x, h, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
+            x, h, xn, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
             dt = x.dtype
             slots = [gslot(ln_w), gslot(ln_b), gslot2(w1), gslot(b1), gslot(wpos), gslot(bpos), gslot2(w2), gslot(b2),
                      gslot(ls)]
@@ -227,7 +229,7 @@ class ConvFFNFn(torch.autograd.Function):
                      zip(slots, [(-1,), (-1,), tuple(w1.shape), (-1,), (w1.shape[0], 9), (-1,), tuple(w2.shape), (-1,),
                                  (-1,)])]
             dx, dlnw, dlnb, dW1, db1, dwpos, dbpos, dW2, db2, dls = K.convffn_bwd(
-                dout.contiguous(), x, h, f, mu, rs, ctx.shape, ln_w, ln_b, wcast(dt, w1), wpos, bpos, wcast(dt, w2), ls,
+                dout.contiguous(), x, h, xn, f, mu, rs, ctx.shape, ln_w, ln_b, wcast(dt, w1), wpos, bpos, wcast(dt, w2), ls,
                 rowscale, grads=slots)
             return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
                     dls)

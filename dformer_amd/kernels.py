@@ -355,18 +355,19 @@ def convffn_fwd(x, shape, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale=N
     d = _ffn_desc(shape, C, R, eps)
     out, f = torch.empty_like(x), torch.empty_like(x)
     h = torch.empty(P, R, device=x.device, dtype=x.dtype)
+    xn = torch.empty_like(x)
     mean = torch.empty(P, device=x.device, dtype=torch.float32)
     rstd = torch.empty(P, device=x.device, dtype=torch.float32)
     check(lib.dfm_convffn_fwd(dtype_code(x), ctypes.byref(d), ptr(x), ptr(ln_w), ptr(ln_b), ptr(w1), ptr(b1),
                               ptr(wpos), ptr(bpos), ptr(w2), ptr(b2), ptr(ls), ptr(rowscale), ptr(out), ptr(f),
-                              ptr(h), ptr(mean), ptr(rstd), stream()), "dfm_convffn_fwd")
+                              ptr(h), ptr(xn), ptr(mean), ptr(rstd), stream()), "dfm_convffn_fwd")
     if ACCOUNT is not None:
         es = _es(x)
-        _acct(4.0 * P * C * R + 18.0 * P * R, es * P * (3 * C + R) + 8 * P + es * 2 * C * R)
-    return out, f, h, mean, rstd
+        _acct(4.0 * P * C * R + 18.0 * P * R, es * P * (4 * C + R) + 8 * P + es * 2 * C * R)
+    return out, f, h, xn, mean, rstd
 
 
-def convffn_bwd(dout, x, h, f, mean, rstd, shape, ln_w, ln_b, w1, wpos, bpos, w2, ls, rowscale=None, eps=1e-6,
+def convffn_bwd(dout, x, h, xn, f, mean, rstd, shape, ln_w, ln_b, w1, wpos, bpos, w2, ls, rowscale=None, eps=1e-6,
                 grads=None):
     """Backward of convffn_fwd. Returns (dx, dln_w, dln_b, dw1, db1, dwpos, dbpos, dw2, db2, dls); the
     parameter gradients go to the tensors of `grads` (same order, None = allocate; float32, overwritten)."""
@@ -381,13 +382,16 @@ def convffn_bwd(dout, x, h, f, mean, rstd, shape, ln_w, ln_b, w1, wpos, bpos, w2
     dx = torch.empty_like(x)
     nbytes = lib.dfm_convffn_bwd_workspace_size(code, ctypes.byref(d))
     ws = _ws(nbytes, dev)
-    check(lib.dfm_convffn_bwd(code, ctypes.byref(d), ptr(dout), ptr(x), ptr(h), ptr(f), ptr(mean), ptr(rstd),
+    check(lib.dfm_convffn_bwd(code, ctypes.byref(d), ptr(dout), ptr(x), ptr(h), ptr(xn), ptr(f), ptr(mean), ptr(rstd),
                               ptr(ln_w), ptr(ln_b), ptr(w1), ptr(wpos), ptr(bpos), ptr(w2), ptr(ls), ptr(rowscale),
                               ptr(dx), *[ptr(o) for o in outs], ptr(ws), nbytes, stream()), "dfm_convffn_bwd")
     if ACCOUNT is not None:
         es = _es(x)
         _acct_named([("residual", 0.0, 3.0 * es * P * C),
                      ("ffn_bwd", 6.0 * P * C * R + 36.0 * P * R, es * P * (2 * R + 2 * C) + 8 * P),
+                     ("ffn_dhpre", 4.0 * P * C * R + 18.0 * P * R, es * P * (2 * R + C)),
+                     ("dw3", 36.0 * P * R, es * P * 3 * R),
+                     ("gemm", 2.0 * P * C * R, es * (P * R + P * C + R * C)),
                      ("gemm", 2.0 * P * C * R, es * (P * R + P * C + R * C)),
                      ("ln_bwd", 0.0, es * P * C * 4 + 8 * P)])
     return (dx, *outs)

@@ -39,7 +39,8 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
+int dfm_abi_version(void); /* 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
+                              dfm_block_workspace_size); 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
                               second stages (dfm_partial_sum_group); 7: DfmGemmDesc.workspace_bytes + stride /
                               leading-dimension validation */
 
@@ -191,8 +192,9 @@ int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, 
  * DFormer.py:48-67 (MLP: LN -> fc1 -> DW3x3 + identity -> GELU -> fc2) inside Block's residual
  * (DFormer.py:176-179):  out = x + rowscale[p / (H*W)] * ls * f,
  *   f = fc2(GELU(DW3x3(h) + bpos + h)) + b2,  h = fc1(LN(x)) + b1.
- * x, out, f, dx, dout: [B*H*W][C] contiguous NHWC rows (dtype); h: [B*H*W][hidden] (dtype), written
- * by the forward for the backward (the only hidden-sized tensor either pass moves through HBM);
+ * x, out, f, xn, dx, dout: [B*H*W][C] contiguous NHWC rows (dtype); h: [B*H*W][hidden] (dtype), written
+ * by the forward for the backward (the only hidden-sized tensor the forward writes); xn = LN(x) (the
+ * fc1 weight gradient's operand; the forward writes it when xn is non-NULL, the backward requires it);
  * w1 [hidden][C], w2 [C][hidden] (dtype); ln_w, ln_b, b1, bpos, b2, ls: float32; wpos [hidden][9]
  * float32; rowscale float32 [B] (DropPath keep mask / keep probability) or NULL; mean / rstd float32
  * [B*H*W] (the LayerNorm statistics, written by the forward). dtype bf16 or f16 (float32 runs the
@@ -208,14 +210,77 @@ int dfm_convffn_supported(int dtype, const DfmConvFFNDesc* d);
 int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x, const float* ln_w, const float* ln_b,
                     const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
                     const float* b2, const float* ls, const float* rowscale, void* out, void* f, void* h,
-                    float* mean, float* rstd, dfm_stream_t stream);
+                    void* xn, float* mean, float* rstd, dfm_stream_t stream);
 size_t dfm_convffn_bwd_workspace_size(int dtype, const DfmConvFFNDesc* d);
 int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const void* x, const void* h,
-                    const void* f, const float* mean, const float* rstd, const float* ln_w, const float* ln_b,
+                    const void* xn, const void* f, const float* mean, const float* rstd, const float* ln_w,
+                    const float* ln_b,
                     const void* w1, const float* wpos, const float* bpos, const void* w2, const float* ls,
                     const float* rowscale, void* dx, float* dln_w, float* dln_b, float* dw1, float* db1,
                     float* dwpos, float* dbpos, float* dw2, float* db2, float* dls, void* workspace,
                     size_t workspace_bytes, dfm_stream_t stream);
+
+/* ---------------------------------------------------------------- encoder Block
+ * DFormer.py:147-181 Block.forward (x, x_e) -> (x + DropPath(ls1 * attn(x, x_e)) + DropPath(ls2 * mlp(.)),
+ * x_e likewise with ls1_e / mlp_e2 / ls2_e), forward and backward, every kernel enqueued on `stream`.
+ * x, y, dx, dy: [B*H*W][C]; xe, ye, dxe, dye: [B*H*W][C/2] (NHWC rows, dtype).
+ * params: DFM_BLOCK_NPARAM pointers indexed by the DFM_BP_* enum (the reference state_dict entries of
+ *   one Block, DFormer.py:70-181): the nn.Linear weights (the 11 names marked "dtype" below) are dtype
+ *   copies ([out][in] row-major), every other entry (LayerNorm affine, biases, depthwise [C][k][k]
+ *   weights, layer scales) float32. Entries the Block does not have are ignored (kv / short_cut_linear
+ *   without a window; proj_e, layer_scale_1_e / _2_e and mlp_e2 with drop_depth).
+ *   Contiguous q | q_cut | l (weights and biases, in that order) run as one GEMM, as the training step does.
+ * grads: the same indexing, float32 [same shape] (overwritten; NULL entries are not allowed for
+ *   parameters the Block has).
+ * rowscale: NULL, or 4 float32 [B] pointers (each may be NULL = 1): the per-sample DropPath scales
+ *   (keep mask / keep prob) of, in mmcv's call order, attn x, mlp x, attn x_e, mlp x_e.
+ * The forward writes `saved` (dfm_block_saved_size bytes) for the backward, which also reads x and
+ * xe again; both use `workspace` (dfm_block_workspace_size bytes) as scratch. With drop_depth, x_e
+ * passes through: ye is not written (may be NULL) and dye may be NULL (no gradient from above).
+ * fused_ffn: ConvFFNs with fused kernels (dfm_convffn_supported) run dfm_convffn_fwd / _bwd. */
+typedef struct DfmBlockDesc {
+  int B, H, W, C;
+  int heads;      /* num_head */
+  int window;     /* 7: pooled-query attention (DFormer.py:90-96, 119-131); 0: none */
+  int hidden;     /* mlp hidden width = mlp_ratio * C (mlp_e2: hidden / 2) */
+  int drop_depth; /* last Block of the last stage: no proj_e / layer_scale_*_e / mlp_e2 */
+  int fused_ffn;
+  float ln_eps;   /* 1e-6 */
+} DfmBlockDesc;
+enum {
+  DFM_BP_NORM_W, DFM_BP_NORM_B, DFM_BP_NORM_E_W, DFM_BP_NORM_E_B, /* attn.norm, attn.norm_e */
+  DFM_BP_Q_W, DFM_BP_Q_B,               /* attn.q [C][C] (dtype) */
+  DFM_BP_QCUT_W, DFM_BP_QCUT_B,         /* attn.q_cut [C/2][C] (dtype) */
+  DFM_BP_L_W, DFM_BP_L_B,               /* attn.l [C][C] (dtype) */
+  DFM_BP_CONV_W, DFM_BP_CONV_B,         /* attn.conv [C][7][7] */
+  DFM_BP_A_W, DFM_BP_A_B,               /* attn.a [C][C] (dtype) */
+  DFM_BP_EFORE_W, DFM_BP_EFORE_B,       /* attn.e_fore [C/2][C/2] (dtype) */
+  DFM_BP_ECONV_W, DFM_BP_ECONV_B,       /* attn.e_conv [C/2][7][7] */
+  DFM_BP_EBACK_W, DFM_BP_EBACK_B,       /* attn.e_back [C/2][C/2] (dtype) */
+  DFM_BP_KV_W, DFM_BP_KV_B,             /* attn.kv [C][C] (dtype; window only) */
+  DFM_BP_SC_W, DFM_BP_SC_B,             /* attn.short_cut_linear [C/2][3C/2] (dtype; window only) */
+  DFM_BP_PROJ_W, DFM_BP_PROJ_B,         /* attn.proj [C][fw] (dtype), fw = 2C with a window, 3C/2 without */
+  DFM_BP_PROJE_W, DFM_BP_PROJE_B,       /* attn.proj_e [C/2][fw] (dtype) */
+  DFM_BP_LS1, DFM_BP_LS1E, DFM_BP_LS2, DFM_BP_LS2E, /* layer_scale_1, _1_e, _2, _2_e */
+  DFM_BP_MLP_NORM_W, DFM_BP_MLP_NORM_B, /* mlp.norm */
+  DFM_BP_MLP_FC1_W, DFM_BP_MLP_FC1_B,   /* mlp.fc1 [hidden][C] (dtype) */
+  DFM_BP_MLP_POS_W, DFM_BP_MLP_POS_B,   /* mlp.pos [hidden][3][3] */
+  DFM_BP_MLP_FC2_W, DFM_BP_MLP_FC2_B,   /* mlp.fc2 [C][hidden] (dtype) */
+  DFM_BP_MLPE_NORM_W, DFM_BP_MLPE_NORM_B, /* mlp_e2.*, C/2 and hidden/2 */
+  DFM_BP_MLPE_FC1_W, DFM_BP_MLPE_FC1_B,
+  DFM_BP_MLPE_POS_W, DFM_BP_MLPE_POS_B,
+  DFM_BP_MLPE_FC2_W, DFM_BP_MLPE_FC2_B,
+  DFM_BLOCK_NPARAM
+};
+size_t dfm_block_saved_size(int dtype, const DfmBlockDesc* d);
+size_t dfm_block_workspace_size(int dtype, const DfmBlockDesc* d);
+int dfm_block_fwd(int dtype, const DfmBlockDesc* d, const void* const* params, const float* const* rowscale,
+                  const void* x, const void* xe, void* y, void* ye, void* saved, size_t saved_bytes, void* workspace,
+                  size_t workspace_bytes, dfm_stream_t stream);
+int dfm_block_bwd(int dtype, const DfmBlockDesc* d, const void* const* params, const float* const* rowscale,
+                  const void* x, const void* xe, const void* saved, size_t saved_bytes, const void* dy,
+                  const void* dye, void* dx, void* dxe, float* const* grads, void* workspace, size_t workspace_bytes,
+                  dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- reductions / elementwise */
 /* out[c] (+= when accumulate) = sum_rows x[r,c] * (mul ? mul[r,c] : 1) * (rowscale ? rowscale[r/rps] : 1)

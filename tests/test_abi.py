@@ -42,7 +42,7 @@ def test_binding_signatures_match_header():
 
 def test_abi_version_and_error_path():
     from dformer_amd import _lib
-    assert _lib.lib.dfm_abi_version() == 10
+    assert _lib.lib.dfm_abi_version() == 11
     # argument validation fails before touching the GPU
     st = _lib.lib.dfm_layernorm_fwd(0, 10, 100000, None, 0, None, None, 1e-6, None, 0, None, None, None)
     assert st == -1
@@ -51,23 +51,66 @@ def test_abi_version_and_error_path():
         _lib.check(st, "dfm_layernorm_fwd")
 
 
-def test_gemm_desc_layout_matches_c_struct(tmp_path):
-    """ctypes GemmDesc must have the C struct's size and every field offset (checked with gcc)."""
+@pytest.mark.parametrize("cname,pyname", [("DfmGemmDesc", "GemmDesc"), ("DfmPartialSum", "PartialSum"),
+                                          ("DfmConvFFNDesc", "ConvFFNDesc"), ("DfmBlockDesc", "BlockDesc")])
+def test_desc_layout_matches_c_struct(tmp_path, cname, pyname):
+    """Each ctypes descriptor must have the C struct's size and every field offset (checked with gcc)."""
     import shutil
     import subprocess
     from dformer_amd import _lib
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
-    names = [f[0] for f in _lib.GemmDesc._fields_]
-    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"%s\"\nint main(){printf(\"%%zu\", sizeof(DfmGemmDesc));" % HEADER
+    cls = getattr(_lib, pyname)
+    names = [f[0] for f in cls._fields_]
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"%s\"\nint main(){printf(\"%%zu\", sizeof(%s));" % (
+        HEADER, cname)
     for n in names:
-        src += 'printf(" %%zu", offsetof(DfmGemmDesc, %s));' % n
+        src += 'printf(" %%zu", offsetof(%s, %s));' % (cname, n)
     src += "return 0;}\n"
     (tmp_path / "t.c").write_text(src)
     subprocess.run(["gcc", str(tmp_path / "t.c"), "-o", str(tmp_path / "t")], check=True)
     vals = [int(v) for v in subprocess.run([str(tmp_path / "t")], capture_output=True, text=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(_lib.GemmDesc)
-    assert vals[1:] == [getattr(_lib.GemmDesc, n).offset for n in names]
+    assert vals[0] == ctypes.sizeof(cls)
+    assert vals[1:] == [getattr(cls, n).offset for n in names]
+
+
+def test_block_param_enum_matches_names(tmp_path):
+    """BLOCK_PARAM_NAMES follows the header's DFM_BP_* enum: same count, and the enum names spell the
+    reference state_dict keys in the same order."""
+    import shutil
+    import subprocess
+    from dformer_amd import _lib
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = open(HEADER).read()
+    start = src.index("enum {", src.index("} DfmBlockDesc;"))
+    body = src[start:src.index("DFM_BLOCK_NPARAM", start)]
+    enum = re.findall(r"DFM_BP_\w+", re.sub(r"/\*.*?\*/", "", body, flags=re.S))
+    assert len(enum) == len(_lib.BLOCK_PARAM_NAMES)
+    (tmp_path / "n.c").write_text("#include <stdio.h>\n#include \"%s\"\nint main(){printf(\"%%d\", DFM_BLOCK_NPARAM);"
+                                  "return 0;}\n" % HEADER)
+    subprocess.run(["gcc", str(tmp_path / "n.c"), "-o", str(tmp_path / "n")], check=True)
+    assert int(subprocess.run([str(tmp_path / "n")], capture_output=True, text=True).stdout) == len(enum)
+    short = {"attn.norm.weight": "NORM_W", "attn.norm_e.bias": "NORM_E_B", "attn.short_cut_linear.weight": "SC_W",
+             "attn.proj_e.bias": "PROJE_B", "layer_scale_1_e": "LS1E", "mlp.pos.weight": "MLP_POS_W",
+             "mlp_e2.fc2.bias": "MLPE_FC2_B"}
+    for name, tag in short.items():
+        assert enum[_lib.BLOCK_PARAM_NAMES.index(name)] == "DFM_BP_" + tag, name
+
+
+def test_block_sizes_and_validation():
+    """dfm_block_*_size plan the Block on the host (no GPU); bad descriptors are rejected before any launch."""
+    from dformer_amd import _lib
+    d = _lib.BlockDesc(2, 30, 40, 256, 8, 7, 1024, 0, 0, 1e-6)
+    sv, ws = _lib.lib.dfm_block_saved_size(_lib.BF16, d), _lib.lib.dfm_block_workspace_size(_lib.BF16, d)
+    P = 2 * 30 * 40
+    assert sv > 2 * P * (256 + 1024 + 256) and ws > 0
+    assert _lib.lib.dfm_block_saved_size(_lib.F32, d) > sv
+    bad = _lib.BlockDesc(2, 30, 40, 250, 8, 7, 1024, 0, 0, 1e-6)
+    assert _lib.lib.dfm_block_saved_size(_lib.BF16, bad) == 0
+    fake = ctypes.c_void_p(1 << 20)
+    st = _lib.lib.dfm_block_fwd(_lib.BF16, d, fake, None, fake, fake, fake, fake, fake, 16, fake, 16, None)
+    assert st == -1 and b"needed" in _lib.lib.dfm_last_error()
 
 
 @pytest.mark.parametrize("bad", [

@@ -88,8 +88,8 @@ def bench_stage(st, branch="mlp"):
         rows += [
             ("FUSED fwd", lambda: K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs),
              P * (3 * C + hid) * E),
-            ("FUSED bwd", lambda: K.convffn_bwd(dout, x, fo[2], fo[1], fo[3], fo[4], (B, H, W), lnw, lnb, w1, wpos,
-                                                bpos, w2, ls, rs),
+            ("FUSED bwd", lambda: K.convffn_bwd(dout, x, fo[2], fo[3], fo[1], fo[4], fo[5], (B, H, W), lnw, lnb, w1,
+                                                wpos, bpos, w2, ls, rs),
              P * (3 * C + 2 * C + 3 * hid + 5 * C) * E),
         ]
     res = []

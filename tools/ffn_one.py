@@ -34,8 +34,8 @@ def main():
     ls, rs = torch.rand(C, device=dev), torch.rand(B, device=dev)
     dout = torch.randn(P, C, device=dev).to(bf)
     for _ in range(it):
-        out, f, h, mu, rstd = K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs)
-        K.convffn_bwd(dout, x, h, f, mu, rstd, (B, H, W), lnw, lnb, w1, wpos, bpos, w2, ls, rs)
+        out, f, h, xn, mu, rstd = K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs)
+        K.convffn_bwd(dout, x, h, xn, f, mu, rstd, (B, H, W), lnw, lnb, w1, wpos, bpos, w2, ls, rs)
     torch.cuda.synchronize()
     print("ok", st, br, it)
 

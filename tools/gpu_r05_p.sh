@@ -1,9 +1,9 @@
-# round 5: fused ConvFFN parity + timing + backward variant breakdown
+# round 5: fused ConvFFN parity + per-stage timing + PMC passes over the stage-0 fused kernels
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
-T=${1:-r05k}
+T=${1:-r05p}
 timeout -k 10 300 python -u -m pytest tests/test_convffn_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/${T}_convffn.log 2>&1 || { tail -20 gpurun_out/${T}_convffn.log; exit 11; }
 tail -1 gpurun_out/${T}_convffn.log
 timeout -k 10 300 python -u tools/ffn_kernels_bench.py 0 1 2 > gpurun_out/${T}_ffn.log 2>&1 || exit 12
 grep -E "unfused" gpurun_out/${T}_ffn.log
-bash tools/gpu_r05_var.sh ${T}v || exit 13
+bash tools/ffn_pmc.sh ${T}pmc 0 mlp || exit 13
