@@ -64,9 +64,12 @@ extern "C" size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d) {
   if (n < 1 || n > GMAX || d == nullptr) return 0;
   int splits[GMAX];
   group_splits(n, d, splits);
-  size_t total = 0;
-  for (int q = 0; q < n; ++q) total += group_ws_bytes(&d[q], splits[q]);
-  return total;
+  size_t total = 0, one = 0;
+  for (int q = 0; q < n; ++q) {
+    total += group_ws_bytes(&d[q], splits[q]);
+    one = std::max(one, dfm_gemm_workspace_size(&d[q]));  // k-contiguous-A groups may run problems singly
+  }
+  return std::max(total, one);
 }
 
 extern "C" int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,

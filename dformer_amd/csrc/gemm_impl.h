@@ -766,8 +766,9 @@ template <int N>
 DFM_INLINE void wait_vm() { __builtin_amdgcn_s_waitcnt(vmcnt_imm(N)); }
 DFM_INLINE void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8)); }
 
-template <typename T, int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
-__global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
+// One block's work of the ring GEMM: logical block lid (XCD-renumbered) of problem a.
+template <typename T, int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS>
+DFM_INLINE void glds_block(const GemmArgs& a, int lid, char* smem) {
   constexpr int NT = 64 * NW;
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -781,14 +782,8 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
   static_assert(NS >= 2, "ring too shallow");
   (void)NT;
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
-
-  // XCD-aware renumbering (bijective for any grid size): blocks id and id + 8 share an XCD
-  const int nblk = gridDim.x, id = blockIdx.x;
-  const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
   const int tiles = a.tiles_m * a.tiles_n;
   const int tile = lid % tiles, zs = lid / tiles;
   const int bm = (a.n_fast ? tile / a.tiles_n : tile % a.tiles_m) * BM;
@@ -950,6 +945,27 @@ __global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
     __syncthreads();
   }
   gemm_epilogue<T, BM, BN, NW, WAVES_M>(a, acc, smem, bm, bn, b, split);
+}
+
+template <typename T, int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
+__global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_kernel(GemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // XCD-aware renumbering (bijective for any grid size): blocks id and id + 8 share an XCD
+  glds_block<T, BM, BN, NW, WAVES_M, AK, BKC, NS>(a, xcd_lid(blockIdx.x, gridDim.x), smem);
+}
+
+// Up to GMAX independent ring GEMMs (k-contiguous A: forwards and input gradients of one Block phase,
+// e.g. q | q_cut | l with e_fore) in ONE launch: problem q owns blocks [start[q], start[q+1]) as in
+// gemm_group_kernel, so the short k-loops of the stage-2 / 3 shapes share one ramp and one tail.
+template <typename T, int BM, int BN, int NW, int WAVES_M, bool AK, bool BKC, int NS, int MINB>
+__global__ __launch_bounds__(64 * NW, MINB) void gemm_glds_group_kernel(GemmGroup g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int q = group_problem(g, blockIdx.x);
+  const GemmArgs& a = g.p[q];
+  const int nblk = a.tiles_m * a.tiles_n * a.batch * a.splits;
+  const int local = blockIdx.x - g.start[q];
+  if (local >= nblk) return;  // padding up to the next multiple of 8
+  glds_block<T, BM, BN, NW, WAVES_M, AK, BKC, NS>(a, xcd_lid(local, nblk), smem);
 }
 
 template <typename T, int BM, int BN, int NW, int WM_, bool AK, bool BKC, int NS, int MINB>
@@ -1257,10 +1273,74 @@ int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* 
   return DFM_OK;
 }
 
+// k-contiguous-A problems whose operands suit the ring kernel (16-byte aligned, >= 2 whole k-slices)
+// go to gemm_glds_group_kernel, unsplit, in 64 x 64 tiles (the single-GEMM route's tile for these shapes)
+template <typename T, bool BKC>
+int group_launch_glds(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
+                      hipStream_t s) {
+  constexpr int BM = 64, BN = 64, NW = 4, WM_ = 2, NS = 2, MINB = 4;
+  using IA = GImg<BM, true>;
+  using IB = GImg<BN, BKC>;
+  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
+  const size_t lds = std::max((size_t)NS * (IA::BYTES + IB::BYTES), (size_t)RP * (BN + 4) * sizeof(float));
+  auto kern = gemm_glds_group_kernel<T, BM, BN, NW, WM_, true, BKC, NS, MINB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  GemmGroup g;
+  g.n = n;
+  g.start[0] = 0;
+  for (int q = 0; q < n; ++q) {
+    fill_args<T>(g.p[q], &d[q], A[q], B[q], C[q], nullptr, 1);
+    g.p[q].tiles_m = cdiv(d[q].M, BM);
+    g.p[q].tiles_n = cdiv(g.p[q].Nw, BN);
+    g.p[q].n_fast = d[q].M >= d[q].N;
+    const int nblk = g.p[q].tiles_m * g.p[q].tiles_n * g.p[q].batch;
+    g.start[q + 1] = g.start[q] + (nblk + 7) / 8 * 8;
+  }
+  DFM_LAUNCH(kern, dim3((unsigned)g.start[n]), dim3(64 * NW), lds, s, g);
+  DFM_LAUNCH_CHECK();
+  return DFM_OK;
+}
+
+template <typename T>
+bool glds_group_member(const DfmGemmDesc* d, const void* A, const void* B) {
+  if (sizeof(T) != 2 || !d->a_kcontig) return false;
+  GemmArgs a;
+  fill_args<T>(a, d, A, B, nullptr, nullptr, 1);
+  return a.ala && a.alb && d->K >= 2 * GBK && d->split_k <= 1 && !d->colsum;
+}
+
 template <typename T>
 int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
                      void* ws, hipStream_t s) {
   const bool ak = d[0].a_kcontig, bk = d[0].b_kcontig;
+  if (ak) {
+    // forwards / input gradients: the ring-kernel members as one grouped launch, the rest (short K,
+    // unaligned operands, fp32) one by one on their own single-GEMM route (sharing the workspace)
+    DfmGemmDesc gd[GMAX];
+    const void *ga[GMAX], *gb[GMAX];
+    void* gc[GMAX];
+    int m = 0;
+    for (int q = 0; q < n; ++q) {
+      if (glds_group_member<T>(&d[q], A[q], B[q])) {
+        gd[m] = d[q];
+        ga[m] = A[q], gb[m] = B[q], gc[m] = C[q];
+        ++m;
+        continue;
+      }
+      DfmGemmDesc one = d[q];
+      one.workspace_bytes = d[0].workspace_bytes;
+      if (int st = gemm_typed<T>(&one, A[q], B[q], C[q], ws, s)) return st;
+    }
+    if constexpr (sizeof(T) == 2) {
+      if (m == 1) return gemm_typed<T>(&gd[0], ga[0], gb[0], gc[0], ws, s);
+      if (m > 1) return bk ? group_launch_glds<T, true>(m, gd, ga, gb, gc, s) : group_launch_glds<T, false>(m, gd, ga, gb, gc, s);
+    }
+    return DFM_OK;
+  }
   if (ak && bk) return group_launch<T, true, true>(n, d, A, B, C, (char*)ws, s);
   if (ak) return group_launch<T, true, false>(n, d, A, B, C, (char*)ws, s);
   if (bk) return group_launch<T, false, true>(n, d, A, B, C, (char*)ws, s);

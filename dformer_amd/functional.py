@@ -299,19 +299,23 @@ class AttentionFn(torch.autograd.Function):
         bqcl = _cat1(bq, bqc, bl)
         qcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         lpre = torch.empty(P, C, device=dev, dtype=dt)
-        K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl)
-        e1 = K.linear(xen, wcast(dt, wef), bef)
+        e1 = torch.empty(P, Ch, device=dev, dtype=dt)
+        # independent GEMMs of one phase run as one grouped launch (K.gemm_many): q | q_cut | l with e_fore
+        K.gemm_many([lambda c: K.linear(xn, Wqcl, bqcl, act=3, preact=lpre, act_col0=C + Ch, out=qcl, collect=c),
+                     lambda c: K.linear(xen, wcast(dt, wef), bef, out=e1, collect=c)])
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         xep = torch.empty(P, Ch, device=dev, dtype=dt)
         # a = Linear_a(DW7(g)); f[:, :C] = q * a   (a kept for backward)
         apre = K.dwconv(g, shape, wconv, bconv, 7)
         e2 = K.dwconv(e1, shape, wec, bec, 7)
         a = torch.empty(P, C, device=dev, dtype=dt)
-        K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C])
+        kv = torch.empty(P, C, device=dev, dtype=dt) if window else None
+        # a with kv and e_back; depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
+        calls = [lambda c: K.linear(apre, wcast(dt, wa), ba, mul=q, preact=a, out=f[:, :C], collect=c),
+                 lambda c: K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:], collect=c)]
         if window:
-            kv = K.linear(g, wcast(dt, wkv), bkv)
-        # depth branch: xe' = e_back(DW7(e_fore(LN xe))); f[:, -Ch:] = cx * xe'
-        K.linear(e2, wcast(dt, web), beb, mul=cx, preact=xep, out=f[:, fw - Ch:])
+            calls.append(lambda c: K.linear(g, wcast(dt, wkv), bkv, out=kv, collect=c))
+        K.gemm_many(calls)
         saved_attn = ()
         if window:
             dh = C // heads // 2
@@ -324,13 +328,17 @@ class AttentionFn(torch.autograd.Function):
             saved_attn = (kv, pooled, m, o, lse)
         # projections with the Block's residual / layer-scale / DropPath epilogue
         p1 = torch.empty(P, C, device=dev, dtype=dt)
-        x1 = K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale, rows_per_scale=rps)
+        x1 = torch.empty(P, C, device=dev, dtype=dt)
+        calls = [lambda c: K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale,
+                                    rows_per_scale=rps, out=x1, collect=c)]
         if drop_depth:
             xe1, p1e = xe, None
         else:
             p1e = torch.empty(P, Ch, device=dev, dtype=dt)
-            xe1 = K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e, rowscale=rowscale_e,
-                           rows_per_scale=rps)
+            xe1 = torch.empty(P, Ch, device=dev, dtype=dt)
+            calls.append(lambda c: K.linear(f, wcast(dt, wpe), bpe, preact=p1e, res=xe, colscale=ls1e,
+                                            rowscale=rowscale_e, rows_per_scale=rps, out=xe1, collect=c))
+        K.gemm_many(calls)  # proj with proj_e
         ctx.shape, ctx.heads, ctx.window, ctx.drop_depth = shape, heads, window, drop_depth
         ctx.n_attn = len(saved_attn)
         ctx.save_for_backward(x, xe, xn, mu1, rs1, xen, mu2, rs2, qcl, lpre, apre, a, e1, e2, xep, f, p1,
@@ -431,13 +439,17 @@ class AttentionFn(torch.autograd.Function):
         if window:
             dxn, dpooled, dkv = pooled_branch()
             dpooled_e = dpooled[:, C:]
-            K.linear_dgrad(dkv, wcast(dt, wkv), out=dg)
         # q * a
         dqa = df[:, :C]
         _, da = K.dual_mul(dqa, a, q, out1=dq)
         ow, ob = gslot2(wa), gslot(ba)
         grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=ow, bias_grad=True, bias_out=ob)
-        dapre = K.linear_dgrad(da, wcast(dt, wa))
+        dapre = torch.empty(P, C, device=dev, dtype=dt)
+        # the a and kv input gradients as one grouped launch
+        calls = [lambda c: K.linear_dgrad(da, wcast(dt, wa), out=dapre, collect=c)]
+        if window:
+            calls.append(lambda c: K.linear_dgrad(dkv, wcast(dt, wkv), out=dg, collect=c))
+        K.gemm_many(calls)
         ow, ob = gslot(wconv), gslot(bconv)
         grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=ow, db=ob)
         K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))

@@ -5,6 +5,7 @@ All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose la
 Activations are float32 or bfloat16; statistics / params / param-grads are float32.
 """
 import ctypes
+import os
 
 import torch
 
@@ -179,9 +180,9 @@ def flush_wgrad(pending):
 def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
          ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
-         colsum_accumulate=False, mul_gelu_grad=False, defer=False):
+         colsum_accumulate=False, mul_gelu_grad=False, defer=False, collect=None):
     """One dfm_gemm launch. defer=True (weight gradients) inside `with wgrad_group():` queues it for
-    the block's grouped launch instead."""
+    the block's grouped launch instead; `collect` (a list, from gemm_many) receives it unlaunched."""
     dt = dtype_code(a)
     assert b.dtype == a.dtype, (a.dtype, b.dtype)
     c_f32 = int(out.dtype == torch.float32 and a.dtype != torch.float32)
@@ -200,6 +201,9 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None))
     byt += 4 * N * (bias is not None) + 4 * M * (colsum is not None)
     peak = "bf16" if a.dtype != torch.float32 else "f32"
+    if collect is not None:
+        collect.append((d, dt, a, b, out, 2.0 * M * N * K * nb, byt, peak))
+        return out
     if defer and _WG_PENDING is not None and a.is_cuda:
         # queued for the block's grouped launch; the tensors stay referenced until it is issued
         _WG_PENDING.append((d, dt, a, b, out, 2.0 * M * N * K * nb, byt, peak, colsum, bias))
@@ -213,8 +217,42 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     return out
 
 
+# DFM_FWD_GROUP=0 (A/B measurement only): gemm_many launches its GEMMs one by one
+_FWD_GROUP = os.environ.get("DFM_FWD_GROUP", "1") != "0"
+
+
+def gemm_many(calls):
+    """Run independent GEMMs (thunks that call linear / linear_dgrad with collect=lst) as ONE grouped
+    launch (dfm_gemm_group: k-contiguous A problems go to the LDS-DMA ring kernel's grouped variant);
+    a single call launches alone. The calls must not read each other's outputs."""
+    items = []
+    for c in calls:
+        c(items)
+    if len(items) == 1 or not _FWD_GROUP:
+        for d, dt, a, b, out, fl, by, peak in items:
+            ws = _ws(lib.dfm_gemm_workspace_size(d), a.device)
+            d.workspace_bytes = ws.numel() if ws is not None else 0
+            check(lib.dfm_gemm(dt, d, ptr(a), ptr(b), ptr(out), ptr(ws), stream()), "dfm_gemm")
+            if ACCOUNT is not None:
+                _acct(fl, by, peak)
+        return
+    for i in range(0, len(items), 8):
+        chunk = items[i:i + 8]
+        n = len(chunk)
+        descs = (_lib.GemmDesc * n)(*[c[0] for c in chunk])
+        pa = (ctypes.c_void_p * n)(*[c[2].data_ptr() for c in chunk])
+        pb = (ctypes.c_void_p * n)(*[c[3].data_ptr() for c in chunk])
+        pc = (ctypes.c_void_p * n)(*[c[4].data_ptr() for c in chunk])
+        ws = _ws(lib.dfm_gemm_group_workspace_size(n, descs), chunk[0][2].device)
+        descs[0].workspace_bytes = ws.numel() if ws is not None else 0
+        check(lib.dfm_gemm_group(chunk[0][1], n, descs, ctypes.cast(pa, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p),
+                                 ctypes.cast(pc, ctypes.c_void_p), ptr(ws), stream()), "dfm_gemm_group")
+        if ACCOUNT is not None:
+            _acct(sum(c[5] for c in chunk), sum(c[6] for c in chunk), chunk[0][7])
+
+
 def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=None, rowscale=None,
-           rows_per_scale=1, out=None, beta=0.0, act_col0=0):
+           rows_per_scale=1, out=None, beta=0.0, act_col0=0, collect=None):
     """y[M,N] = epi(x[M,K] @ w[N,K]^T)  (nn.Linear forward)."""
     M, K = x.shape
     N = w.shape[0]
@@ -223,10 +261,11 @@ def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=
     return gemm(x, w, M=M, N=N, K=K, a_kcontig=True, b_kcontig=True, lda=ld(x), ldb=ld(w), out=out, ldc=ld(out),
                 beta=beta, bias=bias, act=act, preact=preact, ldpre=ld(preact) if preact is not None else 0,
                 mul=mul, ldmul=ld(mul) if mul is not None else 0, res=res, ldres=ld(res) if res is not None else 0,
-                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0)
+                colscale=colscale, rowscale=rowscale, rows_per_scale=rows_per_scale, act_col0=act_col0,
+                collect=collect)
 
 
-def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None):
+def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None, collect=None):
     """dx[M,K] (+)= dy[M,N] @ w[N,K]   (times `mul` elementwise, or times gelu'(gelu_grad_of))."""
     M, N = dy.shape
     K = w.shape[1]
@@ -236,7 +275,7 @@ def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None)
         mul = gelu_grad_of
     return gemm(dy, w, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=ld(dy), ldb=ld(w), out=out, ldc=ld(out),
                 beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0,
-                mul_gelu_grad=gelu_grad_of is not None)
+                mul_gelu_grad=gelu_grad_of is not None, collect=collect)
 
 
 def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False, bias_out=None):

@@ -139,7 +139,7 @@ def test_block_capi_bf16_vs_autograd_path(name, fused):
     pairs += [(n, grads[n], p.grad) for n, p in blk.named_parameters() if p.grad is not None]
     bad = {}
     for n, a, b in pairs:
-        e = rel_err(a.float().cpu(), b.float().cpu().numpy())
+        e = rel_err(a.detach().float().cpu(), b.detach().float().cpu())
         if not np.isfinite(e) or e > 2e-2:
             bad[n] = e
     assert not bad, bad

@@ -74,12 +74,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sweep", default="gpurun_out/gemm_sweep_r02.json")
     ap.add_argument("--out", default="gpurun_out/gemm_blas.json")
+    ap.add_argument("--max-k", type=int, default=0, help="only shapes with K <= this (0: all)")
     args = ap.parse_args()
     rows = json.load(open(args.sweep))["rows"]
     out, tm, tb, td = [], 0.0, 0.0, 0.0
     for r in rows:
         d = r["desc"]
-        if d["batch"] > 1:
+        if d["batch"] > 1 or (args.max_k and d["K"] > args.max_k):
             continue
         t_mine, t_blas, em, eb = run(d)
         cnt = r["count"]

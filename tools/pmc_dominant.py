@@ -5,7 +5,10 @@ algorithmic bytes for the same launches -> profiles/<round>_dominant_pmc.json (r
   rocprofv3 --pmc FETCH_SIZE --kernel-include-regex <re> -d <fetch_dir> -- python3 bench.py --eager ...
   rocprofv3 --pmc WRITE_SIZE ...                       -d <write_dir> ...
   rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE ... -d <mfma_dir> ...
-  python tools/pmc_dominant.py <step_table.json> <fetch_dir> <write_dir> <mfma_dir> <out.json>
+  python tools/pmc_dominant.py <step_table.json> <fetch_dir> <write_dir> <mfma_dir> <out.json> [kernel substring]
+
+With a kernel substring the record is for the first census kernel whose name contains it instead of
+the dominant one (e.g. the 7x7 depthwise / MFMA attention kernels, tools/gpu_pmc_kernels.sh).
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; on gfx950 FETCH_SIZE counts wide
 streaming reads at half their bytes, MI355X_MICROARCH.md HBM section). MFMA busy = the per-SIMD
@@ -29,9 +32,13 @@ def counter_rows(d, counter, name):
 
 def main():
     table_path, fdir, wdir, mdir, out = sys.argv[1:6]
+    sub = sys.argv[6] if len(sys.argv) > 6 else None
     with open(table_path) as f:
         table = json.load(f)
-    name, row = next(iter(table["kernels"].items()))  # sorted by measured time: the dominant kernel
+    if sub:
+        name, row = next((k, r) for k, r in table["kernels"].items() if sub in k)
+    else:
+        name, row = next(iter(table["kernels"].items()))  # sorted by measured time: the dominant kernel
     algo = row["bytes"] / row["launches"]
     flops = row["flops"] / row["launches"]
     fetch = counter_rows(fdir, "FETCH_SIZE", name)
@@ -42,7 +49,10 @@ def main():
         raise SystemExit(f"no FETCH_SIZE / WRITE_SIZE rows for {name[:80]}")
     rd = 2 * sum(fetch) / len(fetch) * 1024
     wr = sum(write) / len(write) * 1024
+    ms = row["measured_ms"] / row["launches"]
     rec = {"kernel": name, "launches_profiled": [len(fetch), len(write), len(busy)],
+           "census_ms_per_launch": round(ms, 4),
+           "algorithmic_GBs": round(algo / ms / 1e6, 1), "algorithmic_frac_of_8TBs": round(algo / ms / 1e6 / 8000, 4),
            "census_launches_per_step": row["launches"],
            "algorithmic_bytes_per_launch": round(algo), "algorithmic_flops_per_launch": round(flops),
            "hbm_read_bytes_per_launch": round(rd), "hbm_write_bytes_per_launch": round(wr),
