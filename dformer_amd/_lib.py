@@ -96,7 +96,7 @@ _SIGS = {
                                c_int, P, P, P, P, P]),
     "dfm_partial_sum_group": (c_int, [c_int, P, P]),
     "dfm_convffn_supported": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)]),
-    "dfm_convffn_fwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 18),
+    "dfm_convffn_fwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 20),
     "dfm_convffn_bwd_workspace_size": (c_size_t, [c_int, ctypes.POINTER(ConvFFNDesc)]),
     "dfm_convffn_bwd": (c_int, [c_int, ctypes.POINTER(ConvFFNDesc)] + [P] * 26 + [c_size_t, P]),
     "dfm_block_saved_size": (c_size_t, [c_int, ctypes.POINTER(BlockDesc)]),

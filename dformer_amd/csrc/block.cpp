@@ -78,12 +78,45 @@ DfmGemmDesc gdesc() {
   return d;
 }
 
+// GEMMs issued while a Group is open are collected and launched together (dfm_gemm_group: the
+// independent forward / input-gradient GEMMs of one Block phase, as functional.AttentionFn does)
+struct GemmBatch {
+  int n = 0;
+  DfmGemmDesc d[8];
+  const void* A[8];
+  const void* B[8];
+  void* C[8];
+};
+thread_local GemmBatch* t_batch = nullptr;
+
 void gemm(Run& r, DfmGemmDesc d, const void* A, const void* B, void* C) {
+  if (t_batch && t_batch->n < 8) {
+    const int i = t_batch->n++;
+    t_batch->d[i] = d, t_batch->A[i] = A, t_batch->B[i] = B, t_batch->C[i] = C;
+    return;
+  }
   const size_t need = dfm_gemm_workspace_size(&d);
   void* ws = r.scr(need);
   d.workspace_bytes = (long)r.scratch_cap;
   if (r.live()) r.ok(dfm_gemm(r.dt, &d, A, B, C, ws, r.s));
 }
+
+struct Group {
+  Run& r;
+  GemmBatch b;
+  explicit Group(Run& run) : r(run) { t_batch = &b; }
+  ~Group() {
+    t_batch = nullptr;
+    if (b.n == 1) {
+      gemm(r, b.d[0], b.A[0], b.B[0], b.C[0]);
+      return;
+    }
+    if (b.n == 0) return;
+    void* ws = r.scr(dfm_gemm_group_workspace_size(b.n, b.d));
+    b.d[0].workspace_bytes = (long)r.scratch_cap;
+    if (r.live()) r.ok(dfm_gemm_group(r.dt, b.n, b.d, b.A, b.B, b.C, ws, r.s));
+  }
+};
 
 struct Epi {  // optional epilogue operands of a forward Linear (see DfmGemmDesc)
   int act = 0;
@@ -306,7 +339,7 @@ void ffn_fwd(Run& r, const Dims& m, bool fused, int C, int R, V x, const void* c
     DfmConvFFNDesc fd{m.sh.B, m.sh.H, m.sh.W, C, R, m.eps};
     if (r.live())
       r.ok(dfm_convffn_fwd(r.dt, &fd, x.p, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale, out.p, sv.f.p, sv.h.p,
-                           sv.xn.p, sv.mean, sv.rstd, r.s));
+                           sv.xn.p, sv.mean, sv.rstd, nullptr, nullptr, r.s));
     return;
   }
   ffn_chain_fwd(r, m.sh, C, R, m.eps, x, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale, out, sv);
@@ -346,15 +379,18 @@ void block_fwd(Run& r, const Dims& m, const BlockIO& io, V y, V ye) {
                    adjacent(p[DFM_BP_QCUT_B], (size_t)Ch * 4, p[DFM_BP_L_B]);
   Epi el;
   el.act = 3, el.preact = s.lpre;
-  if (one) {
-    el.act_col0 = C + Ch;
-    linear(r, s.xn, P, C, p[DFM_BP_Q_W], 2 * C + Ch, F(p, DFM_BP_Q_B), s.qcl, el);
-  } else {
-    linear(r, s.xn, P, C, p[DFM_BP_Q_W], C, F(p, DFM_BP_Q_B), s.qcl);
-    linear(r, s.xn, P, C, p[DFM_BP_QCUT_W], Ch, F(p, DFM_BP_QCUT_B), s.qcl.col(C));
-    linear(r, s.xn, P, C, p[DFM_BP_L_W], C, F(p, DFM_BP_L_B), s.qcl.col(C + Ch), el);
+  {
+    Group grp(r);  // q | q_cut | l with e_fore
+    if (one) {
+      el.act_col0 = C + Ch;
+      linear(r, s.xn, P, C, p[DFM_BP_Q_W], 2 * C + Ch, F(p, DFM_BP_Q_B), s.qcl, el);
+    } else {
+      linear(r, s.xn, P, C, p[DFM_BP_Q_W], C, F(p, DFM_BP_Q_B), s.qcl);
+      linear(r, s.xn, P, C, p[DFM_BP_QCUT_W], Ch, F(p, DFM_BP_QCUT_B), s.qcl.col(C));
+      linear(r, s.xn, P, C, p[DFM_BP_L_W], C, F(p, DFM_BP_L_B), s.qcl.col(C + Ch), el);
+    }
+    linear(r, s.xen, P, Ch, p[DFM_BP_EFORE_W], Ch, F(p, DFM_BP_EFORE_B), s.e1);
   }
-  linear(r, s.xen, P, Ch, p[DFM_BP_EFORE_W], Ch, F(p, DFM_BP_EFORE_B), s.e1);
   V q = s.qcl, cx = s.qcl.col(C), g = s.qcl.col(C + Ch);
   if (r.live())
     r.ok(dfm_dwconv_fwd(r.dt, m.sh.B, m.sh.H, m.sh.W, C, 7, g.p, g.ld, F(p, DFM_BP_CONV_W), F(p, DFM_BP_CONV_B), 0,
@@ -362,13 +398,16 @@ void block_fwd(Run& r, const Dims& m, const BlockIO& io, V y, V ye) {
   if (r.live())
     r.ok(dfm_dwconv_fwd(r.dt, m.sh.B, m.sh.H, m.sh.W, Ch, 7, s.e1.p, s.e1.ld, F(p, DFM_BP_ECONV_W),
                         F(p, DFM_BP_ECONV_B), 0, s.e2.p, s.e2.ld, nullptr, 0, r.s));
-  Epi ea;  // f[:, :C] = q * a(DW7(l)), a kept
-  ea.mul = q, ea.preact = s.a;
-  linear(r, s.apre, P, C, p[DFM_BP_A_W], C, F(p, DFM_BP_A_B), s.f, ea);
-  if (m.window) linear(r, g, P, C, p[DFM_BP_KV_W], C, F(p, DFM_BP_KV_B), s.kv);
-  Epi ee;  // f[:, fw - Ch:] = cx * e_back(DW7(e_fore(LN_e xe))), e_back's output kept
-  ee.mul = cx, ee.preact = s.xep;
-  linear(r, s.e2, P, Ch, p[DFM_BP_EBACK_W], Ch, F(p, DFM_BP_EBACK_B), s.f.col(fw - Ch), ee);
+  {
+    Group grp(r);  // a with e_back and kv
+    Epi ea;        // f[:, :C] = q * a(DW7(l)), a kept
+    ea.mul = q, ea.preact = s.a;
+    linear(r, s.apre, P, C, p[DFM_BP_A_W], C, F(p, DFM_BP_A_B), s.f, ea);
+    Epi ee;  // f[:, fw - Ch:] = cx * e_back(DW7(e_fore(LN_e xe))), e_back's output kept
+    ee.mul = cx, ee.preact = s.xep;
+    linear(r, s.e2, P, Ch, p[DFM_BP_EBACK_W], Ch, F(p, DFM_BP_EBACK_B), s.f.col(fw - Ch), ee);
+    if (m.window) linear(r, g, P, C, p[DFM_BP_KV_W], C, F(p, DFM_BP_KV_B), s.kv);
+  }
   if (m.window) {  // softmax(q_pool k^T) v over the 7 x 7 pooled queries, upsampled into f[:, C:C+Ch]
     const int B = m.sh.B;
     if (r.live())
@@ -383,13 +422,16 @@ void block_fwd(Run& r, const Dims& m, const BlockIO& io, V y, V ye) {
     if (r.live())
       r.ok(dfm_bilinear_fwd(r.dt, B, 7, 7, m.sh.H, m.sh.W, Ch, s.o.p, s.o.ld, s.f.col(C).p, s.f.ld, 0, r.s));
   }
-  Epi ep;
-  ep.preact = s.p1, ep.res = io.x, ep.colscale = F(p, DFM_BP_LS1), ep.rowscale = io.rs[0], ep.rps = rps;
-  linear(r, s.f, P, fw, p[DFM_BP_PROJ_W], C, F(p, DFM_BP_PROJ_B), s.x1, ep);
-  if (!m.drop_depth) {
-    Epi epe;
-    epe.preact = s.p1e, epe.res = io.xe, epe.colscale = F(p, DFM_BP_LS1E), epe.rowscale = io.rs[2], epe.rps = rps;
-    linear(r, s.f, P, fw, p[DFM_BP_PROJE_W], Ch, F(p, DFM_BP_PROJE_B), s.xe1, epe);
+  {
+    Group grp(r);  // proj with proj_e
+    Epi ep;
+    ep.preact = s.p1, ep.res = io.x, ep.colscale = F(p, DFM_BP_LS1), ep.rowscale = io.rs[0], ep.rps = rps;
+    linear(r, s.f, P, fw, p[DFM_BP_PROJ_W], C, F(p, DFM_BP_PROJ_B), s.x1, ep);
+    if (!m.drop_depth) {
+      Epi epe;
+      epe.preact = s.p1e, epe.res = io.xe, epe.colscale = F(p, DFM_BP_LS1E), epe.rowscale = io.rs[2], epe.rps = rps;
+      linear(r, s.f, P, fw, p[DFM_BP_PROJE_W], Ch, F(p, DFM_BP_PROJE_B), s.xe1, epe);
+    }
   }
   // the ConvFFNs with the Block's second residuals (DFormer.py:176-181)
   ffn_fwd(r, m, m.fused_ffn, C, m.R, s.x1, p, DFM_BP_MLP_NORM_W, F(p, DFM_BP_LS2), io.rs[1], y, s.ffn);
@@ -458,13 +500,14 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
   V dxen = r.temp(P, Ch);
   dgrad(r, de1, P, Ch, p[DFM_BP_EFORE_W], Ch, dxen);
   // pooled-query attention
-  V dg = r.temp(P, C), dxn = r.temp(P, C), dpooled;
+  V dg = r.temp(P, C), dxn = r.temp(P, C), dpooled, dkv;
   if (m.window) {
     const long B49 = (long)B * 49;
     V dout_o = r.temp(B49, Ch);
     if (r.live())
       r.ok(dfm_bilinear_bwd(r.dt, B, 7, 7, m.sh.H, m.sh.W, Ch, df.col(C).p, df.ld, dout_o.p, dout_o.ld, 0, r.s));
-    V dm = r.temp(B49, Ch), dkv = r.temp(P, C);
+    V dm = r.temp(B49, Ch);
+    dkv = r.temp(P, C);
     void* ws = r.scr(dfm_pooled_attn_workspace(B, m.heads, (int)(P / B), m.dhd));
     if (r.live())
       r.ok(dfm_pooled_attn_bwd(r.dt, B, m.heads, (int)(P / B), m.dhd, s.m.p, s.m.ld, s.kv.p, s.kv.col(Ch).p, s.kv.ld,
@@ -476,7 +519,6 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
     if (r.live())
       r.ok(dfm_adaptive_pool7_bwd(r.dt, B, m.sh.H, m.sh.W, C, dpooled.p, dpooled.ld, dxn.p, dxn.ld, 0, r.s));
     wgrad(r, dkv, P, C, g, C, gr[DFM_BP_KV_W], gr[DFM_BP_KV_B]);
-    dgrad(r, dkv, P, C, p[DFM_BP_KV_W], C, dg);
   }
   // q * a(DW7(l))
   V da = r.temp(P, C);
@@ -484,7 +526,11 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
     r.ok(dfm_dual_mul(r.dt, P, C, df.p, df.ld, s.a.p, s.a.ld, q.p, q.ld, dq.p, dq.ld, da.p, da.ld, r.s));
   wgrad(r, da, P, C, s.apre, C, gr[DFM_BP_A_W], gr[DFM_BP_A_B]);
   V dapre = r.temp(P, C);
-  dgrad(r, da, P, C, p[DFM_BP_A_W], C, dapre);
+  {
+    Group grp(r);  // the a and kv input gradients
+    dgrad(r, da, P, C, p[DFM_BP_A_W], C, dapre);
+    if (m.window) dgrad(r, dkv, P, C, p[DFM_BP_KV_W], C, dg);
+  }
   {
     void* ws = r.scr(dfm_dwconv_bwd_weight_workspace(B, m.sh.H, m.sh.W, C, 7));
     if (r.live())

@@ -94,6 +94,8 @@ struct FfnFwdArgs {
   void* f;
   void* h;   // [P][R] saved for the backward
   void* xn;  // [P][C] LN(x), or NULL
+  void* gout;   // [P][R] GELU(hpre), or NULL (with gdout: the op-level backward's saved operands)
+  void* gdout;  // [P][R] GELU'(hpre), or NULL
   float* mean;
   float* rstd;
 };
@@ -119,7 +121,7 @@ struct FwdGeom {
   static_assert(T % 16 == 0 && HC % 32 == 0 && C % 32 == 0, "tile geometry");
 };
 
-template <typename T, int C, int HC, int TH_, int TW_>
+template <typename T, int C, int HC, int TH_, int TW_, bool SAVEG>
 __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
   using G = FwdGeom<C, HC, TH_, TW_>;
   constexpr int TH = G::TH, TW = G::TW;
@@ -321,6 +323,8 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
 #pragma unroll
     for (int cb = 0; cb < G::CB2; ++cb) {
       const int p = 16 * cb + l15, py = p / TW, px = p % TW;
+      const long pix = ((long)b * H + y0 + py) * W + x0 + px;
+      const bool pin = y0 + py < H && x0 + px < W;
 #pragma unroll
       for (int ks = 0; ks < G::KS2; ++ks) {
         const int cc = 32 * ks + 8 * lq;
@@ -344,8 +348,23 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
           for (int j = 0; j < 8; ++j) hp[j] = fmaf(wv[j], hv[j], hp[j]);
         }
         float g[8];
+        if constexpr (SAVEG) {  // GELU and GELU' from one erf, both stored for the op-level backward
+          float gd[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = gelu_f(hp[j]);
+          for (int j = 0; j < 8; ++j) {
+            float cdf, pdf;
+            normal_cdf_pdf(hp[j], cdf, pdf);
+            g[j] = hp[j] * cdf;
+            gd[j] = fmaf(hp[j], pdf, cdf);
+          }
+          if (pin) {
+            st8<T>(static_cast<T*>(a.gout) + pix * R + c0 + cc, g);
+            st8<T>(static_cast<T*>(a.gdout) + pix * R + c0 + cc, gd);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[j] = gelu_f(hp[j]);
+        }
         const bf16x8_t gf = pack16x8<T>(g);
 #pragma unroll
         for (int r = 0; r < G::RB2; ++r) acc[cb][r] = mma16<T>(wb[r][ks], gf, acc[cb][r]);
@@ -691,10 +710,13 @@ template <typename T, int C, int TH, int TW>
 int ffn_fwd_launch_t(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
   using Cf = FfnCfg<C>;
   using G = FwdGeom<C, Cf::FHC, TH, TW>;
-  auto kern = ffn_fwd_kernel<T, C, Cf::FHC, TH, TW>;
+  auto kern = a.gout ? ffn_fwd_kernel<T, C, Cf::FHC, TH, TW, true> : ffn_fwd_kernel<T, C, Cf::FHC, TH, TW, false>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    (void)hipFuncSetAttribute((const void*)ffn_fwd_kernel<T, C, Cf::FHC, TH, TW, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    (void)hipFuncSetAttribute((const void*)ffn_fwd_kernel<T, C, Cf::FHC, TH, TW, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
     attr = true;
   }
   a.tiles_x = (int)cdiv(d->W, G::TW);
@@ -717,8 +739,9 @@ static bool ffn_fwd_small() {
 template <typename T, int C>
 int ffn_fwd_launch(const DfmConvFFNDesc* d, FfnFwdArgs a, hipStream_t s) {
   using Cf = FfnCfg<C>;
-  if constexpr (C <= 128) {
-    if (ffn_fwd_small()) return ffn_fwd_launch_t<T, C, (C == 32 ? 8 : 4), (C == 128 ? 4 : 8)>(d, a, s);
+  if constexpr (C <= 128) {  // (the 8 x 16 tile at C = 32 spills with the GELU outputs: 8 x 8 then)
+    if (ffn_fwd_small() || (C == 32 && a.gout))
+      return ffn_fwd_launch_t<T, C, (C == 32 ? 8 : 4), (C == 128 ? 4 : 8)>(d, a, s);
   }
   return ffn_fwd_launch_t<T, C, Cf::FTH, Cf::FTW>(d, a, s);
 }
@@ -864,11 +887,12 @@ extern "C" int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x
                                const float* ln_b, const void* w1, const float* b1, const float* wpos,
                                const float* bpos, const void* w2, const float* b2, const float* ls,
                                const float* rowscale, void* out, void* f, void* h, void* xn, float* mean,
-                               float* rstd, dfm_stream_t stream) {
+                               float* rstd, void* gelu_out, void* gelu_grad, dfm_stream_t stream) {
   DFM_CHECK_ARG(dfm_convffn_supported(dtype, d), "dfm_convffn_fwd: unsupported dtype %d / shape (C %d, hidden %d)",
                 dtype, d ? d->C : -1, d ? d->hidden : -1);
   DFM_CHECK_ARG(x && ln_w && ln_b && w1 && b1 && wpos && bpos && w2 && b2 && ls && out && f && h && mean && rstd,
                 "dfm_convffn_fwd: null argument");
+  DFM_CHECK_ARG(!gelu_out == !gelu_grad, "dfm_convffn_fwd: gelu_out and gelu_grad go together");
   FfnFwdArgs a{};
   a.B = d->B; a.H = d->H; a.W = d->W; a.R = d->hidden;
   a.eps = d->ln_eps;
@@ -876,6 +900,7 @@ extern "C" int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x
   a.x = x; a.lnw = ln_w; a.lnb = ln_b; a.w1 = w1; a.b1 = b1; a.wpos = wpos; a.bpos = bpos;
   a.w2 = w2; a.b2 = b2; a.ls = ls; a.rowscale = rowscale;
   a.out = out; a.f = f; a.h = h; a.xn = xn; a.mean = mean; a.rstd = rstd;
+  a.gout = gelu_out; a.gdout = gelu_grad;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DFM_BF16) {
     using T = bf16_t;

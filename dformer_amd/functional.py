@@ -29,7 +29,7 @@ def invalidate_weights():
 
 def register_shadow(p, shadow):
     """The fused optimizer keeps `shadow` (bf16 copy of p) up to date itself."""
-    _WCACHE[(id(p), shadow.dtype)] = (_EPOCH[0], shadow, (p.data_ptr(),))
+    _WCACHE[(id(p), shadow.dtype)] = (_EPOCH[0], shadow, (p.data_ptr(),), (weakref.ref(p),))
 
 
 def _adjacent_rows(ts):
@@ -57,7 +57,10 @@ def wcast(dtype, *params):
     key = tuple(id(p) for p in params) + (dtype,)
     ptrs = tuple(p.data_ptr() for p in params)
     hit = _WCACHE.get(key)
-    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
+    # valid while the same parameter objects are alive (a new tensor may reuse a freed one's id() and
+    # address) at the same addresses, in the same epoch
+    if (hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs and
+            all(r() is p for r, p in zip(hit[3], params))):
         return hit[1]
     w = None
     if len(params) > 1:
@@ -68,7 +71,7 @@ def wcast(dtype, *params):
             torch.cat([p.detach().reshape(p.shape[0], -1) for p in params], 0)
         src = src.contiguous()
         w = src if dtype == torch.float32 else K.cast(src, dtype)
-    _WCACHE[key] = (_EPOCH[0], w, ptrs)
+    _WCACHE[key] = (_EPOCH[0], w, ptrs, tuple(weakref.ref(p) for p in params))
     return w
 
 
@@ -168,19 +171,24 @@ def _cat1(*vs):
     key = tuple(id(v) for v in vs) + ("bias",)
     ptrs = tuple(v.data_ptr() for v in vs)
     hit = _WCACHE.get(key)
-    if hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs:
+    if (hit is not None and hit[0] == _EPOCH[0] and hit[2] == ptrs and
+            all(r() is v for r, v in zip(hit[3], vs))):
         return hit[1]
     out = _adjacent_rows([v.detach().view(-1, 1) for v in vs])
     out = out.view(-1) if out is not None else torch.cat([v.detach() for v in vs])
-    _WCACHE[key] = (_EPOCH[0], out, ptrs)
+    _WCACHE[key] = (_EPOCH[0], out, ptrs, tuple(weakref.ref(v) for v in vs))
     return out
 
 
 # ====================================================================== ConvFFN (+ residual)
-# bf16 / fp16 ConvFFNs whose shape has fused kernels run dfm_convffn_fwd / _bwd (csrc/convffn.hip);
-# False routes every ConvFFN through the op-level chain below (tests compare the two; DFM_FUSED_FFN=0|1
-# sets the default for A/B runs)
-FUSED_FFN = os.environ.get("DFM_FUSED_FFN", "0") == "1"
+# FUSED_FFN: True runs bf16 / fp16 ConvFFNs whose shape has fused kernels through dfm_convffn_fwd / _bwd
+# (csrc/convffn.hip); "fwd" runs only the forward fused (it also stores GELU(hpre) / GELU'(hpre)) and the
+# op-level backward; "auto" does that on planes of >= FUSED_FWD_MIN_PLANE pixels (stage 0 at 480 x 640,
+# where the fused forward wins: 431 vs 526 us at 512 hidden channels, 210 vs 229 at 256; it loses from
+# stage 1 on, tools/ffn_kernels_bench.py); False routes every ConvFFN through the op-level chain below
+# (tests compare them; DFM_FUSED_FFN=0|1|fwd|auto sets the default for A/B runs)
+FUSED_FWD_MIN_PLANE = 16384
+FUSED_FFN = {"0": False, "1": True}.get(os.environ.get("DFM_FUSED_FFN", "auto"), os.environ.get("DFM_FUSED_FFN", "auto"))
 
 
 class ConvFFNFn(torch.autograd.Function):
@@ -199,14 +207,21 @@ class ConvFFNFn(torch.autograd.Function):
         dt = x.dtype
         W1, W2 = wcast(dt, w1), wcast(dt, w2)
         ctx.tag = K.TAG
-        ctx.fused = FUSED_FFN and K.convffn_supported(dt, shape, C, w1.shape[0])
+        fused = bool(FUSED_FFN) and K.convffn_supported(dt, shape, C, w1.shape[0])
+        if FUSED_FFN == "auto":
+            fused = fused and shape[1] * shape[2] >= FUSED_FWD_MIN_PLANE
+        ctx.fused = fused and FUSED_FFN is True
+        ctx.shape = shape
         if ctx.fused:  # one kernel: LN, fc1, DW3x3 + identity, GELU, fc2, residual; h is the saved hidden
             out, f, h, xn, mu, rs = K.convffn_fwd(x, shape, ln_w, ln_b, W1, b1, wpos, bpos, W2, b2, ls, rowscale)
-            ctx.shape = shape
             ctx.save_for_backward(x, h, xn, f, mu, rs, rowscale, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls)
             return out
+        if fused:  # the fused forward also storing the op-level backward's operands
+            out, f, h, xn, mu, rs, g, gp = K.convffn_fwd(x, shape, ln_w, ln_b, W1, b1, wpos, bpos, W2, b2, ls,
+                                                         rowscale, save_gelu=True)
+            ctx.save_for_backward(x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls)
+            return out
         xn, mu, rs = K.layernorm(x, ln_w, ln_b, 1e-6)
-        ctx.shape = shape
         h = K.linear(xn, W1, b1)
         g = torch.empty_like(h)
         # the DW kernel writes GELU'(hpre) instead of hpre (GELU and its derivative share one erf):

@@ -386,9 +386,10 @@ def convffn_supported(dtype, shape, C, hidden):
     return bool(lib.dfm_convffn_supported(code, ctypes.byref(d)))
 
 
-def convffn_fwd(x, shape, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, eps=1e-6):
-    """Fused ConvFFN + Block residual (DFormer.py:48-67, 176-179). Returns (out, f, h, mean, rstd):
-    out = x + rowscale * ls * f, f = fc2 pre-residual output, h = fc1 output, LN statistics."""
+def convffn_fwd(x, shape, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale=None, eps=1e-6, save_gelu=False):
+    """Fused ConvFFN + Block residual (DFormer.py:48-67, 176-179). Returns (out, f, h, xn, mean, rstd)
+    (+ (g, gp) = GELU(hpre), GELU'(hpre) with save_gelu, the op-level backward's operands):
+    out = x + rowscale * ls * f, f = fc2 pre-residual output, h = fc1 output, LN output / statistics."""
     P, C = x.shape
     R = w1.shape[0]
     d = _ffn_desc(shape, C, R, eps)
@@ -397,12 +398,17 @@ def convffn_fwd(x, shape, ln_w, ln_b, w1, b1, wpos, bpos, w2, b2, ls, rowscale=N
     xn = torch.empty_like(x)
     mean = torch.empty(P, device=x.device, dtype=torch.float32)
     rstd = torch.empty(P, device=x.device, dtype=torch.float32)
+    g = gp = None
+    if save_gelu:
+        g, gp = torch.empty_like(h), torch.empty_like(h)
     check(lib.dfm_convffn_fwd(dtype_code(x), ctypes.byref(d), ptr(x), ptr(ln_w), ptr(ln_b), ptr(w1), ptr(b1),
                               ptr(wpos), ptr(bpos), ptr(w2), ptr(b2), ptr(ls), ptr(rowscale), ptr(out), ptr(f),
-                              ptr(h), ptr(xn), ptr(mean), ptr(rstd), stream()), "dfm_convffn_fwd")
+                              ptr(h), ptr(xn), ptr(mean), ptr(rstd), ptr(g), ptr(gp), stream()), "dfm_convffn_fwd")
     if ACCOUNT is not None:
         es = _es(x)
-        _acct(4.0 * P * C * R + 18.0 * P * R, es * P * (4 * C + R) + 8 * P + es * 2 * C * R)
+        _acct(4.0 * P * C * R + 18.0 * P * R, es * P * (4 * C + R * (3 if save_gelu else 1)) + 8 * P + es * 2 * C * R)
+    if save_gelu:
+        return out, f, h, xn, mean, rstd, g, gp
     return out, f, h, xn, mean, rstd
 
 

@@ -195,6 +195,8 @@ int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, 
  * x, out, f, xn, dx, dout: [B*H*W][C] contiguous NHWC rows (dtype); h: [B*H*W][hidden] (dtype), written
  * by the forward for the backward (the only hidden-sized tensor the forward writes); xn = LN(x) (the
  * fc1 weight gradient's operand; the forward writes it when xn is non-NULL, the backward requires it);
+ * gelu_out / gelu_grad ([B*H*W][hidden] dtype, both or neither): GELU(hpre) and GELU'(hpre) as well, the
+ * operands the op-level backward (fc2 weight gradient, GELU backward) reads;
  * w1 [hidden][C], w2 [C][hidden] (dtype); ln_w, ln_b, b1, bpos, b2, ls: float32; wpos [hidden][9]
  * float32; rowscale float32 [B] (DropPath keep mask / keep probability) or NULL; mean / rstd float32
  * [B*H*W] (the LayerNorm statistics, written by the forward). dtype bf16 or f16 (float32 runs the
@@ -210,7 +212,7 @@ int dfm_convffn_supported(int dtype, const DfmConvFFNDesc* d);
 int dfm_convffn_fwd(int dtype, const DfmConvFFNDesc* d, const void* x, const float* ln_w, const float* ln_b,
                     const void* w1, const float* b1, const float* wpos, const float* bpos, const void* w2,
                     const float* b2, const float* ls, const float* rowscale, void* out, void* f, void* h,
-                    void* xn, float* mean, float* rstd, dfm_stream_t stream);
+                    void* xn, float* mean, float* rstd, void* gelu_out, void* gelu_grad, dfm_stream_t stream);
 size_t dfm_convffn_bwd_workspace_size(int dtype, const DfmConvFFNDesc* d);
 int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const void* x, const void* h,
                     const void* xn, const void* f, const float* mean, const float* rstd, const float* ln_w,

@@ -63,6 +63,8 @@ def ref64(p, x, shape, rowscale):
 
 def run_fn(p, x, dout, shape, rowscale, fused):
     from dformer_amd import functional as Fn
+    # fresh parameter tensors can reuse a freed one's id() and address: drop the 16-bit weight cache
+    Fn.invalidate_weights()
     prm = {k: v.clone().requires_grad_(True) for k, v in p.items()}
     xr = x.clone().requires_grad_(True)
     old = Fn.FUSED_FFN
@@ -84,9 +86,12 @@ CASES = [  # B, H, W, C, hidden: DFormer-B stages (mlp and mlp_e2), Tiny / odd p
 ]
 
 
+@pytest.mark.parametrize("mode", [True, "fwd"])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES)
-def test_convffn_fused_vs_float64_and_unfused(dt, case):
+def test_convffn_fused_vs_float64_and_unfused(dt, case, mode):
+    """mode True: fused forward and backward; "fwd": the fused forward storing GELU / GELU' for the
+    op-level backward."""
     from dformer_amd import kernels as Kk
     B, H, W, C, R = case
     shape = (B, H, W)
@@ -96,7 +101,7 @@ def test_convffn_fused_vs_float64_and_unfused(dt, case):
     out64, x64, d64 = ref64(p, x, shape, rowscale)
     out64.backward(dout.double())
     ref_g = {k: v.grad for k, v in d64.items()}
-    fo, fdx, fg = run_fn(p, x, dout, shape, rowscale, True)
+    fo, fdx, fg = run_fn(p, x, dout, shape, rowscale, mode)
     uo, udx, ug = run_fn(p, x, dout, shape, rowscale, False)
     rows = [("out", fo, uo, out64), ("dx", fdx, udx, x64.grad)] + [(k, fg[k], ug[k], ref_g[k]) for k in p]
     floor = 4e-3 if dt == torch.bfloat16 else 1e-3
@@ -106,7 +111,7 @@ def test_convffn_fused_vs_float64_and_unfused(dt, case):
         report.append(f"{name} {ef:.2e}/{eu:.2e}")
         assert torch.isfinite(a).all(), name
         assert ef <= max(1.5 * eu, floor), (name, ef, eu, report)
-    print(case, dt, " ".join(report))
+    print(case, dt, mode, " ".join(report))
 
 
 @pytest.mark.parametrize("case", [(2, 60, 80, 64, 512), (2, 40, 48, 32, 256)])

@@ -91,6 +91,9 @@ def bench_stage(st, branch="mlp"):
             ("FUSED bwd", lambda: K.convffn_bwd(dout, x, fo[2], fo[3], fo[1], fo[4], fo[5], (B, H, W), lnw, lnb, w1,
                                                 wpos, bpos, w2, ls, rs),
              P * (3 * C + 2 * C + 3 * hid + 5 * C) * E),
+            ("FUSED fwd+g", lambda: K.convffn_fwd(x, (B, H, W), lnw, lnb, w1, b1, wpos, bpos, w2, b2, ls, rs,
+                                                  save_gelu=True),
+             P * (3 * C + 3 * hid) * E),
         ]
     res = []
     for name, fn, nb in rows:
@@ -123,7 +126,8 @@ def main():
             fus = {r["kernel"]: r["us"] for r in rr if r["kernel"].startswith("FUSED")}
             if fus:
                 print(f"s{st}.{br:6s} unfused fwd {sum(unf[:4]):7.1f} us bwd {sum(unf[4:]):7.1f} us | fused fwd "
-                      f"{fus['FUSED fwd']:7.1f} us bwd {fus['FUSED bwd']:7.1f} us")
+                      f"{fus['FUSED fwd']:7.1f} us bwd {fus['FUSED bwd']:7.1f} us | fused fwd+g "
+                      f"{fus['FUSED fwd+g']:7.1f} us")
     allr = [r for r in allr if not r["kernel"].startswith("FUSED")]
     tot = sum(r["us"] for r in allr)
     ideal = sum(r["bytes"] for r in allr) / HBM * 1e6
