@@ -161,8 +161,8 @@ def dominant_roofline(table, name, durations_ms):
     peak = MFMA_PEAK_TFS[r["peak"] or "bf16"]
     t_mfma, t_hbm = fl / (peak * 1e12), by / (HBM_PEAK_GBS * 1e9)
     traffic = None
-    for pmc in (os.path.join(HERE, "profiles", n) for n in ("r04_pmc_dominant.json", "r03_pmc_dominant.json",
-                                                             "r02_dominant_pmc.json")):
+    for pmc in (os.path.join(HERE, "profiles", n) for n in ("r05_pmc_dominant.json", "r04_pmc_dominant.json",
+                                                             "r03_pmc_dominant.json", "r02_dominant_pmc.json")):
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)

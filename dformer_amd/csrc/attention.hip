@@ -621,6 +621,19 @@ DFM_INLINE bf16x8_t frag_tr(const bf16_t* lds, int LD, int r0, int k0, int lane)
 DFM_INLINE void lds_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 #define MFMA16(A, B, C) mma16<T>((A), (B), (C))
 
+// Block -> (image, head, chunk group). Heads run fastest in the logical order and the logical order
+// is dealt to the XCDs in contiguous runs (blocks p and p + 8 share an XCD): the heads of one image
+// whose K / V column slices share 128-byte lines (DH = 32: two heads per line) are read by blocks of
+// the same XCD at the same time, so each line comes from HBM once instead of once per head.
+DFM_INLINE void attn_block(int heads, int groups, int& bh, int& cg) {
+  const int nblk = gridDim.x, id = blockIdx.x;
+  const int xcd = id & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+  const int h = L % heads, t = L / heads;
+  cg = t % groups;
+  bh = (t / groups) * heads + h;
+}
+
 // Forward: S^T = K Q^T (keys as rows), online softmax per query, O^T += V^T P^T.
 // Partials per wave (chunk): unnormalised O [49][DH], running max m and sum l (scaled units).
 template <typename T, int DH>
@@ -629,7 +642,9 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
   __shared__ __attribute__((aligned(16))) bf16_t sV[4][32 * LDV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int bh = blockIdx.x / groups, chunk = (blockIdx.x % groups) * 4 + w;
+  int bh, cg;
+  attn_block(a.heads, groups, bh, cg);
+  const int chunk = cg * 4 + w;
   if (chunk >= a.nchunk) return;
   const int h = bh % a.heads, b = bh / a.heads;
   const int n0 = chunk * kpw, n1 = min(a.N, n0 + kpw);
@@ -771,7 +786,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma_kernel(AttnArgs a, int kpw,
   __shared__ float sL[64], sD[64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int bh = blockIdx.x / groups, chunk = (blockIdx.x % groups) * 4 + w;
+  int bh, cg;
+  attn_block(a.heads, groups, bh, cg);
+  const int chunk = cg * 4 + w;
   const int h = bh % a.heads, b = bh / a.heads;
   const bf16_t* Q = (const bf16_t*)a.q + (long)b * NQ * a.ldq + h * DH;
   const bf16_t* GO = (const bf16_t*)a.dout + (long)b * NQ * a.lddo + h * DH;

@@ -442,7 +442,7 @@ static_assert((W7L_NG * W7L_IW) % 8 == 4, "LDS pitch");
 
 template <typename T>
 __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
-                                                            const T* __restrict__ x, long ldx,
+                                                            int nsb, int slabs, const T* __restrict__ x, long ldx,
                                                             const T* __restrict__ dy, long lddy,
                                                             float* __restrict__ part) {
   constexpr int CPT = DwCfg<T>::CPT, CP = CPT / 2, NG = W7L_NG, TH = W7L_TH, TW = W7L_TW, NP = W7L_NP;
@@ -451,7 +451,12 @@ __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W,
   __shared__ uint4 xs[IH * IW * NG];
   __shared__ uint4 ds[ND];
   const int ncv = C / CPT;
-  const int cv0 = blockIdx.y * NG;  // first channel vector of the slab
+  // (spatial lane sb, channel slab): slabs fastest in an order dealt to the XCDs in contiguous runs, so
+  // the slabs that read the 64-byte halves of one 128-byte pixel line, and the spatial lanes that share
+  // tile halos, run on one XCD at the same time (their re-reads hit its L2)
+  const int lid = (int)xcd_remap(blockIdx.x, (long)nsb * slabs);
+  const int sb = lid / slabs;
+  const int cv0 = (lid % slabs) * NG;  // first channel vector of the slab
   const long ntiles = (long)B * tiles_h * tiles_w;
   const int t = threadIdx.x;
   const int g = t % NG, i = (t / NG) % 7, prt = t / (NG * 7);
@@ -464,7 +469,7 @@ __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W,
 #pragma unroll
   for (int e = 0; e < CP; ++e) bs[e] = f2v{0.f, 0.f};
 
-  for (long tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (long tile = sb; tile < ntiles; tile += nsb) {
     const int tw = (int)(tile % tiles_w), th = (int)((tile / tiles_w) % tiles_h);
     const long b = tile / ((long)tiles_w * tiles_h);
     const int h0 = th * TH, w0 = tw * TW;
@@ -565,7 +570,7 @@ __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W,
     bred[t * CPT + 2 * e + 1] = bs[e].y;
   }
   __syncthreads();
-  const long pbase = (long)blockIdx.x * C * 50;
+  const long pbase = (long)sb * C * 50;
   if (active && prt == 0 && cv0 + g < ncv) {
 #pragma unroll
     for (int e = 0; e < CP; ++e) {
@@ -602,8 +607,8 @@ long w7l_launch(int B, int H, int W, int C, const void* x, long ldx, const void*
                 hipStream_t s) {
   const long nsb = w7l_nsb<T>(B, H, W, C);
   const unsigned slabs = cdiv(C / DwCfg<T>::CPT, W7L_NG);
-  DFM_LAUNCH(dw7_lds_wgrad_kernel<T>, dim3((unsigned)nsb, slabs), dim3(256), 0, s, B, H, W, C, cdiv(H, W7L_TH),
-             cdiv(W, W7L_TW), (const T*)x, ldx, (const T*)dy, lddy, part);
+  DFM_LAUNCH(dw7_lds_wgrad_kernel<T>, dim3((unsigned)(nsb * slabs)), dim3(256), 0, s, B, H, W, C, cdiv(H, W7L_TH),
+             cdiv(W, W7L_TW), (int)nsb, (int)slabs, (const T*)x, ldx, (const T*)dy, lddy, part);
   return nsb;
 }
 
