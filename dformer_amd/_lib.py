@@ -37,7 +37,7 @@ class GemmDesc(ctypes.Structure):
 class PartialSum(ctypes.Structure):
     """DfmPartialSum: a deferred reduction second stage (dfm_partial_sum_group)."""
     _fields_ = [("part", P), ("out0", P), ("out1", P), ("n", c_long), ("n0", c_long), ("nblk", c_int),
-                ("layout", c_int), ("accumulate", c_int), ("ncol", c_long)]
+                ("layout", c_int), ("accumulate", c_int)]
 
 
 class ConvFFNDesc(ctypes.Structure):
@@ -79,7 +79,6 @@ _SIGS = {
     "dfm_gemm": (c_int, [c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
     "dfm_gemm_group_workspace_size": (c_size_t, [c_int, ctypes.POINTER(GemmDesc)]),
     "dfm_gemm_group": (c_int, [c_int, c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
-    "dfm_gemm_group_deferred": (c_int, [c_int, c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P, P, P]),
     "dfm_layernorm_fwd": (c_int, [c_int, c_long, c_int, P, c_long, P, P, c_float, P, c_long, P, P, P]),
     "dfm_layernorm_bwd_workspace": (c_size_t, [c_long, c_int]),
     "dfm_layernorm_bwd": (c_int, [c_int, c_long, c_int, P, c_long, P, c_long, P, P, P, P, c_long, P, c_long, c_int,

@@ -306,7 +306,7 @@ static inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b)
 static inline int second_stage(int layout, int nblk, long n, const float* part, float* out0, float* out1, long n0,
                                int accumulate, DfmPartialSum* defer, hipStream_t s) {
   if (defer) {
-    *defer = DfmPartialSum{part, out0, out1, n, n0, nblk, layout, accumulate, 0};
+    *defer = DfmPartialSum{part, out0, out1, n, n0, nblk, layout, accumulate};
     return DFM_OK;
   }
   const dim3 grid(cdiv(n, 64));

@@ -703,7 +703,7 @@ extern "C" int dfm_pack_slices(int dtype_out, int n, const void* const* srcs, co
 // ---- deferred second stages of up to PSG_MAX reductions in one launch: block b belongs to the sum q
 // with blk0[q] <= b < blk0[q + 1] and reduces its 64 columns exactly as partial_sum_kernel does
 // (16 row-lanes in block order, then the 16 lanes in order), so the results are bit-identical.
-constexpr int PSG_MAX = 32;
+constexpr int PSG_MAX = 16;
 struct PsGroup {
   DfmPartialSum p[PSG_MAX];
   int blk0[PSG_MAX + 1];
@@ -727,12 +727,9 @@ __global__ __launch_bounds__(1024) void partial_sum_group_kernel(PsGroup g) {
     float* dst;
     if (ps.layout == 0) dst = ps.out0 + e;
     else if (ps.layout == 1) dst = e < ps.n0 ? ps.out0 + e : ps.out1 + (e - ps.n0);
-    else if (ps.layout == 2) {
+    else {
       const long c = e / ps.n0, i = e % ps.n0;
       dst = i < ps.n0 - 1 ? ps.out0 + c * (ps.n0 - 1) + i : (ps.out1 ? ps.out1 + c : nullptr);
-    } else {  // split-K GEMM combine: padded rows of n0 columns
-      const long m = e / ps.n0, j = e % ps.n0;
-      dst = j < ps.ncol ? ps.out0 + m * ps.ncol + j : (j == ps.ncol && ps.out1 ? ps.out1 + m : nullptr);
     }
     if (dst) *dst = ps.accumulate ? *dst + v : v;
   }
@@ -752,9 +749,8 @@ extern "C" int dfm_partial_sum_group(int n, const DfmPartialSum* sums, dfm_strea
   for (int i = 0; i < n; ++i) {
     const DfmPartialSum& p = sums[i];
     if (p.n == 0) continue;  // an entry point that returned before its first stage
-    DFM_CHECK_ARG(p.n > 0 && p.nblk >= 0 && p.part && p.out0 && p.layout >= 0 && p.layout <= 3 &&
-                      (p.layout != 1 || (p.out1 && p.n0 > 0 && p.n0 < p.n)) && (p.layout != 2 || p.n0 >= 2) &&
-                      (p.layout != 3 || (p.n0 > 0 && p.ncol > 0 && p.ncol <= p.n0 && p.n % p.n0 == 0)),
+    DFM_CHECK_ARG(p.n > 0 && p.nblk >= 0 && p.part && p.out0 && p.layout >= 0 && p.layout <= 2 &&
+                      (p.layout != 1 || (p.out1 && p.n0 > 0 && p.n0 < p.n)) && (p.layout != 2 || p.n0 >= 2),
                   "dfm_partial_sum_group: malformed sum %d", i);
     if (g.count == PSG_MAX) {
       const int r = issue();

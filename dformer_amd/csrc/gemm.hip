@@ -72,8 +72,8 @@ extern "C" size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d) {
   return std::max(total, one);
 }
 
-static int gemm_group_any(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
-                          void* const* C, void* ws, dfm_stream_t stream, DfmPartialSum* defer, int* ndefer) {
+extern "C" int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
+                              void* const* C, void* ws, dfm_stream_t stream) {
   DFM_CHECK_ARG(d && A && B && C && n >= 1 && n <= GMAX, "dfm_gemm_group: 1 <= n <= %d problems", GMAX);
   for (int q = 0; q < n; ++q) {
     DFM_CHECK_ARG(A[q] && B[q] && C[q], "dfm_gemm_group: null operand (problem %d)", q);
@@ -86,22 +86,9 @@ static int gemm_group_any(int dtype, int n, const DfmGemmDesc* d, const void* co
   DFM_CHECK_ARG(need == 0 || (ws != nullptr && (size_t)d[0].workspace_bytes >= need),
                 "dfm_gemm_group: workspace of %ld bytes, %zu needed", d[0].workspace_bytes, need);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == DFM_BF16) return dfm_gemm_group_bf16(n, d, A, B, C, ws, s, defer, ndefer);
-  if (dtype == DFM_F16) return dfm_gemm_group_f16(n, d, A, B, C, ws, s, defer, ndefer);
-  if (dtype == DFM_F32) return dfm_gemm_group_f32(n, d, A, B, C, ws, s, defer, ndefer);
+  if (dtype == DFM_BF16) return dfm_gemm_group_bf16(n, d, A, B, C, ws, s);
+  if (dtype == DFM_F16) return dfm_gemm_group_f16(n, d, A, B, C, ws, s);
+  if (dtype == DFM_F32) return dfm_gemm_group_f32(n, d, A, B, C, ws, s);
   dfm_set_error("dfm_gemm_group: unsupported dtype %d", dtype);
   return DFM_ERR_DTYPE;
-}
-
-extern "C" int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
-                              void* const* C, void* ws, dfm_stream_t stream) {
-  return gemm_group_any(dtype, n, d, A, B, C, ws, stream, nullptr, nullptr);
-}
-
-extern "C" int dfm_gemm_group_deferred(int dtype, int n, const DfmGemmDesc* d, const void* const* A,
-                                       const void* const* B, void* const* C, void* ws, DfmPartialSum* combine,
-                                       int* ncombine, dfm_stream_t stream) {
-  DFM_CHECK_ARG(combine && ncombine, "dfm_gemm_group_deferred: null combine / ncombine");
-  *ncombine = 0;
-  return gemm_group_any(dtype, n, d, A, B, C, ws, stream, combine, ncombine);
 }

@@ -6,6 +6,6 @@ int dfm_gemm_bf16(const DfmGemmDesc* d, const void* A, const void* B, void* C, v
 }
 
 int dfm_gemm_group_bf16(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                       void* ws, hipStream_t s, DfmPartialSum* defer, int* ndefer) {
-  return gemm_group_typed<bf16_t>(n, d, A, B, C, ws, s, defer, ndefer);
+                       void* ws, hipStream_t s) {
+  return gemm_group_typed<bf16_t>(n, d, A, B, C, ws, s);
 }

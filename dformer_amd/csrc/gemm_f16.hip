@@ -6,6 +6,6 @@ int dfm_gemm_f16(const DfmGemmDesc* d, const void* A, const void* B, void* C, vo
 }
 
 int dfm_gemm_group_f16(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                       void* ws, hipStream_t s, DfmPartialSum* defer, int* ndefer) {
-  return gemm_group_typed<f16_t>(n, d, A, B, C, ws, s, defer, ndefer);
+                       void* ws, hipStream_t s) {
+  return gemm_group_typed<f16_t>(n, d, A, B, C, ws, s);
 }

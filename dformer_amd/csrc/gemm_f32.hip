@@ -6,6 +6,6 @@ int dfm_gemm_f32(const DfmGemmDesc* d, const void* A, const void* B, void* C, vo
 }
 
 int dfm_gemm_group_f32(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                       void* ws, hipStream_t s, DfmPartialSum* defer, int* ndefer) {
-  return gemm_group_typed<float>(n, d, A, B, C, ws, s, defer, ndefer);
+                       void* ws, hipStream_t s) {
+  return gemm_group_typed<float>(n, d, A, B, C, ws, s);
 }

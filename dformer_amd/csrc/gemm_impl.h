@@ -1225,16 +1225,9 @@ void fill_args(GemmArgs& a, const DfmGemmDesc* d, const void* A, const void* B, 
              al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
 }
 
-// a problem whose split-K combine is a plain float32 store / accumulate (+ the bias-gradient column):
-// the combine can run as a layout-3 deferred reduction (dfm_partial_sum_group)
-bool combine_deferrable(const DfmGemmDesc* d) {
-  return d->c_f32 && (d->beta == 0.f || d->beta == 1.f) && !d->bias && d->act == 0 && !d->preact && !d->mul &&
-         !d->res && (d->batch <= 1) && d->ldc == d->N && (!d->colsum || d->colsum_accumulate == (d->beta != 0.f));
-}
-
 template <typename T, bool AK, bool BKC>
 int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C, char* ws,
-                 hipStream_t s, DfmPartialSum* defer = nullptr, int* ndefer = nullptr) {
+                 hipStream_t s) {
   constexpr int BM = 128, BN = 128, NW = 8, WM_ = 2, BK = sizeof(T) == 2 ? 64 : 32, DEPTH = 2;
   using GA = TileGeom<T, BM, BK, AK, 64 * NW>;
   using GB = TileGeom<T, BN, BK, BKC, 64 * NW>;
@@ -1268,14 +1261,8 @@ int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* 
     g.start[q + 1] = g.start[q] + (nblk + 7) / 8 * 8;
     r.p[q] = g.p[q];
     const long total = (long)g.p[q].batch * g.p[q].M * g.p[q].ldw;
-    bool deferred = false;
-    if (splits[q] > 1 && defer && combine_deferrable(&d[q])) {
-      defer[(*ndefer)++] = DfmPartialSum{g.p[q].ws, (float*)C[q], d[q].colsum, total, (long)g.p[q].ldw, splits[q], 3,
-                                         d[q].beta != 0.f ? 1 : 0, (long)d[q].N};
-      deferred = true;
-    }
-    r.start[q + 1] = r.start[q] + (splits[q] > 1 && !deferred ? (int)cdiv(total, 64) : 0);
-    any_split = any_split || (splits[q] > 1 && !deferred);
+    r.start[q + 1] = r.start[q] + (splits[q] > 1 ? (int)cdiv(total, 64) : 0);
+    any_split = any_split || splits[q] > 1;
   }
   DFM_LAUNCH(kern, dim3((unsigned)g.start[n]), dim3(64 * NW), lds, s, g);
   DFM_LAUNCH_CHECK();
@@ -1328,7 +1315,7 @@ bool glds_group_member(const DfmGemmDesc* d, const void* A, const void* B) {
 
 template <typename T>
 int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                     void* ws, hipStream_t s, DfmPartialSum* defer = nullptr, int* ndefer = nullptr) {
+                     void* ws, hipStream_t s) {
   const bool ak = d[0].a_kcontig, bk = d[0].b_kcontig;
   if (ak) {
     // forwards / input gradients: the ring-kernel members as one grouped launch, the rest (short K,
@@ -1356,8 +1343,8 @@ int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const vo
   }
   if (ak && bk) return group_launch<T, true, true>(n, d, A, B, C, (char*)ws, s);
   if (ak) return group_launch<T, true, false>(n, d, A, B, C, (char*)ws, s);
-  if (bk) return group_launch<T, false, true>(n, d, A, B, C, (char*)ws, s, defer, ndefer);
-  return group_launch<T, false, false>(n, d, A, B, C, (char*)ws, s, defer, ndefer);
+  if (bk) return group_launch<T, false, true>(n, d, A, B, C, (char*)ws, s);
+  return group_launch<T, false, false>(n, d, A, B, C, (char*)ws, s);
 }
 
 // per-dtype instantiations live in gemm_bf16.hip / gemm_f16.hip / gemm_f32.hip (one translation unit
@@ -1368,8 +1355,8 @@ int dfm_gemm_bf16(const DfmGemmDesc* d, const void* A, const void* B, void* C, v
 int dfm_gemm_f16(const DfmGemmDesc* d, const void* A, const void* B, void* C, void* ws, hipStream_t s);
 int dfm_gemm_f32(const DfmGemmDesc* d, const void* A, const void* B, void* C, void* ws, hipStream_t s);
 int dfm_gemm_group_bf16(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                        void* ws, hipStream_t s, DfmPartialSum* defer = nullptr, int* ndefer = nullptr);
+                        void* ws, hipStream_t s);
 int dfm_gemm_group_f16(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                       void* ws, hipStream_t s, DfmPartialSum* defer = nullptr, int* ndefer = nullptr);
+                       void* ws, hipStream_t s);
 int dfm_gemm_group_f32(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                       void* ws, hipStream_t s, DfmPartialSum* defer = nullptr, int* ndefer = nullptr);
+                       void* ws, hipStream_t s);

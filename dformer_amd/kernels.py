@@ -124,8 +124,8 @@ class wgrad_group:
         pending, reds = _WG_PENDING, _RED_PENDING
         _WG_PENDING, _RED_PENDING = self.prev
         if exc_type is None:
-            if pending:  # split-K combines join the reductions' launch where their epilogue allows
-                flush_wgrad(pending, reds if reds is not None else None)
+            if pending:
+                flush_wgrad(pending)
             if reds:
                 flush_reductions(reds)
         return False
@@ -154,10 +154,8 @@ def flush_reductions(reds):
         _acct(0, 0)
 
 
-def flush_wgrad(pending, reds=None):
-    """Issue queued GEMMs as grouped launches: problems of one dtype / operand layout, 8 per launch.
-    With `reds` (the block's pending reductions) the split-K combines are deferred into it
-    (dfm_gemm_group_deferred: layout-3 partial sums, issued by the same dfm_partial_sum_group launch)."""
+def flush_wgrad(pending):
+    """Issue queued GEMMs as grouped launches: problems of one dtype / operand layout, 8 per launch."""
     classes = {}
     for item in pending:
         d, dt = item[0], item[1]
@@ -171,24 +169,10 @@ def flush_wgrad(pending, reds=None):
             pb = (ctypes.c_void_p * n)(*[c[3].data_ptr() for c in chunk])
             pc = (ctypes.c_void_p * n)(*[c[4].data_ptr() for c in chunk])
             dev = chunk[0][2].device
-            nbytes = lib.dfm_gemm_group_workspace_size(n, descs)
-            if reds is not None and nbytes:
-                # the partials are read by the reductions' launch: a buffer of their own until then
-                ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-                descs[0].workspace_bytes = nbytes
-                comb = (_lib.PartialSum * n)()
-                nc = ctypes.c_int(0)
-                check(lib.dfm_gemm_group_deferred(dt, n, descs, ctypes.cast(pa, ctypes.c_void_p),
-                                                  ctypes.cast(pb, ctypes.c_void_p), ctypes.cast(pc, ctypes.c_void_p),
-                                                  ptr(ws), ctypes.cast(comb, ctypes.c_void_p), ctypes.byref(nc),
-                                                  stream()), "dfm_gemm_group_deferred")
-                for i in range(nc.value):
-                    reds.append((comb[i], ws))
-            else:
-                ws = _ws(nbytes, dev)
-                descs[0].workspace_bytes = ws.numel() if ws is not None else 0
-                check(lib.dfm_gemm_group(dt, n, descs, ctypes.cast(pa, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p),
-                                         ctypes.cast(pc, ctypes.c_void_p), ptr(ws), stream()), "dfm_gemm_group")
+            ws = _ws(lib.dfm_gemm_group_workspace_size(n, descs), dev)
+            descs[0].workspace_bytes = ws.numel() if ws is not None else 0
+            check(lib.dfm_gemm_group(dt, n, descs, ctypes.cast(pa, ctypes.c_void_p), ctypes.cast(pb, ctypes.c_void_p),
+                                     ctypes.cast(pc, ctypes.c_void_p), ptr(ws), stream()), "dfm_gemm_group")
             if ACCOUNT is not None:
                 _acct(sum(c[5] for c in chunk), sum(c[6] for c in chunk), chunk[0][7])
 

@@ -40,7 +40,7 @@ typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
 int dfm_abi_version(void); /* 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
-                              dfm_block_workspace_size), dfm_gemm_group_deferred, DfmPartialSum.ncol (layout 3); 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
+                              dfm_block_workspace_size); 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
                               second stages (dfm_partial_sum_group); 7: DfmGemmDesc.workspace_bytes + stride /
                               leading-dimension validation */
 
@@ -115,6 +115,7 @@ int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const void* B, void
 size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d);
 int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
                    void* const* C, void* workspace, dfm_stream_t stream);
+
 /* ---------------------------------------------------------------- deferred reduction second stages
  * The parameter-gradient reductions below (LayerNorm dgamma / dbeta, layer-scale dscale, depthwise
  * dw / db) run in two stages: per-block partials in the caller's workspace, then a fixed-order sum
@@ -126,8 +127,6 @@ int dfm_gemm_group(int dtype, int n, const DfmGemmDesc* d, const void* const* A,
  *   layout 0: out0[e] = sum_b part[b*n + e]                      (e < n)
  *   layout 1: e < n0 ? out0[e] : out1[e - n0]
  *   layout 2: depthwise [C][n0] with n0 = k*k + 1: out0[c*(n0-1) + i] for i < n0-1, out1[c] (bias)
- *   layout 3: a split-K GEMM's combine, rows of n0 (padded) columns: e = m*n0 + j -> j < ncol: out0[m*ncol + j];
- *             j == ncol: out1[m] (the bias-gradient column, when out1 is set); other j: dropped
  *   accumulate: out += sum instead of out = sum. */
 typedef struct DfmPartialSum {
   const float* part;
@@ -138,18 +137,8 @@ typedef struct DfmPartialSum {
   int nblk;
   int layout;
   int accumulate;
-  long ncol; /* layout 3 only */
 } DfmPartialSum;
 int dfm_partial_sum_group(int n, const DfmPartialSum* sums, dfm_stream_t stream);
-/* dfm_gemm_group (above) with the split-K combine deferred: for every problem whose split-K partials
- * need combining and whose epilogue is a plain float32 store / accumulate (c_f32, beta 0 or 1, no bias /
- * act / mul / res, ldc = N; the bias-gradient column allowed) the combine is described in
- * combine[*ncombine] (layout 3) instead of launched — a Block backward issues it with its other deferred
- * reductions in one dfm_partial_sum_group launch; the workspace must stay untouched until then. Other
- * problems' combines are launched as dfm_gemm_group does. combine has room for n entries. */
-int dfm_gemm_group_deferred(int dtype, int n, const DfmGemmDesc* d, const void* const* A, const void* const* B,
-                            void* const* C, void* workspace, DfmPartialSum* combine, int* ncombine,
-                            dfm_stream_t stream);
 
 /* ---------------------------------------------------------------- LayerNorm, channels_last
  * DFormer.py:21-45 (F.layer_norm over the last dim, eps 1e-6). mean/rstd: float32 [rows].
