@@ -9,7 +9,7 @@
 namespace {
 template <int BM, int BN, int NW, int WM_, int NS, int MINB>
 int run(GemmArgs& a, bool bk, hipStream_t s) {
-  return glds_ak<BM, BN, NW, WM_, NS, MINB>(a, bk, s);
+  return glds_ak<bf16_t, BM, BN, NW, WM_, NS, MINB>(a, bk, s);
 }
 }  // namespace
 
