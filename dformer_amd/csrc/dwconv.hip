@@ -274,9 +274,25 @@ W3Geom w3_geom(int B, int H, int W, int C, int waves_per_simd = 2) {
   return g;
 }
 
+// Out-of-image taps: every row load is issued unconditionally from an in-image address (the unit's
+// own first row h0 / first column w0, already in cache) and the out-of-image vectors are zeroed at
+// their first use through a per-row column bitmask. A load under `ok ? load : 0` sits in a divergent
+// branch and hipcc waits for it (vmcnt(0)) at the merge right after issue, so the next row's
+// prefetch never overlapped the current row's FMAs; the mask is applied one loop iteration after the
+// load, where the wait is needed anyway.
 template <typename T>
-DFM_INLINE uint2 w3_ld(const T* p, bool ok) {
-  return ok ? *reinterpret_cast<const uint2*>(p) : make_uint2(0, 0);
+DFM_INLINE uint2 w3_ld(const T* base, long ld, long img, int W, int h, int ww, int c0) {
+  return *reinterpret_cast<const uint2*>(base + (img + (long)h * W + ww) * ld + c0);
+}
+
+template <int N>
+DFM_INLINE void w3_keep(uint2* r, unsigned m) {  // zero the vectors whose bit in m is clear
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    const bool k = (m >> q) & 1u;
+    r[q].x = k ? r[q].x : 0u;
+    r[q].y = k ? r[q].y : 0u;
+  }
 }
 
 template <typename T>
@@ -332,31 +348,36 @@ __global__ __launch_bounds__(256) void dw3_stream_wgrad_kernel(int B, int H, int
     const long b = u / ((long)nstrips * nchunks);
     const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
     const long img = b * H * W;
-    auto load_x = [&](int h, uint2* r) {
+    unsigned cmx = 0, cmd = 0;  // in-image columns of the x window / the dy strip
+#pragma unroll
+    for (int q = 0; q < NX; ++q) cmx |= (unsigned)(w0 - 1 + q >= 0 && w0 - 1 + q < W) << q;
+#pragma unroll
+    for (int t = 0; t < TW; ++t) cmd |= (unsigned)(w0 + t < W) << t;
+    auto load_x = [&](int h, uint2* r) -> unsigned {  // returns the row's keep mask
       const bool hok = h >= 0 && h < H;
+      const int hc = hok ? h : h0;
 #pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        const int w = w0 - 1 + q;
-        r[q] = w3_ld<T>(x + (img + (long)h * W + w) * ldx + c0, hok && w >= 0 && w < W);
-      }
+      for (int q = 0; q < NX; ++q) r[q] = w3_ld<T>(x, ldx, img, W, hc, ((cmx >> q) & 1u) ? w0 - 1 + q : w0, c0);
+      return hok ? cmx : 0u;
     };
-    auto load_dy = [&](int h, uint2* r) {
+    auto load_dy = [&](int h, uint2* r) -> unsigned {
       const bool hok = h < h1;
+      const int hc = hok ? h : h0;
 #pragma unroll
-      for (int t = 0; t < TW; ++t) {
-        const int w = w0 + t;
-        r[t] = w3_ld<T>(dy + (img + (long)h * W + w) * lddy + c0, hok && w < W);
-      }
+      for (int t = 0; t < TW; ++t) r[t] = w3_ld<T>(dy, lddy, img, W, hc, ((cmd >> t) & 1u) ? w0 + t : w0, c0);
+      return hok ? cmd : 0u;
     };
     uint2 x0[NX], x1[NX], x2[NX], dc[TW];
-    load_x(h0 - 1, x0);
-    load_x(h0, x1);
-    load_x(h0 + 1, x2);
-    load_dy(h0, dc);
+    w3_keep<NX>(x0, load_x(h0 - 1, x0));
+    w3_keep<NX>(x1, load_x(h0, x1));
+    unsigned m2 = load_x(h0 + 1, x2);
+    unsigned md = load_dy(h0, dc);
     for (int h = h0; h < h1; ++h) {
+      w3_keep<NX>(x2, m2);  // the rows loaded one iteration ago
+      w3_keep<TW>(dc, md);
       uint2 xn[NX], dn[TW];
-      load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
-      load_dy(h + 1, dn);
+      m2 = load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) reads as zeros
+      md = load_dy(h + 1, dn);
       float gv[TW][CPT];
 #pragma unroll
       for (int t = 0; t < TW; ++t) {
@@ -663,21 +684,24 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
     const long b = u / ((long)nstrips * nchunks);
     const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
     const long img = b * H * W;
-    auto load_x = [&](int h, uint2* r) {
-      const bool hok = h >= 0 && h < H;
+    unsigned cm = 0;  // in-image columns of the window
 #pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        const int ww = w0 - 1 + q;
-        r[q] = w3_ld<T>(x + (img + (long)h * W + ww) * ldx + c0, hok && ww >= 0 && ww < W);
-      }
+    for (int q = 0; q < NX; ++q) cm |= (unsigned)(w0 - 1 + q >= 0 && w0 - 1 + q < W) << q;
+    auto load_x = [&](int h, uint2* r) -> unsigned {  // returns the row's keep mask
+      const bool hok = h >= 0 && h < H;
+      const int hc = hok ? h : h0;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) r[q] = w3_ld<T>(x, ldx, img, W, hc, ((cm >> q) & 1u) ? w0 - 1 + q : w0, c0);
+      return hok ? cm : 0u;
     };
     uint2 x0[NX], x1[NX], x2[NX];
-    load_x(h0 - 1, x0);
-    load_x(h0, x1);
-    load_x(h0 + 1, x2);
+    w3_keep<NX>(x0, load_x(h0 - 1, x0));
+    w3_keep<NX>(x1, load_x(h0, x1));
+    unsigned m2 = load_x(h0 + 1, x2);
     for (int h = h0; h < h1; ++h) {
+      w3_keep<NX>(x2, m2);  // the row loaded one iteration ago
       uint2 xn[NX];
-      load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
+      m2 = load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) reads as zeros
       f2v accp[TW][CP];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
@@ -808,25 +832,31 @@ __global__ __launch_bounds__(256) void dw3_stream_bwd_kernel(int B, int H, int W
     const long b = u / ((long)nstrips * nchunks);
     const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
     const long img = b * H * W;
-    auto load_row = [&](const T* src, long ld, int h, uint2* r) {  // columns w0-1 .. w0+TW, zero outside
-      const bool hok = h >= 0 && h < H;
+    unsigned cm = 0;  // in-image columns of the window
 #pragma unroll
-      for (int q = 0; q < NX; ++q) {
-        const int ww = w0 - 1 + q;
-        r[q] = w3_ld<T>(src + (img + (long)h * W + ww) * ld + c0, hok && ww >= 0 && ww < W);
-      }
+    for (int q = 0; q < NX; ++q) cm |= (unsigned)(w0 - 1 + q >= 0 && w0 - 1 + q < W) << q;
+    // columns w0-1 .. w0+TW of row h; returns the row's keep mask (zero outside the image)
+    auto load_row = [&](const T* src, long ld, int h, uint2* r) -> unsigned {
+      const bool hok = h >= 0 && h < H;
+      const int hc = hok ? h : h0;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) r[q] = w3_ld<T>(src, ld, img, W, hc, ((cm >> q) & 1u) ? w0 - 1 + q : w0, c0);
+      return hok ? cm : 0u;
     };
     uint2 x0[NX], x1[NX], x2[NX], d0[NX], d1[NX], d2[NX];
-    load_row(x, ldx, h0 - 1, x0);
-    load_row(x, ldx, h0, x1);
-    load_row(x, ldx, h0 + 1, x2);
-    load_row(dy, lddy, h0 - 1, d0);
-    load_row(dy, lddy, h0, d1);
-    load_row(dy, lddy, h0 + 1, d2);
+    w3_keep<NX>(x0, load_row(x, ldx, h0 - 1, x0));
+    w3_keep<NX>(x1, load_row(x, ldx, h0, x1));
+    unsigned m2 = load_row(x, ldx, h0 + 1, x2);
+    w3_keep<NX>(d0, load_row(dy, lddy, h0 - 1, d0));
+    w3_keep<NX>(d1, load_row(dy, lddy, h0, d1));
+    unsigned m2d = load_row(dy, lddy, h0 + 1, d2);
     for (int h = h0; h < h1; ++h) {
+      w3_keep<NX>(x2, m2);  // the rows loaded one iteration ago
+      w3_keep<NX>(d2, m2d);
       uint2 xn[NX], dn[NX];
-      load_row(x, ldx, h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) loads as zeros
-      load_row(dy, lddy, h + 1 < h1 ? h + 2 : H, dn);
+      const int hn = h + 1 < h1 ? h + 2 : H;  // row H (and any row past the chunk) reads as zeros
+      m2 = load_row(x, ldx, hn, xn);
+      m2d = load_row(dy, lddy, hn, dn);
       f2v o[TW][CP];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
