@@ -842,6 +842,28 @@ DFM_INLINE void glds_block(const GemmArgs& a, int lid, char* smem) {
   }
   const bool patch = ones_r >= bn && ones_r < bn + BN;  // block-uniform
 
+#ifndef DFM_RING_ASM_DMA
+#define DFM_RING_ASM_DMA 1
+#endif
+#if DFM_RING_ASM_DMA
+  // the DMA as inline asm (measured 471.5 / 472.9 vs 470.1 / 470.9 images/s); m0 is written here
+  // only: the ring kernels have no other m0 user (checked in their ISA): the compiler no longer sees an LDS write in flight, so it stops draining
+  // the ring (s_waitcnt vmcnt(0)) before the transposing fragment reads; ordering comes from the
+  // counted waits, the barrier and the compiler fences below
+  auto issue = [&](int t, int stage) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const T* gp = src[j] + t * step[j];
+      const unsigned l = __builtin_amdgcn_readfirstlane(
+          (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + stage * STAGE + dst[j]));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(gp) : "memory", "m0");
+#pragma clang diagnostic pop
+    }
+  };
+#define DFM_CFENCE() asm volatile("" ::: "memory")
+#else
   auto issue = [&](int t, int stage) {
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -849,6 +871,8 @@ DFM_INLINE void glds_block(const GemmArgs& a, int lid, char* smem) {
                                        (void __attribute__((address_space(3)))*)(smem + stage * STAGE + dst[j]),
                                        16, 0, 0);
   };
+#define DFM_CFENCE() ((void)0)
+#endif
   auto patch_ones = [&](int stage) {  // after this wave's DMAs of the stage landed
 #pragma unroll
     for (int j = 0; j < J; ++j)
@@ -910,15 +934,19 @@ DFM_INLINE void glds_block(const GemmArgs& a, int lid, char* smem) {
       if (NS > 2 && rem >= NS - 2) wait_vm<J * (NS > 2 ? NS - 2 : 0)>();
       else if (NS > 3 && rem == 1) wait_vm<J>();
       else wait_vm<0>();
+      DFM_CFENCE();
       if (patch) patch_ones(stage);
       wait_lgkm0();
       __builtin_amdgcn_s_barrier();
+      DFM_CFENCE();
       if (t + NS - 1 < nfull) issue(t + NS - 1, (t + NS - 1) % NS);
       compute(stage);
     }
   }
   wait_vm<0>();
+  DFM_CFENCE();
   __syncthreads();
+#undef DFM_CFENCE
   // guarded tail: the partial last slice (zero fill past kend), staged through registers into stage 0
   for (int kt = nfull; kt < nk; ++kt) {
     const int k0 = kbeg + kt * GBK;
@@ -995,6 +1023,16 @@ int launch_glds(GemmArgs& a, hipStream_t s) {
     DFM_LAUNCH_CHECK();
   }
   return DFM_OK;
+}
+
+// ring depth of the 64 x 64 tiles (A/B switch DFM_GLDS_NS: 2 = two stages at four blocks per CU,
+// 3 = three stages at three blocks per CU)
+inline int glds_ns() {
+  static const int ns = [] {
+    const char* e = getenv("DFM_GLDS_NS");
+    return e && atoi(e) == 3 ? 3 : 2;
+  }();
+  return ns;
 }
 
 template <typename T, int BM, int BN, int NW, int WM_, int NS, int MINB>
@@ -1153,6 +1191,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
       // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
       // (438.7-438.4 -> 439.0-440.3 images/s on one box; 65-93 vs 81-127 us per launch alone)
       if (a.splits == 1 && d->M >= 65536 && a.Nw >= 512 && d->K >= 512) return glds_ak<T, 128, 128, 8, 2, 2, 2>(a, bk, s);
+      if (glds_ns() == 3) return glds_ak<T, 64, 64, 4, 2, 3, 3>(a, bk, s);
       return glds_ak<T, 64, 64, 4, 2, 2, 4>(a, bk, s);
     }
   }
@@ -1275,10 +1314,10 @@ int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* 
 
 // k-contiguous-A problems whose operands suit the ring kernel (16-byte aligned, >= 2 whole k-slices)
 // go to gemm_glds_group_kernel, unsplit, in 64 x 64 tiles (the single-GEMM route's tile for these shapes)
-template <typename T, bool BKC>
+template <typename T, bool BKC, int NS = 2, int MINB = 4>
 int group_launch_glds(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
                       hipStream_t s) {
-  constexpr int BM = 64, BN = 64, NW = 4, WM_ = 2, NS = 2, MINB = 4;
+  constexpr int BM = 64, BN = 64, NW = 4, WM_ = 2;
   using IA = GImg<BM, true>;
   using IB = GImg<BN, BKC>;
   constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
@@ -1399,6 +1438,8 @@ int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const vo
     }
     if constexpr (sizeof(T) == 2) {
       if (m == 1) return gemm_typed<T>(&gd[0], ga[0], gb[0], gc[0], ws, s);
+      if (m > 1 && glds_ns() == 3)
+        return bk ? group_launch_glds<T, true, 3, 3>(m, gd, ga, gb, gc, s) : group_launch_glds<T, false, 3, 3>(m, gd, ga, gb, gc, s);
       if (m > 1) return bk ? group_launch_glds<T, true>(m, gd, ga, gb, gc, s) : group_launch_glds<T, false>(m, gd, ga, gb, gc, s);
     }
     return DFM_OK;
