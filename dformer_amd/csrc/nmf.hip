@@ -164,7 +164,8 @@ extern "C" int dfm_nmf_fwd(int dtype, int batch, long N, long D, int R, int step
   for (int s = 0; s < steps; ++s) {
     // C_{s+1} = C_s * (x B_s) / (C_s (B_s^T B_s) + eps)
     const float* Cs = F(sl.C(s));
-    NMF_DO(dfm_gemm(dtype, &g.xb, x, Bop, F(sl.NUM1(s)), gws, stream));
+    // (step 0: NUM1(0) still holds x B_0, the softmax's input)
+    if (s > 0) NMF_DO(dfm_gemm(dtype, &g.xb, x, Bop, F(sl.NUM1(s)), gws, stream));
     NMF_DO(dfm_gemm(DFM_F32, &g.btb, Bt, Bt, F(sl.M1(s)), gws, stream));
     float* Cn = F(sl.C(s + 1));
     NMF_DO(dfm_nmf_update_mm(batch, N, R, Cs, F(sl.NUM1(s)), F(sl.M1(s)), eps, F(sl.DEN1(s)), Cn, c16, copy, stream));

@@ -348,7 +348,8 @@ class NMF2DFn(torch.autograd.Function):
             R = b16.shape[2]
             return K.bmm(x, b16, a_t=a_t, out=torch.empty(Bb, D if a_t else N, R, **f32))
 
-        coef = K.softmax_rows(xmm(K.cast(B0, x.dtype) if lp else B0))   # softmax(x^T B)
+        num0 = xmm(K.cast(B0, x.dtype) if lp else B0)
+        coef = K.softmax_rows(num0)                                      # softmax(x^T B)
         hist = []
         Bt, Ct = B0, coef
         Bt16 = K.cast(B0, x.dtype) if lp else B0
@@ -363,8 +364,8 @@ class NMF2DFn(torch.autograd.Function):
             o = K.nmf_update(a, num, den, eps, bf16_copy=x.dtype) if lp else (K.nmf_update(a, num, den, eps),) * 2
             return o[0], den, o[1]
 
-        for _ in range(steps):
-            num1 = xmm(Bt16)                                      # x^T B        [N,R]
+        for s in range(steps):
+            num1 = num0 if s == 0 else xmm(Bt16)                  # x^T B        [N,R]
             M = K.bmm(Bt, Bt, a_t=True)                           # B^T B        [R,R]
             Cn, den1, Cn16 = update(Ct, num1, M)                  # den1 = C (B^T B)
             num2 = xmm(Cn16, a_t=True)                            # x C          [D,R]
