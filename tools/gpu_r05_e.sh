@@ -7,5 +7,5 @@ timeout -k 10 400 python -u bench.py --table-out gpurun_out/${T}_table.json > gp
 tail -1 gpurun_out/${T}_bench.log | cut -c1-400
 bash tools/gpu_prof.sh ${T} || exit 12
 bash tools/gpu_pmc.sh ${T}dom gpurun_out/${T}_table.json || exit 13
-bash tools/gpu_pmc_kernels.sh ${T}k gpurun_out/${T}_table.json "dw7_lds_wgrad_kernel" "dw_tile_fwd_kernel<unsigned short, 7, false" "dw_tile_fwd_kernel<unsigned short, 7, true" "attn_fwd_mfma_kernel" "attn_bwd_mfma_kernel" || exit 14
+bash tools/gpu_pmc_kernels.sh ${T}k gpurun_out/${T}_table.json "dw7_lds_wgrad_kernel" "dw_tile_fwd_kernel<unsigned short, 7, false" "dw_tile_fwd_kernel<unsigned short, 7, true" "attn_fwd_mfma_kernel" "attn_bwd_mfma_kernel" "dw3_stream_bwd_kernel" "dw3_stream_fwd_kernel" || exit 14
 echo evidence done
