@@ -1025,16 +1025,6 @@ int launch_glds(GemmArgs& a, hipStream_t s) {
   return DFM_OK;
 }
 
-// ring depth of the 64 x 64 tiles (A/B switch DFM_GLDS_NS: 2 = two stages at four blocks per CU,
-// 3 = three stages at three blocks per CU)
-inline int glds_ns() {
-  static const int ns = [] {
-    const char* e = getenv("DFM_GLDS_NS");
-    return e && atoi(e) == 3 ? 3 : 2;
-  }();
-  return ns;
-}
-
 template <typename T, int BM, int BN, int NW, int WM_, int NS, int MINB>
 int glds_ak(GemmArgs& a, bool bk, hipStream_t s) {
   if (bk) return launch_glds<T, BM, BN, NW, WM_, true, true, NS, MINB>(a, s);
@@ -1191,7 +1181,6 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
       // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
       // (438.7-438.4 -> 439.0-440.3 images/s on one box; 65-93 vs 81-127 us per launch alone)
       if (a.splits == 1 && d->M >= 65536 && a.Nw >= 512 && d->K >= 512) return glds_ak<T, 128, 128, 8, 2, 2, 2>(a, bk, s);
-      if (glds_ns() == 3) return glds_ak<T, 64, 64, 4, 2, 3, 3>(a, bk, s);
       return glds_ak<T, 64, 64, 4, 2, 2, 4>(a, bk, s);
     }
   }
@@ -1314,10 +1303,10 @@ int group_launch(int n, const DfmGemmDesc* d, const void* const* A, const void* 
 
 // k-contiguous-A problems whose operands suit the ring kernel (16-byte aligned, >= 2 whole k-slices)
 // go to gemm_glds_group_kernel, unsplit, in 64 x 64 tiles (the single-GEMM route's tile for these shapes)
-template <typename T, bool BKC, int NS = 2, int MINB = 4>
+template <typename T, bool BKC>
 int group_launch_glds(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
                       hipStream_t s) {
-  constexpr int BM = 64, BN = 64, NW = 4, WM_ = 2;
+  constexpr int BM = 64, BN = 64, NW = 4, WM_ = 2, NS = 2, MINB = 4;  // (3 stages at 3 blocks per CU: no gain)
   using IA = GImg<BM, true>;
   using IB = GImg<BN, BKC>;
   constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
@@ -1341,68 +1330,6 @@ int group_launch_glds(int n, const DfmGemmDesc* d, const void* const* A, const v
   }
   DFM_LAUNCH(kern, dim3((unsigned)g.start[n]), dim3(64 * NW), lds, s, g);
   DFM_LAUNCH_CHECK();
-  return DFM_OK;
-}
-
-// Weight gradients (row-contiguous A and B: dW = dY^T X over K = pixels) on the LDS-DMA ring in
-// 128 x 128 tiles with the register route's split-K plan (group_splits) and grouped combine: the
-// operand rows of a k-slice land in LDS without register staging and are read with the transposing
-// ds_read_b64_tr_b16 fragments. Taken only when every problem is 16-byte aligned with channel counts
-// that are multiples of 8 (the ring's 8-column chunks never leave a row). A/B switch DFM_WGRAD_RING.
-template <typename T>
-bool wgrad_ring_ok(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, const int* splits) {
-  static const int on = [] {
-    const char* e = getenv("DFM_WGRAD_RING");
-    return e ? atoi(e) : 0;
-  }();
-  if (!on || sizeof(T) != 2) return false;
-  for (int q = 0; q < n; ++q) {
-    GemmArgs a;
-    fill_args<T>(a, &d[q], A[q], B[q], nullptr, nullptr, splits[q]);
-    const int kper = (d[q].K + splits[q] - 1) / splits[q];
-    if (!a.ala || !a.alb || d[q].M % 8 || d[q].N % 8 || kper < 2 * GBK) return false;
-  }
-  return true;
-}
-
-template <typename T>
-int group_launch_ring_wg(int n, const DfmGemmDesc* d, const void* const* A, const void* const* B, void* const* C,
-                         char* ws, const int* splits, hipStream_t s) {
-  constexpr int BM = 128, BN = 128, NW = 8, WM_ = 2, NS = 2, MINB = 4;
-  using IA = GImg<BM, false>;
-  using IB = GImg<BN, false>;
-  constexpr int RP = (128 * NW / (BN / 8)) < BM ? (128 * NW / (BN / 8)) : BM;
-  const size_t lds = std::max((size_t)NS * (IA::BYTES + IB::BYTES), (size_t)RP * (BN + 4) * sizeof(float));
-  auto kern = gemm_glds_group_kernel<T, BM, BN, NW, WM_, false, false, NS, MINB>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  GemmGroup g, r;
-  g.n = r.n = n;
-  g.start[0] = r.start[0] = 0;
-  size_t off = 0;
-  bool any_split = false;
-  for (int q = 0; q < n; ++q) {
-    fill_args<T>(g.p[q], &d[q], A[q], B[q], C[q], splits[q] > 1 ? (float*)(ws + off) : nullptr, splits[q]);
-    off += group_ws_bytes(&d[q], splits[q]);
-    g.p[q].tiles_m = cdiv(d[q].M, BM);
-    g.p[q].tiles_n = cdiv(g.p[q].Nw, BN);
-    g.p[q].n_fast = false;
-    const int nblk = g.p[q].tiles_m * g.p[q].tiles_n * g.p[q].batch * splits[q];
-    g.start[q + 1] = g.start[q] + (nblk + 7) / 8 * 8;
-    r.p[q] = g.p[q];
-    const long total = (long)g.p[q].batch * g.p[q].M * g.p[q].ldw;
-    r.start[q + 1] = r.start[q] + (splits[q] > 1 ? (int)cdiv(total, 64) : 0);
-    any_split = any_split || splits[q] > 1;
-  }
-  DFM_LAUNCH(kern, dim3((unsigned)g.start[n]), dim3(64 * NW), lds, s, g);
-  DFM_LAUNCH_CHECK();
-  if (any_split) {
-    DFM_LAUNCH(splitk_reduce_group_kernel<T>, dim3((unsigned)r.start[n]), dim3(256), 0, s, r);
-    DFM_LAUNCH_CHECK();
-  }
   return DFM_OK;
 }
 
@@ -1438,19 +1365,12 @@ int gemm_group_typed(int n, const DfmGemmDesc* d, const void* const* A, const vo
     }
     if constexpr (sizeof(T) == 2) {
       if (m == 1) return gemm_typed<T>(&gd[0], ga[0], gb[0], gc[0], ws, s);
-      if (m > 1 && glds_ns() == 3)
-        return bk ? group_launch_glds<T, true, 3, 3>(m, gd, ga, gb, gc, s) : group_launch_glds<T, false, 3, 3>(m, gd, ga, gb, gc, s);
       if (m > 1) return bk ? group_launch_glds<T, true>(m, gd, ga, gb, gc, s) : group_launch_glds<T, false>(m, gd, ga, gb, gc, s);
     }
     return DFM_OK;
   }
-  if constexpr (sizeof(T) == 2) {
-    if (!ak && !bk) {
-      int splits[GMAX];
-      group_splits(n, d, splits);
-      if (wgrad_ring_ok<T>(n, d, A, B, splits)) return group_launch_ring_wg<T>(n, d, A, B, C, (char*)ws, splits, s);
-    }
-  }
+  // (weight gradients on the ring kernel in 128 x 128 tiles measured 472.3 / 472.5 vs 472.8 / 473.0
+  // images/s: the register-staged kernel stays)
   if (ak && bk) return group_launch<T, true, true>(n, d, A, B, C, (char*)ws, s);
   if (ak) return group_launch<T, true, false>(n, d, A, B, C, (char*)ws, s);
   if (bk) return group_launch<T, false, true>(n, d, A, B, C, (char*)ws, s);

@@ -10,8 +10,6 @@ the stem's GELU) into the convolution operand and one MFMA GEMM (csrc/conv.hip),
 input image and the previous stage's NHWC rows in place (no NCHW<->NHWC permute copies).
 """
 
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -108,9 +106,6 @@ class Attention(nn.Module):
 
 
 _SIDE = {}
-# largest H*W whose depth ConvFFN runs on the side stream (DFM_FFN_SIDE_MAX_PLANE, A/B switch): above
-# it the kernels alone fill the GPU and the fork / join edges cost more than the overlap gains
-FFN_SIDE_MAX_PLANE = int(os.environ.get("DFM_FFN_SIDE_MAX_PLANE", str(1 << 30)))
 
 
 def _side_stream(dev):
@@ -179,7 +174,7 @@ class Block(nn.Module):
         # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
         # does its backward: autograd replays a node on its forward's stream), which fills the GPU
         # at the late stages where each kernel alone is latency-bound
-        side = _side_stream(x.device) if x1.is_cuda and H * W <= FFN_SIDE_MAX_PLANE else None
+        side = _side_stream(x.device) if x1.is_cuda else None
         if side is not None:
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)

@@ -276,8 +276,6 @@ class ConvFFNFn(torch.autograd.Function):
 # fork / join costs what the overlap gains; a second backward stream for the pooled-attention
 # branch gained nothing either.)
 _ATTN_BWD_SIDE = {}
-# largest H*W whose depth branch runs on the side stream (DFM_ATTN_SIDE_MAX_PLANE, A/B switch)
-ATTN_SIDE_MAX_PLANE = int(os.environ.get("DFM_ATTN_SIDE_MAX_PLANE", str(1 << 30)))
 
 
 def _attn_bwd_side(dev):
@@ -409,7 +407,7 @@ class AttentionFn(torch.autograd.Function):
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
-        side = _attn_bwd_side(dev) if x.is_cuda and P // B <= ATTN_SIDE_MAX_PLANE else None
+        side = _attn_bwd_side(dev) if x.is_cuda else None
         main = torch.cuda.current_stream(dev) if side is not None else None
 
         def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))

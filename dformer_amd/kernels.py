@@ -5,7 +5,6 @@ All tensors are CUDA (HIP) tensors; 2-D operands are [rows, cols] views whose la
 Activations are float32 or bfloat16; statistics / params / param-grads are float32.
 """
 import ctypes
-import os
 
 import torch
 
@@ -217,10 +216,6 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     return out
 
 
-# DFM_FWD_GROUP=0 (A/B measurement only): gemm_many launches its GEMMs one by one
-_FWD_GROUP = os.environ.get("DFM_FWD_GROUP", "1") != "0"
-
-
 def gemm_many(calls):
     """Run independent GEMMs (thunks that call linear / linear_dgrad with collect=lst) as ONE grouped
     launch (dfm_gemm_group: k-contiguous A problems go to the LDS-DMA ring kernel's grouped variant);
@@ -228,7 +223,7 @@ def gemm_many(calls):
     items = []
     for c in calls:
         c(items)
-    if len(items) == 1 or not _FWD_GROUP:
+    if len(items) == 1:
         for d, dt, a, b, out, fl, by, peak in items:
             ws = _ws(lib.dfm_gemm_workspace_size(d), a.device)
             d.workspace_bytes = ws.numel() if ws is not None else 0
