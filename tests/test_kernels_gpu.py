@@ -299,6 +299,30 @@ def test_dwconv_fused_bwd(dt, ident, acc, B, H, W, C):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+# degenerate planes for the streaming 3x3 kernels' clamped-address loads (out-of-image taps read the
+# unit's own first row / column and are zeroed at first use): one pixel, one row, one column, widths
+# below the 4-column strip, a partial last strip and row chunk
+@pytest.mark.parametrize("B,H,W,C", [(1, 1, 1, 8), (2, 1, 5, 16), (1, 3, 2, 24), (2, 9, 1, 8), (1, 2, 9, 48),
+                                     (3, 6, 6, 32)])
+def test_dwconv3_stream_edges(dt, B, H, W, C):
+    k = K()
+    x = torch.randn(B * H * W, C, device=DEV).to(dt)
+    w = torch.randn(C, 1, 3, 3, device=DEV) / 3
+    bias = torch.randn(C, device=DEV)
+    xr = x.float().view(B, H, W, C).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    wr, br = w.clone().requires_grad_(), bias.clone().requires_grad_()
+    ref = F.conv2d(xr, wr, br, padding=1, groups=C) + xr
+    y = k.dwconv(x, (B, H, W), w, bias, 3, True)
+    assert rel(y.float().view(B, H, W, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    dy = torch.randn(B * H * W, C, device=DEV).to(dt)
+    ref.backward(dy.float().view(B, H, W, C).permute(0, 3, 1, 2))
+    dx, dw, db = k.dwconv_bwd(x, dy, (B, H, W), w, 3, add_identity=True)
+    assert rel(dx.float().view(B, H, W, C).permute(0, 3, 1, 2), xr.grad) < TOL[dt]
+    assert rel(dw, wr.grad) < TOL[dt] * 2
+    assert rel(db, br.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 80), (2, 120, 160, 32), (1, 30, 40, 64)])
 def test_dwconv_gelu_grad_out(dt, B, H, W, C):
     """Flag 2: y receives GELU'(pre) while gelu_out receives GELU(pre) (tile and streaming kernels)."""
