@@ -1198,10 +1198,12 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 
 // ---- grouped launch (host)
 // The group's split-K choice: every problem gets split-K slices in proportion to its share of the
-// group's work (tiles x K), so the ~1024 blocks of the launch (two resident per CU, two rounds) each
-// reduce about the same K range (at least 512 elements); d->split_k >= 1 forces a problem's count.
+// group's work (tiles x K), so the ~512 blocks of the launch each reduce about the same K range (at
+// least 512 elements); d->split_k >= 1 forces a problem's count.
 void group_splits(int n, const DfmGemmDesc* d, int* splits) {
-  constexpr double target = 1024.0;
+  // ~512 blocks (one round at two blocks per CU): measured on the step 481.5 / 482.2 images/s vs 472.7 / 473.4 at 1,024 (half the fp32 split-K partials written and
+  // re-read by the combine), 480.5 / 480.8 at 384, 478.5 / 479.2 at 256, 447 at 128, 467 at 2,048
+  constexpr double target = 512.0;
   double work = 0;
   for (int q = 0; q < n; ++q) {
     const int Nw = d[q].N + (d[q].colsum ? 1 : 0);
