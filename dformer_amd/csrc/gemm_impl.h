@@ -1104,6 +1104,7 @@ int choose_splits(const DfmGemmDesc* d, int elem_bytes) {
     return p;
   }
   if (d->K < 1024 || tiles >= 256) return 1;
+  // (~256 blocks: 475.9-476.7 images/s vs 469.4-469.7 at 128 and 473.4-473.8 at 512)
   long s = std::min((256 + tiles - 1) / tiles, (long)d->K / 512);
   int p = 1;
   while (2L * p <= s && p < 1024) p *= 2;
@@ -1201,8 +1202,10 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
 // group's work (tiles x K), so the ~512 blocks of the launch each reduce about the same K range (at
 // least 512 elements); d->split_k >= 1 forces a problem's count.
 void group_splits(int n, const DfmGemmDesc* d, int* splits) {
-  // ~512 blocks (one round at two blocks per CU): measured on the step 481.5 / 482.2 images/s vs 472.7 / 473.4 at 1,024 (half the fp32 split-K partials written and
-  // re-read by the combine), 480.5 / 480.8 at 384, 478.5 / 479.2 at 256, 447 at 128, 467 at 2,048
+  // ~512 blocks (one round at two blocks per CU): measured on the step 481.5 / 482.2 images/s vs
+  // 472.7 / 473.4 at 1,024 (half the fp32 split-K partials written and re-read by the combine),
+  // 480.5 / 480.8 at 384, 478.5 / 479.2 at 256, 447 at 128, 467 at 2,048; the 512-element minimum
+  // per block measured flat against 256 / 1,024
   constexpr double target = 512.0;
   double work = 0;
   for (int q = 0; q < n; ++q) {
