@@ -846,10 +846,10 @@ DFM_INLINE void glds_block(const GemmArgs& a, int lid, char* smem) {
 #define DFM_RING_ASM_DMA 1
 #endif
 #if DFM_RING_ASM_DMA
-  // the DMA as inline asm (measured 471.5 / 472.9 vs 470.1 / 470.9 images/s); m0 is written here
-  // only: the ring kernels have no other m0 user (checked in their ISA): the compiler no longer sees an LDS write in flight, so it stops draining
-  // the ring (s_waitcnt vmcnt(0)) before the transposing fragment reads; ordering comes from the
-  // counted waits, the barrier and the compiler fences below
+  // The DMA as inline asm (measured 471.5 / 472.9 vs 470.1 / 470.9 images/s): the compiler no longer
+  // sees an LDS write in flight, so it stops draining the ring (s_waitcnt vmcnt(0)) before the
+  // transposing fragment reads; ordering comes from the counted waits, the barrier and the compiler
+  // fences below. m0 is written here only (the ring kernels have no other m0 user, checked in their ISA).
   auto issue = [&](int t, int stage) {
 #pragma unroll
     for (int j = 0; j < J; ++j) {
