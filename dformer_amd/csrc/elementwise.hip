@@ -71,7 +71,9 @@ DFM_INLINE void ldvec(const T* p, float* v) {
   }
 }
 
-template <typename T, int MODE>
+// YP: y present (a compile-time flag: a load under a runtime `if (y)` was waited on right where it was
+// issued, which serialized the four rows in flight)
+template <typename T, int MODE, bool YP>
 __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const T* __restrict__ x, long ldx,
                                                          const T* __restrict__ y, long ldy,
                                                          const float* __restrict__ p0, const float* __restrict__ p1,
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const
     if (MODE == 0) {
       const float sc = p1 ? p1[r / rps] : 1.f;
 #pragma unroll
-      for (int e = 0; e < V; ++e) s0[e] += (y ? xv[e] * yv[e] : xv[e]) * sc;
+      for (int e = 0; e < V; ++e) s0[e] += (YP ? xv[e] * yv[e] : xv[e]) * sc;
     } else if (MODE == 1) {
 #pragma unroll
       for (int e = 0; e < V; ++e) {
@@ -121,14 +123,14 @@ __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const
       }
     }
   };
-  constexpr bool HAS_Y = MODE != 1;
+  constexpr bool HAS_Y = MODE != 1 && YP;
   long r = r0 + rl;
   for (; r + 3 * RL < r1; r += 4 * RL) {
     float xv[4][V], yv[4][V];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       ldvec<T>(x + (r + u * RL) * ldx + c0, xv[u]);
-      if (HAS_Y && y) ldvec<T>(y + (r + u * RL) * ldy + c0, yv[u]);
+      if (HAS_Y) ldvec<T>(y + (r + u * RL) * ldy + c0, yv[u]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) add_row(r + u * RL, xv[u], yv[u]);
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(256) void colred_vec_kernel(long rows, int C, const
   for (; r < r1; r += RL) {
     float xv[V], yv[V];
     ldvec<T>(x + r * ldx + c0, xv);
-    if (HAS_Y && y) ldvec<T>(y + r * ldy + c0, yv);
+    if (HAS_Y) ldvec<T>(y + r * ldy + c0, yv);
     add_row(r, xv, yv);
   }
 #pragma unroll
@@ -176,9 +178,12 @@ int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, c
   // input-gradient golden past 1e-3 in round 1).
   const bool vec = C % V == 0 && G <= 256 && 256 % G == 0 && ldx % V == 0 && ((uintptr_t)x & 15) == 0 &&
                    (!y || (ldy % V == 0 && ((uintptr_t)y & 15) == 0));
-  if (vec)
-    DFM_LAUNCH((colred_vec_kernel<T, MODE>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
-                       (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
+  if (vec && y)
+    DFM_LAUNCH((colred_vec_kernel<T, MODE, true>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
+               (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
+  else if (vec)
+    DFM_LAUNCH((colred_vec_kernel<T, MODE, false>), dim3(nblk), dim3(256), 0, s, rows, C, (const T*)x, ldx,
+               (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
   else
     DFM_LAUNCH((colred_kernel<T, MODE>), dim3(nblk, cdiv(C, COLS)), dim3(256), 0, s, rows, C, (const T*)x,
                        ldx, (const T*)y, ldy, p0, p1, rps > 0 ? rps : 1, (float*)ws, nblk, aux);
