@@ -239,7 +239,13 @@ DFM_INLINE float ps_lane_sum(const float* __restrict__ part, long n, long e, int
 #pragma unroll
     for (int i = 0; i < 8; ++i) s += v[i];
   }
-  for (; b < nblk; b += 16) s += part[(long)b * n + e];
+  if (b < nblk) {  // the tail: every load issued before the first add (clamped index, masked add),
+    float v[8];    // the same order of additions
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = part[(long)min(b + 16 * i, nblk - 1) * n + e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = b + 16 * i < nblk ? s + v[i] : s;
+  }
   return s;
 }
 

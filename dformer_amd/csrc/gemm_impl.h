@@ -697,7 +697,13 @@ DFM_INLINE void splitk_reduce_block(const GemmArgs& a, long blk) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) v += t[i];
     }
-    for (; s < a.splits; s += G) v += p[(long)s * total];
+    if (s < a.splits) {  // the tail: every load issued before the first add (clamped index, masked
+      float t[8];        // add), the same order of additions
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = p[(long)min(s + i * G, a.splits - 1) * total];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v = s + i * G < a.splits ? v + t[i] : v;
+    }
   }
   if (G > 1) {
     red[g][o] = v;
