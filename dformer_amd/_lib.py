@@ -75,6 +75,7 @@ BLOCK_GEMM_WEIGHTS = frozenset(n for n in BLOCK_PARAM_NAMES if n.endswith(".weig
 _SIGS = {
     "dfm_last_error": (ctypes.c_char_p, []),
     "dfm_abi_version": (c_int, []),
+    "dfm_build_tag": (ctypes.c_char_p, []),
     "dfm_gemm_workspace_size": (c_size_t, [ctypes.POINTER(GemmDesc)]),
     "dfm_gemm": (c_int, [c_int, ctypes.POINTER(GemmDesc), P, P, P, P, P]),
     "dfm_gemm_group_workspace_size": (c_size_t, [c_int, ctypes.POINTER(GemmDesc)]),
@@ -191,6 +192,7 @@ def _load():
 
 lib = _load()
 SYMBOLS = tuple(_SIGS)
+BUILD_TAG = lib.dfm_build_tag().decode()
 
 
 def check(status, what):

@@ -9,6 +9,8 @@
 // then the launching pass over the caller's buffers. The same code decides both, so the sizes the
 // *_size functions report are exactly what the launches use.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <math.h>
 #include <string.h>
 
@@ -437,6 +439,8 @@ void block_fwd(Run& r, const Dims& m, const BlockIO& io, V y, V ye) {
   ffn_fwd(r, m, m.fused_ffn, C, m.R, s.x1, p, DFM_BP_MLP_NORM_W, F(p, DFM_BP_LS2), io.rs[1], y, s.ffn);
   if (!m.drop_depth)
     ffn_fwd(r, m, m.fused_e, Ch, m.R / 2, s.xe1, p, DFM_BP_MLPE_NORM_W, F(p, DFM_BP_LS2E), io.rs[3], ye, s.ffne);
+  else if (ye.p && r.live())  // DFormer.py:133, 177-181: x_e leaves a drop_depth Block as e_back's output
+    r.ok(dfm_scale_mul(r.dt, P, Ch, s.xep.p, s.xep.ld, nullptr, 0, nullptr, nullptr, 1, 1.f, ye.p, ye.ld, 0, r.s));
 }
 
 // AttentionFn._backward (functional.py), after both ConvFFN backwards
@@ -454,9 +458,7 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
     dxe1 = r.temp(P, Ch);
     ffn_bwd(r, m, m.fused_e, Ch, m.R / 2, dye, s.xe1, p, DFM_BP_MLPE_NORM_W, F(p, DFM_BP_LS2E), io.rs[3], dxe1, gr,
             DFM_BP_LS2E, s.ffne);
-  } else {
-    dxe1 = dye;  // x_e passed through the Block (may be absent)
-  }
+  }  // with drop_depth the x_e output is e_back's output (no identity path): dye joins dxe' below
   // proj / proj_e: one weight-gradient GEMM each, one input-gradient GEMM over [dp1 | dp1e] when the
   // two weights are stacked in memory
   V df = r.temp(P, fw);
@@ -483,6 +485,8 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
   if (r.live())
     r.ok(dfm_dual_mul(r.dt, P, Ch, df.col(fw - Ch).p, df.ld, s.xep.p, s.xep.ld, cx.p, cx.ld, dcx.p, dcx.ld, dxep.p,
                       dxep.ld, r.s));
+  if (m.drop_depth && dye.p && r.live())
+    r.ok(dfm_scale_mul(r.dt, P, Ch, dye.p, dye.ld, nullptr, 0, nullptr, nullptr, 1, 1.f, dxep.p, dxep.ld, 1, r.s));
   wgrad(r, dxep, P, Ch, s.e2, Ch, gr[DFM_BP_EBACK_W], gr[DFM_BP_EBACK_B]);
   V de2 = r.temp(P, Ch);
   dgrad(r, dxep, P, Ch, p[DFM_BP_EBACK_W], Ch, de2);
@@ -562,6 +566,16 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
                 gr[DFM_BP_NORM_E_B]);
 }
 
+// whether the Block described by m has parameter DFM_BP_i (kv / short_cut_linear need the window; proj_e,
+// the _e layer scales and mlp_e2 are absent with drop_depth)
+bool block_has_param(const Dims& m, int i) {
+  if (!m.window && (i == DFM_BP_KV_W || i == DFM_BP_KV_B || i == DFM_BP_SC_W || i == DFM_BP_SC_B)) return false;
+  if (m.drop_depth && (i == DFM_BP_PROJE_W || i == DFM_BP_PROJE_B || i == DFM_BP_LS1E || i == DFM_BP_LS2E ||
+                       (i >= DFM_BP_MLPE_NORM_W && i <= DFM_BP_MLPE_FC2_B)))
+    return false;
+  return true;
+}
+
 bool desc_ok(int dtype, const DfmBlockDesc* d) {
   return d && (dtype == DFM_F32 || dtype == DFM_BF16 || dtype == DFM_F16) && d->B > 0 && d->H > 0 && d->W > 0 &&
          d->C > 0 && d->C % 16 == 0 && d->hidden > 0 && d->hidden % 16 == 0 &&
@@ -569,19 +583,37 @@ bool desc_ok(int dtype, const DfmBlockDesc* d) {
 }
 
 // sizes of (saved, workspace) for one Block
+// Both parameter layouts are planned (separate q / q_cut / l and proj / proj_e weights, and the stacked ones
+// the training step passes, which run as one GEMM): the planning pass only compares pointers, so the stacked
+// layout is described by placeholder addresses that are never dereferenced.
 void block_sizes(int dtype, const DfmBlockDesc* d, size_t* saved, size_t* ws) {
   const Dims m = dims_of(dtype, d);
-  static const void* const none[DFM_BLOCK_NPARAM] = {};
   static float* const gnone[DFM_BLOCK_NPARAM] = {};
-  BlockIO io{none, {nullptr, nullptr, nullptr, nullptr}, V{nullptr, m.C, 2}, V{nullptr, m.Ch, 2}};
-  Run f(dtype, true, nullptr), b(dtype, true, nullptr);
-  io.x.es = io.xe.es = f.es;
-  block_fwd(f, m, io, V{nullptr, m.C, f.es}, V{nullptr, m.Ch, f.es});
-  block_bwd(b, m, io, V{nullptr, m.C, f.es}, V{nullptr, m.Ch, f.es}, V{nullptr, m.C, f.es}, V{nullptr, m.Ch, f.es},
-            gnone);
-  *saved = f.saved.peak;
-  const size_t tmp = f.tmp.peak > b.tmp.peak ? f.tmp.peak : b.tmp.peak;
-  const size_t scr = f.scratch_need > b.scratch_need ? f.scratch_need : b.scratch_need;
+  const void* none[DFM_BLOCK_NPARAM] = {};
+  const void* stacked[DFM_BLOCK_NPARAM] = {};
+  const size_t es = dtype == DFM_F32 ? 4 : 2;
+  char* const w0 = reinterpret_cast<char*>(size_t(1) << 40);
+  char* const b0 = reinterpret_cast<char*>(size_t(1) << 41);
+  char* const p0 = reinterpret_cast<char*>(size_t(1) << 42);
+  stacked[DFM_BP_Q_W] = w0;
+  stacked[DFM_BP_QCUT_W] = w0 + (size_t)m.C * m.C * es;
+  stacked[DFM_BP_L_W] = w0 + (size_t)(m.C + m.Ch) * m.C * es;
+  stacked[DFM_BP_Q_B] = b0;
+  stacked[DFM_BP_QCUT_B] = b0 + (size_t)m.C * 4;
+  stacked[DFM_BP_L_B] = b0 + (size_t)(m.C + m.Ch) * 4;
+  stacked[DFM_BP_PROJ_W] = p0;
+  stacked[DFM_BP_PROJE_W] = p0 + (size_t)m.C * m.fw * es;
+  size_t sv = 0, tmp = 0, scr = 0;
+  for (const void* const* params : {(const void* const*)none, (const void* const*)stacked}) {
+    BlockIO io{params, {nullptr, nullptr, nullptr, nullptr}, V{nullptr, m.C, es}, V{nullptr, m.Ch, es}};
+    Run f(dtype, true, nullptr), b(dtype, true, nullptr);
+    block_fwd(f, m, io, V{nullptr, m.C, es}, V{nullptr, m.Ch, es});
+    block_bwd(b, m, io, V{nullptr, m.C, es}, V{nullptr, m.Ch, es}, V{nullptr, m.C, es}, V{nullptr, m.Ch, es}, gnone);
+    sv = std::max(sv, f.saved.peak);
+    tmp = std::max({tmp, f.tmp.peak, b.tmp.peak});
+    scr = std::max({scr, f.scratch_need, b.scratch_need});
+  }
+  *saved = sv;
   *ws = tmp + up(scr);
 }
 
@@ -623,6 +655,15 @@ int block_call(bool fwd, int dtype, const DfmBlockDesc* d, const void* const* pa
     dfm_set_error("%s: saved %zu / workspace %zu bytes, %zu / %zu needed", who, saved_bytes, workspace_bytes, need_sv,
                   need_ws);
     return DFM_ERR_ARG;
+  }
+  // every parameter (and, backward, every gradient slot) the Block has must be given: a NULL bias or
+  // bias-gradient pointer would otherwise read as "no bias" / "skip" inside the GEMM epilogue
+  for (int i = 0; i < DFM_BLOCK_NPARAM; ++i) {
+    if (!block_has_param(m, i)) continue;
+    if (!params[i] || (!fwd && !grads[i])) {
+      dfm_set_error("%s: %s entry %d is NULL (the Block has this parameter)", who, params[i] ? "grads" : "params", i);
+      return DFM_ERR_ARG;
+    }
   }
   // the temporaries' peak of THIS direction decides where the scratch starts
   Run p(dtype, true, nullptr);

@@ -9,7 +9,15 @@
 
 namespace {
 constexpr int COLS = 64;       // columns per block in column reductions
-constexpr int RED_BLOCKS = 512;
+// column-reduction geometry: at most DFM_RED_BLOCKS blocks of at least DFM_RED_MIN_ROWS rows (compile-time
+// knobs so a variant build can be A/B'd; dfm_build_tag reports them)
+#ifndef DFM_RED_MIN_ROWS
+#define DFM_RED_MIN_ROWS 256
+#endif
+#ifndef DFM_RED_BLOCKS
+#define DFM_RED_BLOCKS 512
+#endif
+constexpr int RED_BLOCKS = DFM_RED_BLOCKS, RED_MIN_ROWS = DFM_RED_MIN_ROWS;
 
 // part[blk][k][c] for k < NOUT: sum over this block's rows of f_k(row, c)
 template <typename T, int MODE>
@@ -164,7 +172,7 @@ __global__ void colred_sum_kernel(int nblk, int n, const float* __restrict__ par
   out[e] = accumulate ? out[e] + s : s;
 }
 
-int red_blocks(long rows) { return (int)min((long)RED_BLOCKS, max(1L, (rows + 255) / 256)); }
+int red_blocks(long rows) { return (int)min((long)RED_BLOCKS, max(1L, (rows + RED_MIN_ROWS - 1) / RED_MIN_ROWS)); }
 
 template <typename T, int MODE>
 int colred(long rows, int C, const void* x, long ldx, const void* y, long ldy, const float* p0, const float* p1,

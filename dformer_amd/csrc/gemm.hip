@@ -62,6 +62,11 @@ extern "C" int dfm_gemm(int dtype, const DfmGemmDesc* d, const void* A, const vo
 
 extern "C" size_t dfm_gemm_group_workspace_size(int n, const DfmGemmDesc* d) {
   if (n < 1 || n > GMAX || d == nullptr) return 0;
+  if (d[0].a_kcontig) {  // forward / input-gradient groups: ring members run unsplit, the rest one by one
+    size_t one = 0;
+    for (int q = 0; q < n; ++q) one = std::max(one, dfm_gemm_workspace_size(&d[q]));
+    return one;
+  }
   int splits[GMAX];
   group_splits(n, d, splits);
   size_t total = 0, one = 0;

@@ -25,7 +25,23 @@ void dfm_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* dfm_last_error(void) { return g_err; }
-extern "C" int dfm_abi_version(void) { return 11; }  // 11: dfm_block_fwd / _bwd; 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
+extern "C" int dfm_abi_version(void) { return 12; }  // 12: dfm_build_tag; 11: dfm_block_fwd / _bwd; 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
+#ifndef DFM_BUILD_TAG
+#define DFM_BUILD_TAG "default"
+#endif
+#ifndef DFM_RED_MIN_ROWS
+#define DFM_RED_MIN_ROWS 256
+#endif
+#ifndef DFM_RED_BLOCKS
+#define DFM_RED_BLOCKS 512
+#endif
+#define DFM_STR2(x) #x
+#define DFM_STR(x) DFM_STR2(x)
+// names the build a process loaded (variant builds set DFM_BUILD_TAG and the compile-time knobs on the
+// make line), so an A/B or diagnostic run records which library it measured
+extern "C" const char* dfm_build_tag(void) {
+  return DFM_BUILD_TAG " red=" DFM_STR(DFM_RED_BLOCKS) "x" DFM_STR(DFM_RED_MIN_ROWS);
+}
 
 // ---------------------------------------------------------------- launch tracer
 // dfm_trace_flags is read by DFM_LAUNCH (common.h) before every kernel launch; 0 = tracer off and

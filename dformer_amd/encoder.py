@@ -170,7 +170,7 @@ class Block(nn.Module):
         if self.drop_depth:
             K.TAG = st + ".mlp"
             x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
-            return x2.view(B, H, W, C), x_e
+            return x2.view(B, H, W, C), xe1.view(B, H, W, C // 2)  # DFormer.py:177-181: e_back's output
         # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
         # does its backward: autograd replays a node on its forward's stream), which fills the GPU
         # at the late stages where each kernel alone is latency-bound

@@ -188,7 +188,16 @@ def _cat1(*vs):
 # stage 1 on, tools/ffn_kernels_bench.py); False routes every ConvFFN through the op-level chain below
 # (tests compare them; DFM_FUSED_FFN=0|1|fwd|auto sets the default for A/B runs)
 FUSED_FWD_MIN_PLANE = 16384
-FUSED_FFN = {"0": False, "1": True}.get(os.environ.get("DFM_FUSED_FFN", "auto"), os.environ.get("DFM_FUSED_FFN", "auto"))
+_FUSED_FFN_MODES = {"0": False, "1": True, "fwd": "fwd", "auto": "auto"}
+
+
+def _fused_ffn_mode(v):
+    if v not in _FUSED_FFN_MODES:
+        raise ValueError(f"DFM_FUSED_FFN={v!r}: expected one of {sorted(_FUSED_FFN_MODES)}")
+    return _FUSED_FFN_MODES[v]
+
+
+FUSED_FFN = _fused_ffn_mode(os.environ.get("DFM_FUSED_FFN", "auto"))
 
 
 class ConvFFNFn(torch.autograd.Function):
@@ -346,8 +355,9 @@ class AttentionFn(torch.autograd.Function):
         x1 = torch.empty(P, C, device=dev, dtype=dt)
         calls = [lambda c: K.linear(f, wcast(dt, wp), bp, preact=p1, res=x, colscale=ls1, rowscale=rowscale,
                                     rows_per_scale=rps, out=x1, collect=c)]
-        if drop_depth:
-            xe1, p1e = xe, None
+        if drop_depth:  # DFormer.py:133, 141-145: x_e leaves the Block as e_back's output (no proj_e)
+            xe1, p1e = xep, None
+            ctx.set_materialize_grads(False)  # the encoder discards it: no zero-filled gradient pass
         else:
             p1e = torch.empty(P, Ch, device=dev, dtype=dt)
             xe1 = torch.empty(P, Ch, device=dev, dtype=dt)
@@ -385,14 +395,14 @@ class AttentionFn(torch.autograd.Function):
         rps = H * W
         fw = f.shape[1]
         grads = {}
-        dx1 = dx1.contiguous()
+        dx1 = dx1.contiguous() if dx1 is not None else torch.zeros_like(x)
         # projections: proj and proj_e read the same f, so their backward runs as ONE weight-gradient
         # GEMM and ONE input-gradient GEMM over [dp1 | dp1e] (K = C + C/2) against [Wp; Wpe]
         if drop_depth:
             dp1, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps)
             grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, out=gslot2(wp), bias_grad=True, bias_out=gslot(bp))
             df = K.linear_dgrad(dp1, wcast(dt, wp))
-            dxe_res = dxe1.contiguous() if dxe1 is not None else None
+            dxe_res = None  # x_e's output is xe' (no identity path), its gradient joins dxe' below
         else:
             dxe1 = dxe1.contiguous()
             dpc = torch.empty(P, C + Ch, device=dev, dtype=dt)
@@ -413,6 +423,8 @@ class AttentionFn(torch.autograd.Function):
         def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))
             dcxe = df[:, fw - Ch:]
             _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
+            if drop_depth and dxe1 is not None:  # the Block's x_e output is xe' itself
+                K.scale_mul(dxe1.contiguous(), out=dxep, accumulate=True)
             ow, ob = gslot2(web), gslot(beb)
             grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=ow, bias_grad=True, bias_out=ob)
             de2 = K.linear_dgrad(dxep, wcast(dt, web))
@@ -427,7 +439,7 @@ class AttentionFn(torch.autograd.Function):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 dxen, side_tmp = depth_branch()
-            for t in (df, xep, cx, e2, e1, xen, dqcl):
+            for t in (df, xep, cx, e2, e1, xen, dqcl) + ((dxe1,) if drop_depth and dxe1 is not None else ()):
                 t.record_stream(side)
         else:
             dxen, _ = depth_branch()

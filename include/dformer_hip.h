@@ -39,10 +39,13 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
+int dfm_abi_version(void); /* 12: dfm_build_tag; 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
                               dfm_block_workspace_size); 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
                               second stages (dfm_partial_sum_group); 7: DfmGemmDesc.workspace_bytes + stride /
                               leading-dimension validation */
+/* The build this process loaded: "default" (or a variant build's DFM_BUILD_TAG) and its compile-time
+ * reduction geometry, e.g. "default red=512x256" (at most 512 column-reduction blocks of >= 256 rows). */
+const char* dfm_build_tag(void);
 
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
@@ -232,13 +235,15 @@ int dfm_convffn_bwd(int dtype, const DfmConvFFNDesc* d, const void* dout, const 
  *   weights, layer scales) float32. Entries the Block does not have are ignored (kv / short_cut_linear
  *   without a window; proj_e, layer_scale_1_e / _2_e and mlp_e2 with drop_depth).
  *   Contiguous q | q_cut | l (weights and biases, in that order) run as one GEMM, as the training step does.
- * grads: the same indexing, float32 [same shape] (overwritten; NULL entries are not allowed for
+ * grads: the same indexing, float32 [same shape] (overwritten; NULL entries are rejected for
  *   parameters the Block has).
  * rowscale: NULL, or 4 float32 [B] pointers (each may be NULL = 1): the per-sample DropPath scales
  *   (keep mask / keep prob) of, in mmcv's call order, attn x, mlp x, attn x_e, mlp x_e.
  * The forward writes `saved` (dfm_block_saved_size bytes) for the backward, which also reads x and
- * xe again; both use `workspace` (dfm_block_workspace_size bytes) as scratch. With drop_depth, x_e
- * passes through: ye is not written (may be NULL) and dye may be NULL (no gradient from above).
+ * xe again; both use `workspace` (dfm_block_workspace_size bytes) as scratch. With drop_depth the x_e
+ * output is the attention's e_back result (no proj_e / residual / mlp_e2; DFormer.py:133, 177-181): ye
+ * receives it when non-NULL, and dye, when non-NULL, flows back through e_back (the encoder discards
+ * the last Block's x_e, so both may be NULL). NULL params / grads entries the Block has: DFM_ERR_ARG.
  * fused_ffn: ConvFFNs with fused kernels (dfm_convffn_supported) run dfm_convffn_fwd / _bwd. */
 typedef struct DfmBlockDesc {
   int B, H, W, C;

@@ -81,7 +81,10 @@ def make_block(model, stage, last=False, drop_prob=0.0):
                          drop_depth=(stage == 3 and last))
 
 
-def golden_block(name, model, stage, B, H, W, last=False, drop_prob=0.0, masks=None):
+def golden_block(name, model, stage, B, H, W, last=False, drop_prob=0.0, masks=None, with_ye=False):
+    """One Block's output, input gradients and parameter gradients (fp64) under a seeded linear loss.
+    with_ye (a drop_depth Block): x_e's output (the attention's e_back result, DFormer.py:133, 141-145,
+    177-181) is in the loss and stored too, although the encoder discards it after the last Block."""
     C = MODELS[model]["dims"][stage]
     blk = make_block(model, stage, last, drop_prob)
     load_weights(blk)
@@ -95,7 +98,7 @@ def golden_block(name, model, stage, B, H, W, last=False, drop_prob=0.0, masks=N
     gy = gen.normal(name + "/gy", y.shape)
     loss = (y * t(gy, False)).sum()
     extra = {}
-    if not last:
+    if not last or with_ye:
         gye = gen.normal(name + "/gye", ye.shape)
         loss = loss + (ye * t(gye, False)).sum()
         extra["y_e"] = ye.detach().numpy().astype(np.float32)
@@ -415,6 +418,8 @@ def main():
         ("block_tiny_s1", "tiny", 1, 2, 11, 13, False),
         ("block_tiny_s3_last", "tiny", 3, 2, 5, 7, True),
         ("block_base_s0", "base", 0, 1, 16, 20, False),
+        # the stage-0 plane of a 480x640 image (19,200 pixels): the fused ConvFFN's "auto" mode runs here
+        ("block_base_s0_120x160", "base", 0, 1, 120, 160, False),
         ("block_base_s1", "base", 1, 2, 15, 20, False),
         ("block_base_s2", "base", 2, 2, 9, 10, False),
         ("block_base_s3", "base", 3, 2, 8, 10, False),
@@ -428,6 +433,8 @@ def main():
     for n, mdl, st, B, H, W, last in blocks:
         if want(n):
             golden_block(n, mdl, st, B, H, W, last)
+    if want("block_tiny_s3_last_ye"):
+        golden_block("block_tiny_s3_last_ye", "tiny", 3, 2, 5, 7, True, with_ye=True)
     if want("block_droppath"):
         # DropPath with injected keep masks: 6 DropPath calls per block (x/xe × attn/mlp … order of Block.forward)
         masks = [np.array([1.0, 0.0]), np.array([0.0, 1.0]), np.array([1.0, 1.0]), np.array([0.0, 1.0])]
@@ -455,7 +462,7 @@ def main():
     if want("bf16env_block"):
         for n, mdl, st, B, H, W, last in blocks:
             if n in ("block_tiny_s1", "block_base_s0", "block_base_s1", "block_base_s2", "block_base_s3",
-                     "block_base_s3_last", "block_large_s2"):
+                     "block_base_s3_last", "block_large_s2", "block_base_s0_120x160"):
                 golden_block_bf16_env(n, mdl, st, B, H, W, last)
     if want("bf16env") and not which == ["bf16env_block"]:
         golden_bf16_env("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)

@@ -42,7 +42,8 @@ def test_binding_signatures_match_header():
 
 def test_abi_version_and_error_path():
     from dformer_amd import _lib
-    assert _lib.lib.dfm_abi_version() == 11
+    assert _lib.lib.dfm_abi_version() == 12
+    assert _lib.BUILD_TAG.startswith("default red="), _lib.BUILD_TAG
     # argument validation fails before touching the GPU
     st = _lib.lib.dfm_layernorm_fwd(0, 10, 100000, None, 0, None, None, 1e-6, None, 0, None, None, None)
     assert st == -1

@@ -75,27 +75,28 @@ def run_capi(name, dtype, stack_qcl=False, fused_ffn=0, droppath=None):
     xe = torch.from_numpy(gen.normal(name + "/xe", (B, H, W, C // 2))).to("cuda", dtype).contiguous()
     y = torch.empty_like(x)
     ye = torch.empty_like(xe)
+    with_ye = "y_e" in g  # every Block with an x_e output; a drop_depth Block's e_back output (*_ye goldens)
     nsv = _lib.lib.dfm_block_saved_size(code, d)
     nws = _lib.lib.dfm_block_workspace_size(code, d)
     assert nsv > 0 and nws > 0
     saved = torch.empty(nsv, dtype=torch.uint8, device="cuda")
     ws = torch.empty(nws, dtype=torch.uint8, device="cuda")
     st = _lib.lib.dfm_block_fwd(code, d, params, rs, x.data_ptr(), xe.data_ptr(), y.data_ptr(),
-                                None if last else ye.data_ptr(), saved.data_ptr(), nsv, ws.data_ptr(), nws, _stream())
+                                ye.data_ptr() if with_ye else None, saved.data_ptr(), nsv, ws.data_ptr(), nws, _stream())
     assert st == 0, _lib.lib.dfm_last_error()
     gy = torch.from_numpy(gen.normal(name + "/gy", y.shape)).to("cuda", dtype).contiguous()
-    gye = None if last else torch.from_numpy(gen.normal(name + "/gye", ye.shape)).to("cuda", dtype).contiguous()
+    gye = torch.from_numpy(gen.normal(name + "/gye", ye.shape)).to("cuda", dtype).contiguous() if with_ye else None
     dx, dxe = torch.empty_like(x), torch.empty_like(xe)
     st = _lib.lib.dfm_block_bwd(code, d, params, rs, x.data_ptr(), xe.data_ptr(), saved.data_ptr(), nsv, gy.data_ptr(),
                                 None if gye is None else gye.data_ptr(), dx.data_ptr(), dxe.data_ptr(), grads,
                                 ws.data_ptr(), nws, _stream())
     assert st == 0, _lib.lib.dfm_last_error()
     torch.cuda.synchronize()
-    return g, last, y, (None if last else ye), dx, dxe, gbuf
+    return g, not with_ye, y, (ye if with_ye else None), dx, dxe, gbuf
 
 
 CASES = [("block_base_s0", False), ("block_base_s2", False), ("block_base_s2", True), ("block_base_s3_last", False),
-         ("block_tiny_s1", True)]
+         ("block_tiny_s1", True), ("block_tiny_s3_last_ye", False)]
 
 
 @pytest.mark.parametrize("name,stack", CASES)
@@ -143,3 +144,49 @@ def test_block_capi_bf16_vs_autograd_path(name, fused):
         if not np.isfinite(e) or e > 2e-2:
             bad[n] = e
     assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["block_base_s0", "block_base_s2", "block_base_s3_last", "block_base_s0_120x160"])
+@pytest.mark.parametrize("fused", [0, 1])
+def test_block_capi_bf16_vs_reference_goldens(name, fused):
+    """bf16 through the C ABI alone, op-level or fused ConvFFNs, against the REFERENCE golden at the same
+    per-tensor gates as the autograd Block (4x the reference's own bf16 error, tests/test_block_gpu.py)."""
+    from test_block_gpu import bf16_envelope_check
+    g, last, y, ye, dx, dxe, grads = run_capi(name, torch.bfloat16, stack_qcl=True, fused_ffn=fused)
+    for n, t in grads.items():
+        assert torch.isfinite(t).all(), n
+    bf16_envelope_check(name, f"capi-fused{fused}", g, y, ye, dx, dxe, grads, last)
+
+
+@pytest.mark.parametrize("which", ["params", "grads"])
+def test_block_capi_rejects_null_entries(which):
+    """A NULL params / grads entry for a parameter the Block has (a bias, a bias gradient) is DFM_ERR_ARG
+    before any launch; entries the Block does not have (kv without a window) may stay NULL."""
+    from dformer_amd import _lib
+    g, blk, (B, H, W, C, stage, last, dp) = _meta("block_base_s0")  # window 0: no kv / short_cut_linear
+    sd = {k: v.detach().float().cuda() for k, v in blk.state_dict().items()}
+    d = _lib.BlockDesc(B, H, W, C, blk.attn.num_head, blk.attn.window, sd["mlp.fc1.weight"].shape[0], 0, 0, 1e-6)
+    params = (ctypes.c_void_p * len(_lib.BLOCK_PARAM_NAMES))()
+    grads = (ctypes.c_void_p * len(_lib.BLOCK_PARAM_NAMES))()
+    keep = []
+    for i, n in enumerate(_lib.BLOCK_PARAM_NAMES):
+        if n in sd:
+            keep += [sd[n].contiguous(), torch.zeros_like(sd[n])]
+            params[i], grads[i] = keep[-2].data_ptr(), keep[-1].data_ptr()
+    victim = _lib.BLOCK_PARAM_NAMES.index("attn.q.bias")
+    (params if which == "params" else grads)[victim] = None
+    x = torch.zeros(B * H * W, C, device="cuda")
+    xe = torch.zeros(B * H * W, C // 2, device="cuda")
+    nsv, nws = _lib.lib.dfm_block_saved_size(_lib.F32, d), _lib.lib.dfm_block_workspace_size(_lib.F32, d)
+    saved = torch.zeros(nsv, dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(nws, dtype=torch.uint8, device="cuda")
+    y, ye = torch.empty_like(x), torch.empty_like(xe)
+    if which == "params":
+        st = _lib.lib.dfm_block_fwd(_lib.F32, d, params, None, x.data_ptr(), xe.data_ptr(), y.data_ptr(),
+                                    ye.data_ptr(), saved.data_ptr(), nsv, ws.data_ptr(), nws, _stream())
+    else:
+        st = _lib.lib.dfm_block_bwd(_lib.F32, d, params, None, x.data_ptr(), xe.data_ptr(), saved.data_ptr(), nsv,
+                                    y.data_ptr(), ye.data_ptr(), x.data_ptr(), xe.data_ptr(), grads, ws.data_ptr(),
+                                    nws, _stream())
+    assert st != 0
+    assert f"entry {victim} is NULL".encode() in _lib.lib.dfm_last_error()

@@ -13,7 +13,7 @@ from goldens import MODELS, RATIOS, check_param_grads, load, rel_err
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BLOCKS = ["block_tiny_s0", "block_tiny_s1", "block_tiny_s3_last", "block_base_s0", "block_base_s1",
           "block_base_s2", "block_base_s3", "block_base_s3_last", "block_large_s1", "block_large_s2",
-          "block_droppath_base_s1"]
+          "block_droppath_base_s1", "block_tiny_s3_last_ye", "block_base_s0_120x160"]
 
 
 def make_block(name, device="cpu"):
@@ -54,13 +54,13 @@ def run_block(name, dtype):
     xe = torch.from_numpy(gen.normal(name + "/xe", (B, H, W, C // 2))).to("cuda", dtype).requires_grad_()
     y, ye = blk(x, xe)
     gy = torch.from_numpy(gen.normal(name + "/gy", y.shape)).to("cuda", dtype)
-    if last:
+    if "y_e" not in g:  # a drop_depth Block whose x_e output the golden's loss leaves out
         y.backward(gy)
-    else:
+    else:  # every other Block, and a drop_depth Block's e_back output (DFormer.py:133, 177-181; *_ye)
         gye = torch.from_numpy(gen.normal(name + "/gye", ye.shape)).to("cuda", dtype)
         torch.autograd.backward([y, ye], [gy, gye])
     torch.cuda.synchronize()
-    return g, blk, x, xe, y, ye, last
+    return g, blk, x, xe, y, ye, "y_e" not in g
 
 
 @pytest.mark.gpu
@@ -87,25 +87,58 @@ BF16_ENV_MULT = 4.0
 BF16_FLOOR = 2.0 ** -8
 
 
+BF16_BLOCKS = ["block_tiny_s1", "block_base_s0", "block_base_s1", "block_base_s2", "block_base_s3",
+               "block_base_s3_last", "block_large_s2", "block_base_s0_120x160"]
+# ConvFFN routes (functional.FUSED_FFN): the op-level chain, the fused forward + op-level backward, fused
+# forward + fused backward, each forced onto every Block (plane threshold 0) so the small golden planes take
+# the fused kernels too; and the default "auto" (fused forward on planes of >= FUSED_FWD_MIN_PLANE pixels)
+# on the 480x640 stage-0 plane, the route the bench runs
+FFN_CASES = [(n, m) for n in BF16_BLOCKS for m in (False, "fwd", True)] + [("block_base_s0_120x160", "auto")]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["block_tiny_s1", "block_base_s0", "block_base_s1", "block_base_s2",
-                                  "block_base_s3", "block_base_s3_last", "block_large_s2"])
-def test_block_bf16_vs_reference_goldens(name):
+@pytest.mark.parametrize("name,ffn", FFN_CASES)
+def test_block_bf16_vs_reference_goldens(name, ffn, monkeypatch):
     """bf16 per Block: forward also within 1e-2 rel-to-max; forward, input gradients and
-    EVERY parameter gradient within BF16_ENV_MULT x the reference's own bf16 envelope."""
-    from goldens import fp_rel_err
+    EVERY parameter gradient within BF16_ENV_MULT x the reference's own bf16 envelope, on every ConvFFN
+    route; the fused kernels must actually run where the route and the shape select them."""
+    from dformer_amd import functional as Fn, kernels as Kk
+    monkeypatch.setattr(Fn, "FUSED_FFN", ffn)
+    if ffn != "auto":
+        monkeypatch.setattr(Fn, "FUSED_FWD_MIN_PLANE", 0)
+    calls = {"fwd": 0, "bwd": 0}
+    for which in ("fwd", "bwd"):
+        orig = getattr(Kk, "convffn_" + which)
+
+        def counted(*a, _o=orig, _w=which, **k):
+            calls[_w] += 1
+            return _o(*a, **k)
+        monkeypatch.setattr(Kk, "convffn_" + which, counted)
     g, blk, x, xe, y, ye, last = run_block(name, torch.bfloat16)
+    B, H, W, C, stage = [int(v) for v in g["meta"][:5]]
+    supported = any(Kk.convffn_supported(torch.bfloat16, (B, H, W), c, RATIOS[stage] * c)
+                    for c in ((C,) if last else (C, C // 2)))
+    fused_fwd = supported and (ffn in ("fwd", True) or (ffn == "auto" and H * W >= Fn.FUSED_FWD_MIN_PLANE))
+    assert (calls["fwd"] > 0) == fused_fwd, (calls, supported)
+    assert (calls["bwd"] > 0) == (supported and ffn is True), (calls, supported)
+    grads = {k: p.grad for k, p in blk.named_parameters() if p.grad is not None}
+    bf16_envelope_check(name, f"ffn-{ffn}", g, y, ye, x.grad, xe.grad, grads, last)
+
+
+def bf16_envelope_check(name, tag, g, y, ye, gx, gxe, grads, last):
+    """Gate one bf16 Block's outputs / input gradients / parameter gradients against the reference golden at
+    BF16_ENV_MULT x the reference's own bf16 error (bf16env_<name>), floored at one bf16 rounding."""
+    from goldens import fp_rel_err
     env = load("bf16env_" + name)
 
     def gate(key):
         return BF16_ENV_MULT * max(float(env["env/" + key]), BF16_FLOOR)
 
-    errs = {"y": rel_err(y.float().cpu(), g["y"]), "gx": rel_err(x.grad.float().cpu(), g["gx"])}
+    errs = {"y": rel_err(y.float().cpu(), g["y"]), "gx": rel_err(gx.float().cpu(), g["gx"])}
     if not last:
         errs["y_e"] = rel_err(ye.float().cpu(), g["y_e"])
-        errs["gxe"] = rel_err(xe.grad.float().cpu(), g["gxe"])
+        errs["gxe"] = rel_err(gxe.float().cpu(), g["gxe"])
     assert errs["y"] < 1e-2 and errs.get("y_e", 0.0) < 1e-2, errs
-    grads = {k: p.grad for k, p in blk.named_parameters() if p.grad is not None}
     for k in env:
         if k.startswith("env/grad/"):
             n = k[len("env/grad/"):]
@@ -116,10 +149,10 @@ def test_block_bf16_vs_reference_goldens(name):
                 errs["grad/" + n] = fp_rel_err(gen.fingerprint(a.numpy(), 256), g["gradfp/" + n])
     ratios = {k: v / max(float(env["env/" + k]), BF16_FLOOR) for k, v in errs.items()}
     worst = max(ratios, key=ratios.get)
-    print(f"{name}: worst {worst} err {errs[worst]:.3e} = {ratios[worst]:.2f} x envelope")
+    print(f"{name} {tag}: worst {worst} err {errs[worst]:.3e} = {ratios[worst]:.2f} x envelope")
     out = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(out):  # the measured ratios, for DESIGN.md (GPU box runs only)
-        with open(os.path.join(out, f"bf16env_ratios_{name}.json"), "w") as fh:
+        with open(os.path.join(out, f"bf16env_ratios_{name}_{tag}.json"), "w") as fh:
             json.dump({"errs": errs, "ratios": ratios, "mult": BF16_ENV_MULT, "floor": BF16_FLOOR}, fh, indent=1)
     bad = {k: (errs[k], gate(k)) for k in errs if errs[k] >= gate(k)}
     assert not bad, bad

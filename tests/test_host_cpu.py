@@ -147,3 +147,15 @@ def test_chain_order_overlapping_chains():
     assert sorted(id(p) for p in order) == sorted(id(p) for p in (a, b, c))
     order = _chain_order([b, c, d], [[a, c, d]])  # head a not present: no regrouping
     assert [id(p) for p in order] == [id(b), id(c), id(d)]
+
+
+def test_fused_ffn_env_values_are_validated():
+    """DFM_FUSED_FFN maps through an explicit table; an unknown value (e.g. 'off') raises instead of
+    silently selecting a fused route."""
+    import pytest
+    from dformer_amd.functional import _fused_ffn_mode
+    assert _fused_ffn_mode("0") is False and _fused_ffn_mode("1") is True
+    assert _fused_ffn_mode("fwd") == "fwd" and _fused_ffn_mode("auto") == "auto"
+    for bad in ("off", "false", "true", "2", ""):
+        with pytest.raises(ValueError):
+            _fused_ffn_mode(bad)

@@ -518,6 +518,41 @@ def test_batchnorm_shifted_stats_large_offset(C):
     assert rel(y.double(), ref) < 1e-3
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("rows", [1, 63, 64, 65, 192, 193, 255, 256, 257, 511, 4801, 76801, 131073, 300001])
+def test_column_reductions_block_tails(dt, rows):
+    """colsum (with multiplier and per-image row scale), BN statistics and BN backward statistics at row
+    counts that split into several blocks with partial tails (any block count / rows-per-block geometry the
+    build was compiled with, dfm_build_tag), on a strided view: each against float64 on the same
+    operands, bounded by the fp32 summation error relative to sum|terms| (conditioning-free)."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(rows)
+    for C in (16, 48, 72, 512):
+        base = (torch.randn(rows, C + 8, device=DEV, generator=g) * 3 + 1).to(dt)
+        x = base[:, 8:]  # a strided view; C = 48 / 72 take the scalar kernel, 16 / 512 the vector one
+        y = torch.randn(rows, C, device=DEV, generator=g).to(dt)
+        rps = max(1, rows // 3)
+        rs = torch.rand((rows + rps - 1) // rps, device=DEV, generator=g)
+        xd, yd = x.double(), y.double()
+        bound = 1e-6 * max(1.0, math.sqrt(rows))
+
+        def chk(got, terms):
+            err = ((got.double() - terms.sum(0)).abs() / terms.abs().sum(0).clamp_min(1e-30)).max().item()
+            assert err < bound, (C, err, bound)
+
+        chk(k.colsum(x, mul=y, rowscale=rs, rows_per_scale=rps), xd * yd * rs.double().repeat_interleave(rps)[:rows, None])
+        st = k.bn_stats(x)
+        sh = xd - xd[0]
+        chk(st[0], sh)
+        chk(st[1], sh * sh)
+        assert torch.equal(st[2], x[0].float())
+        mean = torch.randn(C, device=DEV, generator=g)
+        rstd = torch.rand(C, device=DEV, generator=g) + 0.5
+        s2 = k.bn_bwd_stats(x, y, mean, rstd)
+        chk(s2[0], yd)
+        chk(s2[1], yd * (xd - mean.double()) * rstd.double())
+
+
 def test_nmf_update_softmax():
     k = K()
     a, num, den = (torch.rand(4, 100, 64, device=DEV) for _ in range(3))
@@ -635,6 +670,143 @@ def test_dual_mul(dt, C):
     o1, o2 = k.dual_mul(src, m1, m2, out1=outb[:, :C], out2=outb[:, C + 8:2 * C + 8])
     assert rel(o1.float(), src.float() * m1.float()) < TOL[dt]
     assert rel(o2.float(), src.float() * m2.float()) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("fwd", [True, False])
+def test_gemm_group_kcontig_mixed_members(dt, fwd):
+    """dfm_gemm_group over k-contiguous-A problems (a Block phase's grouped forward / input-gradient
+    launch): the ring-kernel members (aligned, K >= 128) run as ONE gemm_glds_group_kernel launch, the
+    rest (K < 128, a misaligned A view, a bias-gradient column) on their single-GEMM route. Ragged M,
+    N % 64 != 0 and the Block's epilogues (act 3 from act_col0 with GELU' saved, mul + preact, residual +
+    colscale + rowscale, beta = 1; for input gradients the GELU'-multiplier and accumulate), each against
+    torch fp32 and against the same problem launched alone."""
+    k = K()
+    M = 1999
+    g = torch.Generator(device=DEV).manual_seed(7 + int(fwd))
+
+    def rn(*s, scale=1.0):
+        return (torch.randn(*s, device=DEV, generator=g) * scale).to(dt)
+
+    probs = []  # (thunk(collect, out_dict) -> None, reference dict)
+    if fwd:
+        def p_act3(c, o):
+            x, w, b = P["x1"], P["w1"], P["b1"]
+            o["y"] = torch.empty(M, 200, device=DEV, dtype=dt)
+            o["pre"] = torch.empty(M, 64, device=DEV, dtype=dt)
+            k.linear(x, w, b, act=3, preact=o["pre"], act_col0=136, out=o["y"], collect=c)
+
+        def r_act3():
+            lin = P["x1"].float() @ P["w1"].float().t() + P["b1"]
+            p = lin[:, 136:].clone().requires_grad_()
+            F.gelu(p).sum().backward()
+            return {"y": torch.cat([lin[:, :136], F.gelu(lin[:, 136:])], 1), "pre": p.grad}
+
+        def p_mul(c, o):
+            o["y"] = torch.empty(M, 136, device=DEV, dtype=dt)
+            o["pre"] = torch.empty(M, 136, device=DEV, dtype=dt)
+            k.linear(P["x2"], P["w2"], P["b2"], mul=P["m2"], preact=o["pre"], out=o["y"], collect=c)
+
+        def r_mul():
+            lin = P["x2"].float() @ P["w2"].float().t() + P["b2"]
+            return {"y": lin * P["m2"].float(), "pre": lin}
+
+        def p_res(c, o):
+            o["y"] = torch.empty(M, 96, device=DEV, dtype=dt)
+            k.linear(P["x3"], P["w3"], P["b3"], res=P["r3"], colscale=P["ls"], rowscale=P["rs"], rows_per_scale=700,
+                     out=o["y"], collect=c)
+
+        def r_res():
+            lin = P["x3"].float() @ P["w3"].float().t() + P["b3"]
+            return {"y": P["r3"].float() + P["ls"] * P["rs"].repeat_interleave(700)[:M, None] * lin}
+
+        def p_short(c, o):  # K = 64 < 128: not a ring member
+            o["y"] = torch.empty(M, 72, device=DEV, dtype=dt)
+            k.linear(P["x4"], P["w4"], P["b4"], out=o["y"], collect=c)
+
+        def r_short():
+            return {"y": P["x4"].float() @ P["w4"].float().t() + P["b4"]}
+
+        def p_misal(c, o):  # an A view 2 bytes off 16-byte alignment: not a ring member
+            o["y"] = torch.empty(M, 80, device=DEV, dtype=dt)
+            k.linear(P["x5"][:, 1:193], P["w5"], None, out=o["y"], collect=c)
+
+        def r_misal():
+            return {"y": P["x5"][:, 1:193].float() @ P["w5"].float().t()}
+
+        def p_beta(c, o):  # beta = 1 onto a pre-filled output
+            o["y"] = P["y6"].clone()
+            k.linear(P["x6"], P["w6"], P["b6"], out=o["y"], beta=1.0, collect=c)
+
+        def r_beta():
+            return {"y": P["y6"].float() + P["x6"].float() @ P["w6"].float().t() + P["b6"]}
+
+        def p_colsum(c, o):  # bias-gradient column (sum over k of each A row): not a ring member
+            o["y"] = torch.empty(M, 88, device=DEV, dtype=dt)
+            o["cs"] = torch.empty(M, device=DEV, dtype=torch.float32)
+            x, w = P["x7"], P["w7"]
+            k.gemm(x, w, M=M, N=88, K=256, a_kcontig=True, b_kcontig=True, lda=k.ld(x), ldb=k.ld(w), out=o["y"],
+                   ldc=88, colsum=o["cs"], collect=c)
+
+        def r_colsum():
+            return {"y": P["x7"].float() @ P["w7"].float().t(), "cs": P["x7"].float().sum(1)}
+
+        P = dict(x1=rn(M, 256), w1=rn(200, 256, scale=0.06), b1=torch.randn(200, device=DEV, generator=g),
+                 x2=rn(M, 192), w2=rn(136, 192, scale=0.07), b2=torch.randn(136, device=DEV, generator=g),
+                 m2=rn(M, 136), x3=rn(M, 320), w3=rn(96, 320, scale=0.05), b3=torch.randn(96, device=DEV, generator=g),
+                 r3=rn(M, 96), ls=torch.rand(96, device=DEV, generator=g), rs=torch.rand(3, device=DEV, generator=g),
+                 x4=rn(M, 64), w4=rn(72, 64, scale=0.1), b4=torch.randn(72, device=DEV, generator=g),
+                 x5=rn(M, 200), w5=rn(80, 192, scale=0.07), x6=rn(M, 128), w6=rn(104, 128, scale=0.08),
+                 b6=torch.randn(104, device=DEV, generator=g), y6=rn(M, 104), x7=rn(M, 256), w7=rn(88, 256, scale=0.06))
+        probs = [(p_act3, r_act3), (p_mul, r_mul), (p_res, r_res), (p_short, r_short), (p_misal, r_misal),
+                 (p_beta, r_beta), (p_colsum, r_colsum)]
+    else:
+        def p_plain(c, o):
+            o["y"] = torch.empty(M, 200, device=DEV, dtype=dt)
+            k.linear_dgrad(P["d1"], P["w1"], out=o["y"], collect=c)
+
+        def r_plain():
+            return {"y": P["d1"].float() @ P["w1"].float()}
+
+        def p_gg(c, o):  # times GELU'(h)
+            o["y"] = torch.empty(M, 136, device=DEV, dtype=dt)
+            k.linear_dgrad(P["d2"], P["w2"], out=o["y"], gelu_grad_of=P["h2"], collect=c)
+
+        def r_gg():
+            hf = P["h2"].float()
+            gg = 0.5 * (1 + torch.erf(hf / math.sqrt(2))) + hf * torch.exp(-0.5 * hf * hf) / math.sqrt(2 * math.pi)
+            return {"y": (P["d2"].float() @ P["w2"].float()) * gg}
+
+        def p_acc(c, o):
+            o["y"] = P["y3"].clone()
+            k.linear_dgrad(P["d3"], P["w3"], out=o["y"], accumulate=True, collect=c)
+
+        def r_acc():
+            return {"y": P["y3"].float() + P["d3"].float() @ P["w3"].float()}
+
+        def p_short(c, o):  # K = 64: not a ring member
+            o["y"] = torch.empty(M, 72, device=DEV, dtype=dt)
+            k.linear_dgrad(P["d4"], P["w4"], out=o["y"], collect=c)
+
+        def r_short():
+            return {"y": P["d4"].float() @ P["w4"].float()}
+
+        P = dict(d1=rn(M, 256), w1=rn(256, 200, scale=0.06), d2=rn(M, 192), w2=rn(192, 136, scale=0.07),
+                 h2=rn(M, 136), d3=rn(M, 320), w3=rn(320, 96, scale=0.05), y3=rn(M, 96), d4=rn(M, 64),
+                 w4=rn(64, 72, scale=0.1))
+        probs = [(p_plain, r_plain), (p_gg, r_gg), (p_acc, r_acc), (p_short, r_short)]
+    grouped = [dict() for _ in probs]
+    k.gemm_many([lambda c, f=f, o=o: f(c, o) for (f, _), o in zip(probs, grouped)])
+    single = [dict() for _ in probs]
+    for (f, _), o in zip(probs, single):
+        k.gemm_many([lambda c, f=f, o=o: f(c, o)])
+    torch.cuda.synchronize()
+    ulp = {torch.bfloat16: 2.0 ** -7, torch.float16: 2.0 ** -10}[dt]
+    for i, ((f, ref), og, os_) in enumerate(zip(probs, grouped, single)):
+        want = ref()
+        for key, w in want.items():
+            assert rel(og[key].float(), w) < GTOL[dt] * (2 if key == "pre" else 1), (i, f.__name__, key)
+            assert rel(og[key].float(), os_[key].float()) <= ulp, (i, f.__name__, key)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

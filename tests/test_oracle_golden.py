@@ -15,7 +15,7 @@ TOL = 1e-6  # float64 restatement vs float64 reference (goldens stored in float3
 
 BLOCKS = ["block_tiny_s0", "block_tiny_s1", "block_tiny_s3_last", "block_base_s0", "block_base_s1",
           "block_base_s2", "block_base_s3", "block_base_s3_last", "block_large_s1", "block_large_s2",
-          "block_droppath_base_s1"]
+          "block_droppath_base_s1", "block_tiny_s3_last_ye", "block_base_s0_120x160"]
 
 
 def run_block(name, dtype=torch.float64):
@@ -33,10 +33,11 @@ def run_block(name, dtype=torch.float64):
         masks = [torch.tensor(m) for m in ([1.0, 0.0], [0.0, 1.0], [1.0, 1.0], [0.0, 1.0])]
     y, ye = R.block(p, "", x, xe, heads, window, bool(last), drop, masks)
     loss = (y * torch.from_numpy(gen.normal(name + "/gy", y.shape)).to(dtype)).sum()
-    if not last:
+    with_ye = "y_e" in g  # every Block with x_e output, and a drop_depth Block's e_back output (*_ye)
+    if with_ye:
         loss = loss + (ye * torch.from_numpy(gen.normal(name + "/gye", ye.shape)).to(dtype)).sum()
     loss.backward()
-    return g, p, x, xe, y, ye, bool(last)
+    return g, p, x, xe, y, ye, not with_ye
 
 
 @pytest.mark.parametrize("name", BLOCKS)
