@@ -279,11 +279,47 @@ def e2e_forward(model, rgb, dep, bases=None):
     return feats, low, out
 
 
-def golden_e2e(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, backward=True):
+def _e2e_relu_margin(model, B, H, W, seed, bases):
+    """min |input| / max |input| over the ham head's four ReLUs (as _relu_margins) for the inputs drawn
+    with `seed`, in the training-mode forward."""
+    head = model.decode_head
+    seen = {}
+    hooks = [head.squeeze.activate.register_forward_pre_hook(lambda m, a: seen.__setitem__("squeeze", a[0].clone())),
+             head.align.activate.register_forward_pre_hook(lambda m, a: seen.__setitem__("align", a[0].clone())),
+             head.hamburger.ham_in.register_forward_hook(lambda m, a, o: seen.__setitem__("ham_in", o.clone())),
+             head.hamburger.register_forward_pre_hook(lambda m, a: seen.__setitem__("x", a[0].clone())),
+             head.hamburger.ham_out.register_forward_hook(lambda m, a, o: seen.__setitem__("ham_out", o.clone()))]
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=seed)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}  # the running statistics move in train mode
+    with torch.no_grad():
+        e2e_forward(model, t(rgb_np, False), t(dep_np, False), bases)
+    model.load_state_dict(sd)
+    for h in hooks:
+        h.remove()
+    seen["ham"] = seen.pop("x") + seen.pop("ham_out")
+    return min((v.abs().min() / v.abs().max()).item() for v in seen.values())
+
+
+def golden_e2e(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, backward=True, margin=None, tries=200):
+    """End-to-end golden (features, logits, loss, input and parameter gradient fingerprints). With `margin`
+    (ham decoder) the input draw is the first seed from 8964 whose decoder ReLU inputs all stay at least
+    margin x max away from the kink, so an fp32 run cannot flip an activation against fp64 by summation
+    order alone (round 5's e2e_tiny_small had one align-ReLU input at 6e-7 of max: a reduction-geometry
+    change flipped it and moved every gradient behind it by up to 1.2e-2); the seed is meta[4]."""
     t0 = time.time()
     model, cfg = build_segmentor(backbone, decoder, ncls, embed)
     model.train()
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    seed = 8964
+    if margin is not None:
+        bases0 = gen.nmf_bases(B, 512, 64, name=name + "/bases")
+        for seed in range(8964, 8964 + tries):
+            mg = _e2e_relu_margin(model, B, H, W, seed, bases0)
+            if mg > margin:
+                break
+        else:
+            raise RuntimeError(f"no input seed with ReLU margin > {margin}")
+        print(f"  {name}: input seed {seed}, decoder ReLU margin {mg:.2e}")
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=seed)
     rgb, dep = t(rgb_np, backward), t(dep_np, backward)
     lab = torch.from_numpy(gen.labels(B, H, W, ncls))
     bases = gen.nmf_bases(B, 512, 64, name=name + "/bases") if decoder == "ham" else None
@@ -303,7 +339,7 @@ def golden_e2e(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, backw
     save(name, low=low.detach().numpy().astype(np.float32), loss=np.array(loss.item()),
          grgb_fp=gen.fingerprint(rgb.grad.numpy()), gdep_fp=gen.fingerprint(dep.grad.numpy()),
          **{f"feat{i}": f.detach().numpy().astype(np.float32) for i, f in enumerate(feats)},
-         meta=np.array([B, H, W, ncls]), **gfp)
+         meta=np.array([B, H, W, ncls] + ([seed] if margin is not None else [])), **gfp)
     print(f"  {name}: {time.time() - t0:.1f}s")
 
 
@@ -324,7 +360,7 @@ def golden_bf16_env(name, backbone, B, H, W, decoder="ham", ncls=40, embed=512, 
     g = dict(np.load(os.path.join(OUT, name + ".npz")))
     model, cfg = build_segmentor(backbone, decoder, ncls, embed)
     model = model.float().train()
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=int(g["meta"][4]) if g["meta"].size > 4 else 8964)
     rgb = torch.from_numpy(rgb_np).float().requires_grad_()
     dep = torch.from_numpy(dep_np).float().requires_grad_()
     lab = torch.from_numpy(gen.labels(B, H, W, ncls)).long()
@@ -447,7 +483,7 @@ def main():
     if want("mlpdec"):
         golden_mlpdec("mlpdec_small", [32, 64, 128, 256], 2, 16, 20, embed=64)
     if want("e2e_tiny_small"):
-        golden_e2e("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96)
+        golden_e2e("e2e_tiny_small", "DFormer-Tiny", 2, 64, 96, margin=3e-6)
     if want("e2e_base_small"):
         golden_e2e("e2e_base_small", "DFormer-Base", 2, 64, 80)
     if want("e2e_large_mlp"):

@@ -15,6 +15,13 @@ MODELS = {
 RATIOS = [8, 8, 4, 4]
 
 
+def input_seed(g):
+    """The rgb / depth input seed of an end-to-end golden (meta[4] when make_goldens searched for an
+    off-kink draw, else gen.rgb_depth's default)."""
+    m = np.asarray(g["meta"])
+    return int(m[4]) if m.size > 4 else 8964
+
+
 def load(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
 

@@ -9,7 +9,7 @@ import torch
 
 import dformer_ref as R
 import gen
-from goldens import MODELS, RATIOS, check_param_grads, fp_rel_err, load, params, rel_err
+from goldens import MODELS, RATIOS, check_param_grads, fp_rel_err, load, params, rel_err, input_seed
 
 TOL = 1e-6  # float64 restatement vs float64 reference (goldens stored in float32)
 
@@ -114,9 +114,9 @@ E2E = [("e2e_tiny_small", "DFormer-Tiny", "ham", 40), ("e2e_base_small", "DForme
 @pytest.mark.parametrize("name,arch,dec,ncls", E2E)
 def test_e2e_golden(name, arch, dec, ncls):
     g = load(name)
-    B, H, W, _ = [int(v) for v in g["meta"]]
+    B, H, W, _ = [int(v) for v in g["meta"][:4]]
     p = params(R.segmentor_shapes(arch, dec, ncls))
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=input_seed(g))
     rgb = torch.from_numpy(rgb_np).requires_grad_()
     dep = torch.from_numpy(dep_np).requires_grad_()
     lab = torch.from_numpy(gen.labels(B, H, W, ncls))
@@ -146,9 +146,9 @@ def test_e2e_tiny_full_resolution_forward():
     """BASELINE config 1: Tiny forward at 2x3x480x640 (fingerprints)."""
     name = "e2e_tiny_full_fwd"
     g = load(name)
-    B, H, W, ncls = [int(v) for v in g["meta"]]
+    B, H, W, ncls = [int(v) for v in g["meta"][:4]]
     p = params(R.segmentor_shapes("DFormer-Tiny"), requires_grad=False)
-    rgb, dep = (torch.from_numpy(a) for a in gen.rgb_depth(B, H, W))
+    rgb, dep = (torch.from_numpy(a) for a in gen.rgb_depth(B, H, W, seed=input_seed(g)))
     bases = torch.from_numpy(gen.nmf_bases(B, 512, 64, name=name + "/bases"))
     bufs = {k: v.clone() for k, v in p.items() if "running" in k}
     with torch.no_grad():

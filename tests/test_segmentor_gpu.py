@@ -6,7 +6,7 @@ import torch
 
 import dformer_ref as R
 import gen
-from goldens import check_param_grads, fp_rel_err, load, params, rel_err
+from goldens import check_param_grads, fp_rel_err, load, params, rel_err, input_seed
 
 
 class Cfg(dict):
@@ -44,13 +44,13 @@ def test_segmentor_state_dict_matches_reference(name, arch, dec, ncls):
 @pytest.mark.parametrize("name,arch,dec,ncls", E2E)
 def test_segmentor_fp32_vs_reference(name, arch, dec, ncls):
     g = load(name)
-    B, H, W, _ = [int(v) for v in g["meta"]]
+    B, H, W, _ = [int(v) for v in g["meta"][:4]]
     model = build(arch, dec, ncls, "cuda")
     model.train()
     if dec == "ham":
         model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
             gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=input_seed(g))
     rgb = torch.from_numpy(rgb_np).float().cuda().requires_grad_()
     dep = torch.from_numpy(dep_np).float().cuda().requires_grad_()
     lab = torch.from_numpy(gen.labels(B, H, W, ncls)).cuda()
@@ -107,8 +107,8 @@ def test_segmentor_fp32_vs_oracle_full():
 def fp32_audit(name, arch, dec, ncls):
     """{quantity: rel-to-max error} of the fp32 HIP path vs the fp64 oracle on a golden case."""
     g = load(name)
-    B, H, W, _ = [int(v) for v in g["meta"]]
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    B, H, W, _ = [int(v) for v in g["meta"][:4]]
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=input_seed(g))
     lab_np = gen.labels(B, H, W, ncls)
     bases = gen.nmf_bases(B, 512, 64, name=name + "/bases") if dec == "ham" else None
     model = build(arch, dec, ncls, "cuda")
@@ -263,11 +263,11 @@ def test_tiny_full_480x640_fp32_vs_reference():
     four encoder maps, the 1/8 logits and the full-resolution upsampled logits, gate 1e-3."""
     name = "e2e_tiny_full_fwd"
     g = load(name)
-    B, H, W, ncls = [int(v) for v in g["meta"]]
+    B, H, W, ncls = [int(v) for v in g["meta"][:4]]
     model = build("DFormer-Tiny", "ham", ncls, "cuda").train()
     model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
         gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=input_seed(g))
     rgb = torch.from_numpy(rgb_np).float().cuda()
     dep = torch.from_numpy(dep_np).float().cuda()
     with torch.no_grad():
@@ -303,13 +303,13 @@ BF16_GRAD_Q = 1.5   # the distribution over parameters of the gradient-fingerpri
 def test_segmentor_bf16_vs_reference_envelope(name, arch, dec, ncls):
     g = load(name)
     env = load("bf16env_" + name)
-    B, H, W, _ = [int(v) for v in g["meta"]]
+    B, H, W, _ = [int(v) for v in g["meta"][:4]]
     model = build(arch, dec, ncls, "cuda").set_compute_dtype(torch.bfloat16)
     model.train()
     if dec == "ham":
         model.decode_head.hamburger.ham.injected_bases = torch.from_numpy(
             gen.nmf_bases(B, 512, 64, name=name + "/bases")).float()
-    rgb_np, dep_np = gen.rgb_depth(B, H, W)
+    rgb_np, dep_np = gen.rgb_depth(B, H, W, seed=input_seed(g))
     rgb = torch.from_numpy(rgb_np).float().cuda().requires_grad_()
     dep = torch.from_numpy(dep_np).float().cuda().requires_grad_()
     lab = torch.from_numpy(gen.labels(B, H, W, ncls)).cuda()
