@@ -285,6 +285,29 @@ DFM_INLINE uint2 w3_ld(const T* base, long ld, long img, int W, int h, int ww, i
   return *reinterpret_cast<const uint2*>(base + (img + (long)h * W + ww) * ld + c0);
 }
 
+// The streaming forward's input through a raw buffer resource (tensors of < 2 GiB, the host checks): a
+// load's 32-bit byte offset is a running row offset (one add per row) plus a wave-uniform column step (one
+// add per load), instead of a 64-bit multiply per load. Rows / columns outside the tensor (negative offsets
+// wrap past the extent) read as zero through the resource's range check (num_records = the operand's
+// extent; the whole offset is in the VGPR operand, which is what the check covers) and are masked at
+// first use anyway, so no address needs clamping. Isolated (tools/ffn_kernels_bench.py): stage 1 / 2
+// forwards 137.7 -> 120.8, 61.4 -> 53.2, 32.0 -> 30.5 us, stage 0 unchanged; the same change in the fused
+// backward (2 operands) was slower (242.9 -> 248.5 us at stage 0, 39.1 -> 45.9 at stage 2) and is not used:
+// at 2 waves per SIMD that kernel is latency-bound, not bound by its quarter-rate address instructions.
+template <typename T>
+DFM_INLINE __amdgpu_buffer_rsrc_t w3_rsrc(const T* p, long rows, long ld, int C) {
+  const long ext = ((rows - 1) * ld + C) * (long)sizeof(T);  // (unused past 2 GiB: the pointer path runs)
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)min(ext, 0x7fffffffL), 0x00020000);
+}
+DFM_INLINE uint2 w3_bld(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+// the buffer path addresses every operand byte with a 32-bit offset
+template <typename T>
+bool w3_buf_ok(long rows, long ld, int C) {
+  return ((rows - 1) * ld + C) * (long)sizeof(T) < (1L << 31) - (1L << 20);
+}
+
 template <int N>
 DFM_INLINE void w3_keep(uint2* r, unsigned m) {  // zero the vectors whose bit in m is clear
 #pragma unroll
@@ -655,7 +678,7 @@ DFM_INLINE void w3_store(T* p, const float* v) {
   }
 }
 
-template <typename T, bool FLIP>
+template <typename T, bool FLIP, bool BUF>
 __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W, int C, int RC, int nstrips,
                                                              int nchunks, int LPU, int UPW,
                                                              const T* __restrict__ x, long ldx,
@@ -664,6 +687,7 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
                                                              T* __restrict__ y, long ldy, int accumulate,
                                                              T* __restrict__ gout, long ldg) {
   constexpr int CPT = W3Cfg<T>::EPL, CP = CPT / 2, TW = W3_TW, NX = TW + 2;
+  constexpr unsigned ES = sizeof(T);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lg = lane % LPU, usub = lane / LPU;
   const int G = C / CPT, cg = blockIdx.y * LPU + lg;
@@ -679,6 +703,8 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
     bv[e] = bias ? f2v{bias[c0 + 2 * e], bias[c0 + 2 * e + 1]} : f2v{0.f, 0.f};
   }
   const long stride = (long)gridDim.x * 4 * UPW;
+  const __amdgpu_buffer_rsrc_t xr_ = w3_rsrc(x, (long)B * H * W, ldx, C);
+  const unsigned rstep = (unsigned)(W * ldx) * ES, cstep = (unsigned)ldx * ES;  // wave-uniform byte steps
   for (long u = ((long)blockIdx.x * 4 + wave) * UPW + usub; u < units; u += stride) {
     const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
     const long b = u / ((long)nstrips * nchunks);
@@ -687,21 +713,32 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
     unsigned cm = 0;  // in-image columns of the window
 #pragma unroll
     for (int q = 0; q < NX; ++q) cm |= (unsigned)(w0 - 1 + q >= 0 && w0 - 1 + q < W) << q;
+    // BUF: byte offset of (row h0 - 1, column w0 - 1); negative offsets wrap out of range and read zero
+    unsigned xoff = (unsigned)(((img + (long)(h0 - 1) * W + w0 - 1) * ldx + c0) * (long)ES);
     auto load_x = [&](int h, uint2* r) -> unsigned {  // returns the row's keep mask
       const bool hok = h >= 0 && h < H;
-      const int hc = hok ? h : h0;
+      if constexpr (BUF) {
 #pragma unroll
-      for (int q = 0; q < NX; ++q) r[q] = w3_ld<T>(x, ldx, img, W, hc, ((cm >> q) & 1u) ? w0 - 1 + q : w0, c0);
+        for (int q = 0; q < NX; ++q) r[q] = w3_bld(xr_, xoff + q * cstep, 0u);
+        xoff += rstep;
+      } else {
+        const int hc = hok ? h : h0;
+#pragma unroll
+        for (int q = 0; q < NX; ++q) r[q] = w3_ld<T>(x, ldx, img, W, hc, ((cm >> q) & 1u) ? w0 - 1 + q : w0, c0);
+      }
       return hok ? cm : 0u;
     };
     uint2 x0[NX], x1[NX], x2[NX];
     w3_keep<NX>(x0, load_x(h0 - 1, x0));
     w3_keep<NX>(x1, load_x(h0, x1));
     unsigned m2 = load_x(h0 + 1, x2);
-    for (int h = h0; h < h1; ++h) {
+    T* yrow = y + (img + (long)h0 * W + w0) * ldy + c0;
+    T* grow = gout ? gout + (img + (long)h0 * W + w0) * ldg + c0 : nullptr;
+    for (int h = h0; h < h1; ++h, yrow += W * ldy, grow += gout ? W * ldg : 0) {
       w3_keep<NX>(x2, m2);  // the row loaded one iteration ago
       uint2 xn[NX];
-      m2 = load_x(h + 1 < h1 ? h + 2 : H, xn);  // row H (and any row past the chunk) reads as zeros
+      // the next row (its loads in flight during this row's FMAs); past the chunk it is not used
+      m2 = load_x(BUF ? h + 2 : (h + 1 < h1 ? h + 2 : H), xn);
       f2v accp[TW][CP];
 #pragma unroll
       for (int t = 0; t < TW; ++t)
@@ -741,8 +778,7 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
       for (int t = 0; t < TW; ++t) {
         const int ww = w0 + t;
         if (ww >= W) break;
-        const long p = img + (long)h * W + ww;
-        T* yp = y + p * ldy + c0;
+        T* yp = yrow + t * ldy;
         if (accumulate) {
           float o[CPT];
           w3_unpack<T>(*reinterpret_cast<const uint2*>(yp), o);
@@ -759,7 +795,7 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
             dv[e] = fmaf(acc[t][e], pdf, cdf);
           }
           w3_store<T>(yp, (add_identity & 2) ? dv : acc[t]);
-          w3_store<T>(gout + p * ldg + c0, gv);
+          w3_store<T>(grow + t * ldg, gv);
         } else {
           w3_store<T>(yp, acc[t]);
         }
@@ -778,9 +814,10 @@ template <typename T, bool FLIP>
 int f3_launch(int B, int H, int W, int C, const void* x, long ldx, const float* w, const float* bias, int id,
               void* y, long ldy, int acc, void* gout, long ldg, hipStream_t s) {
   const W3Geom g = f3_geom<T>(B, H, W, C);
-  DFM_LAUNCH((dw3_stream_fwd_kernel<T, FLIP>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B,
-                     H, W, C, g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, w, bias, id, (T*)y, ldy,
-                     acc, (T*)gout, ldg);
+  auto kern = w3_buf_ok<T>((long)B * H * W, ldx, C) ? dw3_stream_fwd_kernel<T, FLIP, true>
+                                                    : dw3_stream_fwd_kernel<T, FLIP, false>;
+  DFM_LAUNCH(kern, dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C, g.RC, g.nstrips,
+             g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, w, bias, id, (T*)y, ldy, acc, (T*)gout, ldg);
   DFM_LAUNCH_CHECK();
   return DFM_OK;
 }
