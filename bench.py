@@ -153,6 +153,38 @@ def census(step_fn):
     return table
 
 
+def pmc_traffic(name):
+    """HBM bytes per launch of kernel `name` from the newest PMC record under profiles/ that names it
+    (tools/pmc_dominant.py output: r<round>_pmc_*.json, r02_dominant_pmc.json), with the file it came from."""
+    import glob
+    import re
+    recs = []
+    for path in glob.glob(os.path.join(HERE, "profiles", "r*_*pmc*.json")):
+        m = re.match(r"r(\d+)_", os.path.basename(path))
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if isinstance(rec, dict) and rec.get("kernel") == name and rec.get("traffic_bytes_per_launch"):
+            recs.append((int(m.group(1)) if m else 0, os.path.basename(path), rec["traffic_bytes_per_launch"]))
+    if not recs:
+        return None, None
+    _, src, traffic = max(recs)
+    return traffic, "profiles/" + src
+
+
+# the census kernels the timed region probes: the measured-dominant one and every kernel within
+# PROBE_WITHIN of it (the top two swap between boxes when their census times are that close)
+PROBE_WITHIN = 0.05
+
+
+def probed_kernels(table):
+    order = sorted(table, key=lambda n: -table[n]["measured_ms"])
+    top = table[order[0]]["measured_ms"]
+    return [n for n in order[:3] if table[n]["measured_ms"] >= (1.0 - PROBE_WITHIN) * top]
+
+
 def dominant_roofline(table, name, durations_ms):
     r = table[name]
     n_c = max(r["launches"], 1)
@@ -160,15 +192,7 @@ def dominant_roofline(table, name, durations_ms):
     avg_s = sum(durations_ms) / len(durations_ms) * 1e-3
     peak = MFMA_PEAK_TFS[r["peak"] or "bf16"]
     t_mfma, t_hbm = fl / (peak * 1e12), by / (HBM_PEAK_GBS * 1e9)
-    traffic = None
-    for pmc in (os.path.join(HERE, "profiles", n) for n in ("r05_pmc_dominant.json", "r04_pmc_dominant.json",
-                                                             "r03_pmc_dominant.json", "r02_dominant_pmc.json")):
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                rec = json.load(f)
-            if rec.get("kernel") == name:
-                traffic = rec.get("traffic_bytes_per_launch")
-                break
+    traffic, traffic_src = pmc_traffic(name)
     if t_mfma >= t_hbm:
         ach = fl / avg_s / 1e12
         out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4)}
@@ -179,7 +203,8 @@ def dominant_roofline(table, name, durations_ms):
     # exact per-launch roofline: sum over the census launches of max(F_i/P, B_i/BW) (launches of one kernel
     # have different shapes, some HBM-, some MFMA-bound) over the probe's mean launch time
     out["frac_exact"] = round(r["ideal_ms"] / n_c * 1e-3 / avg_s, 4)
-    out.update(traffic=traffic, kernel=name, launches=len(durations_ms), avg_us=round(avg_s * 1e6, 2),
+    out.update(traffic=traffic, traffic_source=traffic_src, kernel=name, launches=len(durations_ms),
+               avg_us=round(avg_s * 1e6, 2),
                bytes_per_launch=round(by), flops_per_launch=round(fl),
                census_share=round(r["measured_ms"] / max(sum(t["measured_ms"] for t in table.values()), 1e-9), 4))
     return out
@@ -275,10 +300,11 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    table, dom = None, None
+    table, dom, probes = None, None, []
     if not args.no_census:
         table = census(step)
-        dom = max(table, key=lambda n: table[n]["measured_ms"])
+        probes = probed_kernels(table)
+        dom = probes[0]
     # HIP-graph mode: the whole step is captured once and replayed, so ~1.6k kernel launches cost one
     # graph launch. Default at world 1 (DFM_GRAPH=0 disables). At world > 1 the step runs EAGERLY unless
     # DFM_GRAPH=1: a captured multi-rank RCCL step has never run on N > 1 hardware (only the one-rank
@@ -294,7 +320,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     if dom is not None and not use_graph:
-        K.trace(2, dom)
+        K.trace(2, probes)
     s = torch.cuda.current_stream()
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
@@ -314,11 +340,14 @@ def main():
             # launches inside a replayed graph cannot be bracketed from the host: the dominant
             # kernel is timed by the same per-launch HIP events over a window of eager steps run
             # right after the timed region (same kernels, same stream, same shapes)
-            K.trace(2, dom)
+            K.trace(2, probes)
             for _ in range(3):
                 step.eager()
             torch.cuda.synchronize()
-        dom_ms = [ms for _, ms in K.trace_read()]
+        probe_ms = {}
+        for nm, ms in K.trace_read():
+            probe_ms.setdefault(nm, []).append(ms)
+        dom_ms = probe_ms.get(dom)
         K.trace(0)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
@@ -343,6 +372,8 @@ def main():
     if rank == 0:
         if table is not None and dom_ms:
             roof = dominant_roofline(table, dom, dom_ms)
+            # the other census kernels within PROBE_WITHIN of the dominant one, with the same fields
+            roof["close"] = [dominant_roofline(table, n, probe_ms[n]) for n in probes[1:] if probe_ms.get(n)]
             ideal = sum(r["ideal_ms"] for r in table.values())
             traced = sum(r["measured_ms"] for r in table.values())
             survey_ms = None

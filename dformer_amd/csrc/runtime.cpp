@@ -58,7 +58,7 @@ std::vector<const void*> g_launched;          // DFM_TRACE_RECORD: kernels since
 std::vector<Timed> g_timed;                   // DFM_TRACE_TIME: event pairs awaiting read
 std::vector<hipEvent_t> g_pool;               // recycled events
 std::unordered_map<const void*, std::string> g_names;
-std::string g_probe;                          // demangled name to time ("" = every kernel)
+std::vector<std::string> g_probe;             // demangled names to time (empty = every kernel)
 hipEvent_t g_open = nullptr;                  // start event of the launch in flight
 
 const std::string& name_of(const void* f) {
@@ -86,7 +86,13 @@ hipEvent_t take_event() {
   return e;
 }
 
-bool timed(const void* f) { return g_probe.empty() || name_of(f) == g_probe; }
+bool timed(const void* f) {
+  if (g_probe.empty()) return true;
+  const std::string& n = name_of(f);
+  for (const std::string& p : g_probe)
+    if (n == p) return true;
+  return false;
+}
 }  // namespace
 
 void dfm_trace_pre(const void* func, hipStream_t s) {
@@ -110,7 +116,13 @@ void dfm_trace_post(const void* func, hipStream_t s) {
 
 extern "C" int dfm_trace_set(int flags, const char* probe_name) {
   std::lock_guard<std::mutex> lk(g_mu);
-  g_probe = probe_name ? probe_name : "";
+  g_probe.clear();  // one name, or several separated by '\n'
+  for (const char* c = probe_name ? probe_name : ""; *c;) {
+    const char* e = strchr(c, '\n');
+    const size_t len = e ? (size_t)(e - c) : strlen(c);
+    if (len) g_probe.emplace_back(c, len);
+    c += len + (e ? 1 : 0);
+  }
   g_launched.clear();
   dfm_trace_flags = flags;
   return DFM_OK;

@@ -29,7 +29,10 @@ _FUNCS = (ctypes.c_void_p * 64)()
 
 def trace(flags, probe=None):
     """Launch tracer of the library: flags 0 off, 1 record launched kernels, 2 time (HIP events) the
-    kernel named `probe` (demangled, as rocprofv3 prints it; None = every kernel), 3 both."""
+    kernel(s) named `probe` (demangled, as rocprofv3 prints it; a name or a list of names; None = every
+    kernel), 3 both."""
+    if isinstance(probe, (list, tuple)):
+        probe = "\n".join(probe)
     check(lib.dfm_trace_set(flags, probe.encode() if probe else None), "dfm_trace_set")
 
 

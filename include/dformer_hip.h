@@ -50,7 +50,8 @@ const char* dfm_build_tag(void);
 /* ---------------------------------------------------------------- launch tracer (measurement)
  * Off by default (one branch per launch). DFM_TRACE_RECORD: every kernel the library enqueues is
  * recorded (dfm_trace_take returns and clears them: the kernels one entry point launched);
- * DFM_TRACE_TIME: launches of the kernel whose demangled name is `probe_name` (NULL or "" = every
+ * DFM_TRACE_TIME: launches of the kernel(s) whose demangled name is `probe_name` (several names separated
+ * by '\n'; NULL or "" = every
  * kernel) are bracketed by HIP events on their own stream; dfm_trace_read synchronises on the last
  * event and returns per-launch milliseconds. dfm_kernel_name: the demangled name rocprofv3 prints.
  * Used by bench.py (per-kernel FLOP/byte accounting and the dominant kernel's live roofline). */
