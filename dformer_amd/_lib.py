@@ -31,7 +31,8 @@ class GemmDesc(ctypes.Structure):
                 ("mul", P), ("ldmul", c_long), ("res", P), ("ldres", c_long),
                 ("colscale", P), ("rowscale", P), ("rows_per_scale", c_long), ("split_k", c_int),
                 ("act_col0", c_int), ("colsum", P), ("colsum_accumulate", c_int), ("mul_gelu_grad", c_int),
-                ("workspace_bytes", ctypes.c_long)]
+                ("workspace_bytes", ctypes.c_long),
+                ("mul2", P), ("ldmul2", c_long), ("out2", P), ("ldout2", c_long)]
 
 
 class PartialSum(ctypes.Structure):

@@ -635,19 +635,25 @@ DFM_INLINE void attn_block(int heads, int groups, int& bh, int& cg) {
 }
 
 // Forward: S^T = K Q^T (keys as rows), online softmax per query, O^T += V^T P^T.
-// Partials per wave (chunk): unnormalised O [49][DH], running max m and sum l (scaled units).
+// Each wave walks one chunk of keys; the block's 4 wave states (unnormalised O [49][DH], running max m
+// and sum l, scaled units) are merged through LDS and wave 0 writes ONE partial per block (chunk group
+// cg), so the combine kernel reads groups = nchunk / 4 partials (round 5 wrote one per wave: 7.65 MB of
+// fp32 partials per launch against ~0.2 MB of output, 1.66x the kernel's algorithmic bytes). Isolated,
+// forward + combine (tools/attn_kernels_bench.py): 25.5 -> 18.2 us (stage 1), 18.1 -> 13.1 (2), 11.8 ->
+// 10.6 (3); the step is within noise (479.7 / 479.5 vs 479.5 / 479.1 images/s).
 template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw, int groups) {
   constexpr int KD = (DH + 31) / 32, ND = DH / 16, LDV = DH + 8;
   __shared__ __attribute__((aligned(16))) bf16_t sV[4][32 * LDV];
+  __shared__ float4 mO[3][4][ND][64];  // waves 1..3: O in the C-fragment layout, lane-contiguous
+  __shared__ float mML[3][4][2][16];   // waves 1..3: m, l per (row tile, row)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
   int bh, cg;
   attn_block(a.heads, groups, bh, cg);
-  const int chunk = cg * 4 + w;
-  if (chunk >= a.nchunk) return;
+  const int chunk = cg * 4 + w;  // a wave past the last chunk contributes an empty state (m = -inf, l = 0)
   const int h = bh % a.heads, b = bh / a.heads;
-  const int n0 = chunk * kpw, n1 = min(a.N, n0 + kpw);
+  const int n0 = min(a.N, chunk * kpw), n1 = chunk < a.nchunk ? min(a.N, n0 + kpw) : n0;
   const bf16_t* Q = (const bf16_t*)a.q + (long)b * NQ * a.ldq + h * DH;
   const bf16_t* K = (const bf16_t*)a.k + (long)b * a.N * a.ldkv + h * DH;
   const bf16_t* V = (const bf16_t*)a.v + (long)b * a.N * a.ldkv + h * DH;
@@ -757,20 +763,58 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma_kernel(AttnArgs a, int kpw,
     }
     lds_wave_sync();  // the next block's V stage overwrites sv
   }
-  float* pm = a.ws + (long)a.B * a.heads * a.nchunk * NQ * DH;
-  float* pl = pm + (long)a.B * a.heads * a.nchunk * NQ;
-  const long base = ((long)bh * a.nchunk + chunk) * NQ;
+  if (w > 0) {  // waves 1..3 hand their state to wave 0
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+        mO[w - 1][nt][dt][lane] = make_float4(o[dt][nt][0], o[dt][nt][1], o[dt][nt][2], o[dt][nt][3]);
+      if (g == 0) {
+        mML[w - 1][nt][0][j] = mrun[nt];
+        mML[w - 1][nt][1][j] = lrun[nt];
+      }
+    }
+  }
+  __syncthreads();
+  if (w > 0) return;
+  // the block's partial = the log-sum-exp merge of its waves' states (wave 0 always holds a chunk)
+  const int groups_total = (a.nchunk + 3) / 4;
+  float* pm = a.ws + (long)a.B * a.heads * groups_total * NQ * DH;
+  float* pl = pm + (long)a.B * a.heads * groups_total * NQ;
+  const long base = ((long)bh * groups_total + cg) * NQ;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
     const int q = 16 * nt + j;
+    float mw[3], M = mrun[nt];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      mw[u] = mML[u][nt][0][j];
+      M = fmaxf(M, mw[u]);
+    }
+    const float s0 = __expf(mrun[nt] - M);
+    float L = lrun[nt] * s0, su[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      su[u] = __expf(mw[u] - M);  // an empty state (m = -inf) scales to 0
+      L += mML[u][nt][1][j] * su[u];
+    }
     if (q >= NQ) continue;
 #pragma unroll
-    for (int dt = 0; dt < ND; ++dt)
-      *reinterpret_cast<float4*>(a.ws + (base + q) * DH + 16 * dt + 4 * g) =
-          make_float4(o[dt][nt][0], o[dt][nt][1], o[dt][nt][2], o[dt][nt][3]);
+    for (int dt = 0; dt < ND; ++dt) {
+      float4 v = make_float4(o[dt][nt][0] * s0, o[dt][nt][1] * s0, o[dt][nt][2] * s0, o[dt][nt][3] * s0);
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const float4 ou = mO[u][nt][dt][lane];
+        v.x += ou.x * su[u];
+        v.y += ou.y * su[u];
+        v.z += ou.z * su[u];
+        v.w += ou.w * su[u];
+      }
+      *reinterpret_cast<float4*>(a.ws + (base + q) * DH + 16 * dt + 4 * g) = v;
+    }
     if (g == 0) {
-      pm[base + q] = mrun[nt];
-      pl[base + q] = lrun[nt];
+      pm[base + q] = M;
+      pl[base + q] = L;
     }
   }
 }
@@ -1250,6 +1294,7 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
     a.dh = dp; a.q = pq; a.ldq = ldp; a.k = pk; a.v = pv; a.ldkv = ldp; a.o = po; a.ldo = ldp;
     a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
     attn_mfma(dtype, a, false, s);
+    a.nchunk = (a.nchunk + 3) / 4;  // one merged partial per block (chunk group)
     attn_combine16(dtype, a, s);
     head_repack((long)B * NQ, heads, dp, ldp, dh, ldo, po, o, s);
     DFM_LAUNCH_CHECK();
@@ -1262,6 +1307,7 @@ extern "C" int dfm_pooled_attn_fwd(int dtype, int B, int heads, int N, int dh, c
       a.nchunk = (N + attn_kpw(N) - 1) / attn_kpw(N);
       attn_mfma(dtype, a, false, s);
       DFM_LAUNCH_CHECK();
+      a.nchunk = (a.nchunk + 3) / 4;  // one merged partial per block (chunk group)
       attn_combine16(dtype, a, s);
       DFM_LAUNCH_CHECK();
       return DFM_OK;

@@ -155,6 +155,19 @@ void dgrad(Run& r, V dy, long M, long N, const void* w, long K, V dx, bool accum
   gemm(r, d, dy.p, w, dx.p);
 }
 
+// dx[M][Kc] = (dy[M][N] W[N][k0 : k0 + Kc]) (* mul), dx2 = (dy W[N][k0 : k0 + Kc]) * mul2 (second epilogue
+// output, when dx2 is given): column block k0 of an input gradient, W rows ldw elements apart
+void dgrad_cols(Run& r, V dy, long M, long N, const void* w, long ldw, long k0, long Kc, V dx, V mul = V(),
+                V mul2 = V(), V dx2 = V()) {
+  DfmGemmDesc d = gdesc();
+  d.M = (int)M, d.N = (int)Kc, d.K = (int)N;
+  d.a_kcontig = 1, d.b_kcontig = 0;
+  d.lda = dy.ld, d.ldb = ldw, d.ldc = dx.ld;
+  d.mul = mul.p, d.ldmul = mul.ld;
+  d.mul2 = mul2.p, d.ldmul2 = mul2.ld, d.out2 = dx2.p, d.ldout2 = dx2.ld;
+  gemm(r, d, dy.p, w ? static_cast<const char*>(w) + k0 * r.es : nullptr, dx.p);
+}
+
 // dW[N][K] = dy[M][N]^T x[M][K] (float32), db[N] = sum_M dy
 void wgrad(Run& r, V dy, long M, long N, V x, long K, float* dw, float* db) {
   DfmGemmDesc d = gdesc();
@@ -461,30 +474,42 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
   }  // with drop_depth the x_e output is e_back's output (no identity path): dye joins dxe' below
   // proj / proj_e: one weight-gradient GEMM each, one input-gradient GEMM over [dp1 | dp1e] when the
   // two weights are stacked in memory
-  V df = r.temp(P, fw);
   V dpc = r.temp(P, C + Ch);
   residual_bwd(r, P, C, dx1, s.p1, F(p, DFM_BP_LS1), io.rs[0], rps, dpc, gr[DFM_BP_LS1]);
   wgrad(r, dpc, P, C, s.f, fw, gr[DFM_BP_PROJ_W], gr[DFM_BP_PROJ_B]);
-  if (m.drop_depth) {
-    dgrad(r, dpc, P, C, p[DFM_BP_PROJ_W], fw, df);
-  } else {
+  // the projections' input gradient df = dpc [Wp; Wpe] (one GEMM when the two weights are stacked in
+  // memory, or Wp alone with drop_depth) by its column blocks f = cat(q * a, attn, cx * xe'), the two
+  // products' backward in the epilogues (second output): dq = df_q a, da = df_q q; dcx = df_e xe',
+  // dxe' = df_e cx; df is only materialised for the attention block (or, with separate weights, whole)
+  const bool stacked = m.drop_depth || adjacent(p[DFM_BP_PROJ_W], (size_t)C * fw * es, p[DFM_BP_PROJE_W]);
+  const long Kp = m.drop_depth ? C : C + Ch;
+  if (!m.drop_depth) {
     residual_bwd(r, P, Ch, dxe1, s.p1e, F(p, DFM_BP_LS1E), io.rs[2], rps, dpc.col(C), gr[DFM_BP_LS1E]);
     wgrad(r, dpc.col(C), P, Ch, s.f, fw, gr[DFM_BP_PROJE_W], gr[DFM_BP_PROJE_B]);
-    if (adjacent(p[DFM_BP_PROJ_W], (size_t)C * fw * es, p[DFM_BP_PROJE_W])) {
-      dgrad(r, dpc, P, C + Ch, p[DFM_BP_PROJ_W], fw, df);
-    } else {
-      dgrad(r, dpc, P, C, p[DFM_BP_PROJ_W], fw, df);
-      dgrad(r, dpc.col(C), P, Ch, p[DFM_BP_PROJE_W], fw, df, true);
-    }
   }
   V q = s.qcl, cx = s.qcl.col(C), g = s.qcl.col(C + Ch);
   V dqcl = r.temp(P, 2 * C + Ch);
   V dq = dqcl, dcx = dqcl.col(C), dl = dqcl.col(C + Ch);
+  V da = r.temp(P, C), dxep = r.temp(P, Ch);
+  V dfa;  // df's attention block (window only)
+  if (stacked) {
+    if (m.window) dfa = r.temp(P, Ch);
+    Group grp(r);
+    dgrad_cols(r, dpc, P, Kp, p[DFM_BP_PROJ_W], fw, 0, C, dq, s.a, q, da);
+    dgrad_cols(r, dpc, P, Kp, p[DFM_BP_PROJ_W], fw, fw - Ch, Ch, dcx, s.xep, cx, dxep);
+    if (m.window) dgrad_cols(r, dpc, P, Kp, p[DFM_BP_PROJ_W], fw, C, Ch, dfa);
+  } else {
+    V df = r.temp(P, fw);
+    dgrad(r, dpc, P, C, p[DFM_BP_PROJ_W], fw, df);
+    dgrad(r, dpc.col(C), P, Ch, p[DFM_BP_PROJE_W], fw, df, true);
+    if (r.live())
+      r.ok(dfm_dual_mul(r.dt, P, C, df.p, df.ld, s.a.p, s.a.ld, q.p, q.ld, dq.p, dq.ld, da.p, da.ld, r.s));
+    if (r.live())
+      r.ok(dfm_dual_mul(r.dt, P, Ch, df.col(fw - Ch).p, df.ld, s.xep.p, s.xep.ld, cx.p, cx.ld, dcx.p, dcx.ld, dxep.p,
+                        dxep.ld, r.s));
+    dfa = df.col(C);
+  }
   // depth branch: cx * e_back(DW7(e_fore(LN_e xe)))
-  V dxep = r.temp(P, Ch);
-  if (r.live())
-    r.ok(dfm_dual_mul(r.dt, P, Ch, df.col(fw - Ch).p, df.ld, s.xep.p, s.xep.ld, cx.p, cx.ld, dcx.p, dcx.ld, dxep.p,
-                      dxep.ld, r.s));
   if (m.drop_depth && dye.p && r.live())
     r.ok(dfm_scale_mul(r.dt, P, Ch, dye.p, dye.ld, nullptr, 0, nullptr, nullptr, 1, 1.f, dxep.p, dxep.ld, 1, r.s));
   wgrad(r, dxep, P, Ch, s.e2, Ch, gr[DFM_BP_EBACK_W], gr[DFM_BP_EBACK_B]);
@@ -509,7 +534,7 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
     const long B49 = (long)B * 49;
     V dout_o = r.temp(B49, Ch);
     if (r.live())
-      r.ok(dfm_bilinear_bwd(r.dt, B, 7, 7, m.sh.H, m.sh.W, Ch, df.col(C).p, df.ld, dout_o.p, dout_o.ld, 0, r.s));
+      r.ok(dfm_bilinear_bwd(r.dt, B, 7, 7, m.sh.H, m.sh.W, Ch, dfa.p, dfa.ld, dout_o.p, dout_o.ld, 0, r.s));
     V dm = r.temp(B49, Ch);
     dkv = r.temp(P, C);
     void* ws = r.scr(dfm_pooled_attn_workspace(B, m.heads, (int)(P / B), m.dhd));
@@ -524,10 +549,7 @@ void block_bwd(Run& r, const Dims& m, const BlockIO& io, V dy, V dye, V dx, V dx
       r.ok(dfm_adaptive_pool7_bwd(r.dt, B, m.sh.H, m.sh.W, C, dpooled.p, dpooled.ld, dxn.p, dxn.ld, 0, r.s));
     wgrad(r, dkv, P, C, g, C, gr[DFM_BP_KV_W], gr[DFM_BP_KV_B]);
   }
-  // q * a(DW7(l))
-  V da = r.temp(P, C);
-  if (r.live())
-    r.ok(dfm_dual_mul(r.dt, P, C, df.p, df.ld, s.a.p, s.a.ld, q.p, q.ld, dq.p, dq.ld, da.p, da.ld, r.s));
+  // q * a(DW7(l)) (dq, da from the projection's input-gradient epilogue)
   wgrad(r, da, P, C, s.apre, C, gr[DFM_BP_A_W], gr[DFM_BP_A_B]);
   V dapre = r.temp(P, C);
   {

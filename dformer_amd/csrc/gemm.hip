@@ -41,6 +41,11 @@ static int validate_desc(const DfmGemmDesc* d, const char* who, int q) {
                 q);
   DFM_CHECK_ARG(d->colsum == nullptr || d->batch <= 1, "%s: colsum needs batch 1 (problem %d)", who, q);
   DFM_CHECK_ARG(d->workspace_bytes >= 0, "%s: negative workspace size (problem %d)", who, q);
+  DFM_CHECK_ARG(!d->out2 == !d->mul2, "%s: out2 and mul2 go together (problem %d)", who, q);
+  DFM_CHECK_ARG(d->out2 == nullptr || (d->ldout2 >= d->N && d->ldmul2 >= d->N && d->batch <= 1 && !d->res &&
+                                       !d->c_f32 && !d->colsum),
+                "%s: out2 needs ldout2 / ldmul2 >= N, batch 1, no res / colsum, output in the operand dtype (problem %d)",
+                who, q);
   return DFM_OK;
 }
 

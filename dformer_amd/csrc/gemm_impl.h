@@ -52,6 +52,10 @@ struct GemmArgs {
   int tiles_m;     // output row tiles (glds kernel)
   int n_fast;      // glds kernel: consecutive (XCD-local) blocks walk column tiles of one row tile
   int xcd_map;     // gemm_kernel: XCD-aware block renumbering (always on)
+  const void* mul2;  // optional second output C2[m, n] = (value before mul / res) * mul2[m, n]
+  long ldmul2;
+  void* C2;
+  long ldc2;
 };
 
 
@@ -286,6 +290,7 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
       else if (a.act == 2) v = fmaxf(v, 0.0f);
     }
   }
+  if (a.C2) stf((TO*)a.C2 + (long)m * a.ldc2 + n, v * ldf((const TO*)a.mul2 + (long)m * a.ldmul2 + n));
   if (a.mul) {
     const float mv = ldf((const TO*)a.mul + (long)m * a.ldmul + n);
     v *= a.mul_gelu_grad ? gelu_grad_f(mv) : mv;
@@ -303,13 +308,14 @@ DFM_INLINE void epilogue_store(const GemmArgs& a, int b, int m, int n, float v) 
 // all of its vectors are in flight together.
 template <typename TO>
 struct EpiIn {
-  Raw8<TO> mul, res, c;
+  Raw8<TO> mul, res, c, mul2;
 };
 
 template <typename TO>
 DFM_INLINE void epi_load(const GemmArgs& a, int b, int m, int n, EpiIn<TO>& in) {
   if (a.beta != 0.0f && !a.c_f32) in.c = ldraw8<TO>((const TO*)a.C + b * a.sc + (long)m * a.ldc + n);
   if (a.mul) in.mul = ldraw8<TO>((const TO*)a.mul + (long)m * a.ldmul + n);
+  if (a.C2) in.mul2 = ldraw8<TO>((const TO*)a.mul2 + (long)m * a.ldmul2 + n);
   if (a.res) in.res = ldraw8<TO>((const TO*)a.res + (long)m * a.ldres + n);
 }
 
@@ -346,6 +352,13 @@ DFM_INLINE void epilogue8(const GemmArgs& a, int b, int m, int n, float* v, cons
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.0f);
     }
+  }
+  if (a.C2) {  // second output: the value before the multiplier times mul2
+    float t2[8];
+    unpack8(in.mul2, t2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t2[e] *= v[e];
+    st8<TO>((TO*)a.C2 + (long)m * a.ldc2 + n, t2);
   }
   if (a.mul) {
     unpack8(in.mul, t);
@@ -1140,6 +1153,7 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
   a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
+  a.mul2 = d->mul2; a.ldmul2 = d->ldmul2; a.C2 = d->out2; a.ldc2 = d->ldout2;
   a.xcd_map = 1;
   int BM, BN;
   pick_tile(d, BM, BN);
@@ -1153,7 +1167,8 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0) &&
           ext_b < 2147483647.0;
   a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
-             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
+             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0) &&
+             al16<T>(d->mul2, d->ldmul2) && al16<T>(d->out2, d->ldout2);
   const bool ak = d->a_kcontig, bk = d->b_kcontig;
   const bool small_k = sizeof(T) == 2 ? d->K <= 128 : d->K <= 64;
   // (a persistent M-streaming kernel for large M x short K, column tiles <= 64, was measured slower
@@ -1161,7 +1176,9 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // finishes late when the concurrent ConvFFN stream holds CUs)
   // bf16 k-contiguous A on the LDS-DMA ring: split-K off (one unsplit 64x64 ring block per tile beats
   // the split + reduction at 4,800 rows x K >= 1024: 16.8 vs 34.8 us, profiles/r04_glds_variants.txt)
-  bool glds_ok = sizeof(T) == 2 && ak && a.ala && a.alb;
+  // (the ring kernel writes the virtual ones column of a bias-gradient colsum for a row-contiguous B
+  // only; a k-contiguous B with colsum takes the register-staged kernel)
+  bool glds_ok = sizeof(T) == 2 && ak && a.ala && a.alb && !(d->colsum && bk);
   if (glds_ok && d->split_k < 1) a.splits = 1;
   glds_ok = glds_ok && (d->K + a.splits - 1) / a.splits >= 2 * GBK;  // >= 2 whole k-slices per split
   // tall short-K GEMMs with more than one 128-column slice (gemm_wide.h): measured per shape on the
@@ -1253,6 +1270,7 @@ void fill_args(GemmArgs& a, const DfmGemmDesc* d, const void* A, const void* B, 
   a.colscale = d->colscale; a.rowscale = d->rowscale; a.act_col0 = d->act_col0;
   a.rps = d->rows_per_scale > 0 ? d->rows_per_scale : 1;
   a.colsum = d->colsum; a.colsum_acc = d->colsum_accumulate;
+  a.mul2 = d->mul2; a.ldmul2 = d->ldmul2; a.C2 = d->out2; a.ldc2 = d->ldout2;
   a.splits = splits;
   const double ext_a = ((double)(d->a_kcontig ? d->M : d->K) * d->lda) * sizeof(T);
   const double ext_b = ((double)(d->b_kcontig ? d->N : d->K) * d->ldb) * sizeof(T);
@@ -1261,7 +1279,8 @@ void fill_args(GemmArgs& a, const DfmGemmDesc* d, const void* A, const void* B, 
   a.alb = (d->ldb % VEC == 0) && ((uintptr_t)B % 16 == 0) && (a.batch == 1 || d->stride_b % VEC == 0) &&
           ext_b < 2147483647.0;
   a.vec_ok = al16<T>(C, d->ldc) && (a.batch == 1 || d->stride_c % 8 == 0) && al16<T>(d->preact, d->ldpre) &&
-             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0);
+             al16<T>(d->mul, d->ldmul) && al16<T>(d->res, d->ldres) && (d->act_col0 % 8 == 0) &&
+             al16<T>(d->mul2, d->ldmul2) && al16<T>(d->out2, d->ldout2);
 }
 
 template <typename T, bool AK, bool BKC>

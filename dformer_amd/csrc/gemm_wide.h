@@ -215,7 +215,8 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs a, const T* 
 template <typename T>
 bool wide_eligible(const GemmArgs& a, const DfmGemmDesc* d) {
   if (sizeof(T) != 2) return false;
-  if (!d->a_kcontig || a.splits != 1 || a.batch != 1 || d->colsum || d->c_f32 || !a.ala || !a.alb || !a.vec_ok)
+  if (!d->a_kcontig || a.splits != 1 || a.batch != 1 || d->colsum || d->c_f32 || d->out2 || !a.ala || !a.alb ||
+      !a.vec_ok)
     return false;
   if (d->K % 32 != 0 || d->K > 128 || d->K < 32 || d->N % 8 != 0 || d->M < 65536 || d->N < 144) return false;
   const int tiles = (d->mul != nullptr) + (d->res != nullptr) + (d->beta != 0.0f);

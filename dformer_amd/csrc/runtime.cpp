@@ -25,7 +25,7 @@ void dfm_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* dfm_last_error(void) { return g_err; }
-extern "C" int dfm_abi_version(void) { return 12; }  // 12: dfm_build_tag; 11: dfm_block_fwd / _bwd; 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
+extern "C" int dfm_abi_version(void) { return 13; }  // 13: DfmGemmDesc.mul2 / out2; 12: dfm_build_tag; 11: dfm_block_fwd / _bwd; 10: dfm_convffn_fwd / _bwd; 9: dfm_nmf_fwd; 8: deferred reduction second stages; 7: DfmGemmDesc.workspace_bytes; 6: dfm_gemm_group
 #ifndef DFM_BUILD_TAG
 #define DFM_BUILD_TAG "default"
 #endif

@@ -401,7 +401,7 @@ class AttentionFn(torch.autograd.Function):
         if drop_depth:
             dp1, grads["ls1"] = K.residual_bwd(dx1, p1, ls1, rowscale, rps)
             grads["wp"], grads["bp"] = K.linear_wgrad(dp1, f, out=gslot2(wp), bias_grad=True, bias_out=gslot(bp))
-            df = K.linear_dgrad(dp1, wcast(dt, wp))
+            dpc, Wc = dp1, wcast(dt, wp)
             dxe_res = None  # x_e's output is xe' (no identity path), its gradient joins dxe' below
         else:
             dxe1 = dxe1.contiguous()
@@ -412,17 +412,27 @@ class AttentionFn(torch.autograd.Function):
             dWc, dbc = K.linear_wgrad(dpc, f, out=ow, bias_grad=True, bias_out=ob)
             grads["wp"], grads["wpe"] = dWc[:C], dWc[C:]
             grads["bp"], grads["bpe"] = dbc[:C], dbc[C:]
-            df = K.linear_dgrad(dpc, wcast(dt, wp, wpe))
+            Wc = wcast(dt, wp, wpe)
             dxe_res = dxe1
         q, cx, g = qcl[:, :C], qcl[:, C:C + Ch], qcl[:, C + Ch:]
         dqcl = torch.empty(P, 2 * C + Ch, device=dev, dtype=dt)
         dq, dcx, dl = dqcl[:, :C], dqcl[:, C:C + Ch], dqcl[:, C + Ch:]
+        # df = dpc [Wp; Wpe] by its column blocks f = cat(q*a, attn, cx*xe') in one grouped launch; the two
+        # products' backward rides in the epilogues (second output): dq = df_q * a, da = df_q * q;
+        # dcx = df_e * xe', dxe' = df_e * cx -- df itself is only materialised for the attention block
+        da = torch.empty(P, C, device=dev, dtype=dt)
+        dxep = torch.empty(P, Ch, device=dev, dtype=dt)
+        dfa = torch.empty(P, Ch, device=dev, dtype=dt) if window else None
+        calls = [lambda c: K.linear_dgrad(dpc, Wc[:, :C], out=dq, mul=a, mul2=q, out2=da, collect=c),
+                 lambda c: K.linear_dgrad(dpc, Wc[:, fw - Ch:], out=dcx, mul=xep, mul2=cx, out2=dxep, collect=c)]
+        if window:
+            calls.append(lambda c: K.linear_dgrad(dpc, Wc[:, C:C + Ch], out=dfa, collect=c))
+        # (measured on the step against df + two dual_mul passes: 478.3 / 480.8 vs 475.0 / 476.7 images/s)
+        K.gemm_many(calls)
         side = _attn_bwd_side(dev) if x.is_cuda else None
         main = torch.cuda.current_stream(dev) if side is not None else None
 
         def depth_branch():  # cxe = cx * xe',  xe' = e_back(DW7(e_fore(LN_e xe)))
-            dcxe = df[:, fw - Ch:]
-            _, dxep = K.dual_mul(dcxe, xep, cx, out1=dcx)
             if drop_depth and dxe1 is not None:  # the Block's x_e output is xe' itself
                 K.scale_mul(dxe1.contiguous(), out=dxep, accumulate=True)
             ow, ob = gslot2(web), gslot(beb)
@@ -439,7 +449,7 @@ class AttentionFn(torch.autograd.Function):
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 dxen, side_tmp = depth_branch()
-            for t in (df, xep, cx, e2, e1, xen, dqcl) + ((dxe1,) if drop_depth and dxe1 is not None else ()):
+            for t in (dxep, e2, e1, xen) + ((dxe1,) if drop_depth and dxe1 is not None else ()):
                 t.record_stream(side)
         else:
             dxen, _ = depth_branch()
@@ -450,7 +460,7 @@ class AttentionFn(torch.autograd.Function):
         def pooled_branch():  # softmax(q_pool k^T) v over the pooled queries, DFormer.py:119-131
             kv, pooled, m, o, lse = saved_attn
             dh = C // heads // 2
-            do = K.bilinear_bwd(df[:, C:C + Ch], (7, 7), (H, W), B)
+            do = K.bilinear_bwd(dfa, (7, 7), (H, W), B)
             dm = torch.empty_like(m)
             dkv = torch.empty(P, C, device=dev, dtype=dt)
             K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
@@ -466,9 +476,7 @@ class AttentionFn(torch.autograd.Function):
         if window:
             dxn, dpooled, dkv = pooled_branch()
             dpooled_e = dpooled[:, C:]
-        # q * a
-        dqa = df[:, :C]
-        _, da = K.dual_mul(dqa, a, q, out1=dq)
+        # q * a (dq, da came out of the projection's input-gradient epilogue)
         ow, ob = gslot2(wa), gslot(ba)
         grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=ow, bias_grad=True, bias_out=ob)
         dapre = torch.empty(P, C, device=dev, dtype=dt)

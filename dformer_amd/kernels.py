@@ -182,7 +182,7 @@ def flush_wgrad(pending):
 def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, stride_a=0, stride_b=0,
          stride_c=0, alpha=1.0, beta=0.0, bias=None, act=0, preact=None, ldpre=0, mul=None, ldmul=0, res=None,
          ldres=0, colscale=None, rowscale=None, rows_per_scale=1, split_k=0, act_col0=0, colsum=None,
-         colsum_accumulate=False, mul_gelu_grad=False, defer=False, collect=None):
+         colsum_accumulate=False, mul_gelu_grad=False, mul2=None, out2=None, defer=False, collect=None):
     """One dfm_gemm launch. defer=True (weight gradients) inside `with wgrad_group():` queues it for
     the block's grouped launch instead; `collect` (a list, from gemm_many) receives it unlaunched."""
     dt = dtype_code(a)
@@ -193,14 +193,15 @@ def gemm(a, b, *, M, N, K, a_kcontig, b_kcontig, lda, ldb, out, ldc, batch=1, st
     d = _lib.GemmDesc(M, N, K, batch, int(a_kcontig), int(b_kcontig), lda, ldb, ldc, stride_a, stride_b, stride_c,
                       alpha, beta, c_f32, ptr(bias), act, ptr(preact), ldpre, ptr(mul), ldmul, ptr(res), ldres,
                       ptr(colscale), ptr(rowscale), rows_per_scale, split_k, act_col0, ptr(colsum),
-                      int(colsum_accumulate), int(mul_gelu_grad))
+                      int(colsum_accumulate), int(mul_gelu_grad), 0, ptr(mul2), ld(mul2) if mul2 is not None else 0,
+                      ptr(out2), ld(out2) if out2 is not None else 0)
     if GEMM_TRACE is not None:
         GEMM_TRACE.append({f: getattr(d, f) for f, _ in d._fields_ if not f in ("alpha", "beta")} |
                           {"dtype": dt, "beta": d.beta, "out_f32": out.dtype == torch.float32})
     es, nb = _es(a), max(batch, 1)
     byt = es * (M * K * nb + N * K * (nb if stride_b else 1))
     byt += M * N * nb * (out.element_size() * (2 if beta != 0.0 else 1))
-    byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None))
+    byt += es * M * N * nb * ((preact is not None) + (mul is not None) + (res is not None) + 2 * (out2 is not None))
     byt += 4 * N * (bias is not None) + 4 * M * (colsum is not None)
     peak = "bf16" if a.dtype != torch.float32 else "f32"
     if collect is not None:
@@ -263,8 +264,11 @@ def linear(x, w, bias=None, *, act=0, preact=None, mul=None, res=None, colscale=
                 collect=collect)
 
 
-def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None, collect=None):
-    """dx[M,K] (+)= dy[M,N] @ w[N,K]   (times `mul` elementwise, or times gelu'(gelu_grad_of))."""
+def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None, mul2=None, out2=None,
+                 collect=None):
+    """dx[M,K] (+)= dy[M,N] @ w[N,K]   (times `mul` elementwise, or times gelu'(gelu_grad_of)); with
+    mul2 / out2 also out2 = (dy @ w) * mul2 from the same accumulator (an elementwise product's two
+    input gradients in one pass: out = g * y, out2 = g * x for the product x * y)."""
     M, N = dy.shape
     K = w.shape[1]
     if out is None:
@@ -273,7 +277,7 @@ def linear_dgrad(dy, w, out=None, accumulate=False, mul=None, gelu_grad_of=None,
         mul = gelu_grad_of
     return gemm(dy, w, M=M, N=K, K=N, a_kcontig=True, b_kcontig=False, lda=ld(dy), ldb=ld(w), out=out, ldc=ld(out),
                 beta=1.0 if accumulate else 0.0, mul=mul, ldmul=ld(mul) if mul is not None else 0,
-                mul_gelu_grad=gelu_grad_of is not None, collect=collect)
+                mul_gelu_grad=gelu_grad_of is not None, mul2=mul2, out2=out2, collect=collect)
 
 
 def linear_wgrad(dy, x, out=None, accumulate=False, bias_grad=False, bias_out=None):

@@ -39,7 +39,7 @@ extern "C" {
 typedef void* dfm_stream_t;
 
 const char* dfm_last_error(void);
-int dfm_abi_version(void); /* 12: dfm_build_tag; 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
+int dfm_abi_version(void); /* 13: DfmGemmDesc.mul2 / out2 (second epilogue output); 12: dfm_build_tag; 11: dfm_block_fwd / dfm_block_bwd (+ dfm_block_saved_size /
                               dfm_block_workspace_size); 10: dfm_convffn_fwd / dfm_convffn_bwd (fused ConvFFN); 9: dfm_nmf_fwd / dfm_nmf_bwd (+ dfm_nmf_saved_size); 8: deferred reduction
                               second stages (dfm_partial_sum_group); 7: DfmGemmDesc.workspace_bytes + stride /
                               leading-dimension validation */
@@ -107,6 +107,13 @@ typedef struct DfmGemmDesc {
   long workspace_bytes; /* size of the workspace passed with the call; it must be at least
                            dfm_gemm_workspace_size(d) (for dfm_gemm_group: d[0] carries the size of
                            the one shared workspace, >= dfm_gemm_group_workspace_size) */
+  /* optional second output (ABI 13): out2[m, n] = v * mul2[m, n], v the epilogue value before `mul` /
+   * `res` (after beta, bias, act) — the two products of an elementwise x * y backward
+   * (dy*y -> dx, dy*x -> dy') written by the GEMM that produces dy (batch 1, output dtype, no res) */
+  const void* mul2;
+  long ldmul2;
+  void* out2;
+  long ldout2;
 } DfmGemmDesc;
 
 size_t dfm_gemm_workspace_size(const DfmGemmDesc* d);

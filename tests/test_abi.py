@@ -42,7 +42,7 @@ def test_binding_signatures_match_header():
 
 def test_abi_version_and_error_path():
     from dformer_amd import _lib
-    assert _lib.lib.dfm_abi_version() == 12
+    assert _lib.lib.dfm_abi_version() == 13
     assert _lib.BUILD_TAG.startswith("default red="), _lib.BUILD_TAG
     # argument validation fails before touching the GPU
     st = _lib.lib.dfm_layernorm_fwd(0, 10, 100000, None, 0, None, None, 1e-6, None, 0, None, None, None)
@@ -122,6 +122,8 @@ def test_block_sizes_and_validation():
     dict(stride_b=100),
     dict(stride_c=0),                   # every batch writing one output
     dict(split_k=4, workspace_bytes=1024),  # split-K partials need 4 * 16 * 4800 * 512 * 4 bytes
+    dict(out2=1 << 20, ldout2=512),     # a second output without its multiplier
+    dict(out2=1 << 20, ldout2=512, mul2=1 << 20, ldmul2=512),  # ... with batch 16
 ])
 def test_gemm_validation_rejects_bad_descriptors(bad):
     """dfm_gemm validates leading dimensions, batch strides and the workspace size before any launch

@@ -810,6 +810,33 @@ def test_gemm_group_kcontig_mixed_members(dt, fwd):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,Kd,ldo", [(19200, 256, 384, 640), (1999, 136, 192, 136), (300, 40, 96, 48),
+                                        (4800, 128, 1536, 128), (307200, 64, 96, 64)])
+def test_dgrad_second_output_epilogue(dt, M, N, Kd, ldo):
+    """Input-gradient GEMM with the second epilogue output (the backward of an elementwise product riding
+    on the GEMM that produces its incoming gradient): out = (dy W) * mul, out2 = (dy W) * mul2, on the
+    ring / register-staged / split-K routes, a strided output view, ragged N and the scalar tail."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    dy = (torch.randn(M, Kd, device=DEV, generator=g)).to(dt)
+    wfull = (torch.randn(Kd, N + 24, device=DEV, generator=g) / Kd ** 0.5).to(dt)
+    w = wfull[:, 8:8 + N]  # a column block of a wider weight (ldb = N + 24)
+    m1 = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    m2 = torch.randn(M, N, device=DEV, generator=g).to(dt)
+    outb = torch.zeros(M, ldo, device=DEV, dtype=dt)
+    out = outb[:, :N]
+    out2 = torch.empty(M, N, device=DEV, dtype=dt)
+    k.linear_dgrad(dy, w, out=out, mul=m1, mul2=m2, out2=out2)
+    base = dy.float() @ w.float()
+    assert rel(out.float(), base * m1.float()) < GTOL[dt]
+    assert rel(out2.float(), base * m2.float()) < GTOL[dt]
+    # identical to the plain GEMM followed by the two products on the same (rounded) accumulator
+    plain = k.linear_dgrad(dy, w)
+    if dt == torch.float32:
+        assert rel(out2.float(), plain.float() * m2.float()) < 1e-6
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("rows", [19200, 777, 4800])
 def test_wgrad_group(dt, rows):
     """dfm_gemm_group: the weight gradients queued inside kernels.wgrad_group() (different M / N, bias
