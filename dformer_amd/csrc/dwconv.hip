@@ -345,6 +345,18 @@ DFM_INLINE void w3_pairs(uint2 q, f2v* v) {
 }
 
 template <typename T>
+DFM_INLINE void w3_store(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 q;
+    q.x = (uint32_t)bits16<T>(v[0]) | ((uint32_t)bits16<T>(v[1]) << 16);
+    q.y = (uint32_t)bits16<T>(v[2]) | ((uint32_t)bits16<T>(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = q;
+  } else {
+    *reinterpret_cast<uint2*>(p) = make_uint2(__float_as_uint(v[0]), __float_as_uint(v[1]));
+  }
+}
+
+template <typename T>
 __global__ __launch_bounds__(256) void dw3_stream_wgrad_kernel(int B, int H, int W, int C, int RC, int nstrips,
                                                                int nchunks, int LPU, int UPW,
                                                                const T* __restrict__ x, long ldx,
@@ -637,6 +649,222 @@ __global__ __launch_bounds__(256) void dw7_lds_wgrad_kernel(int B, int H, int W,
   }
 }
 
+// ---------------------------------------------------------------- one-pass 7x7 backward (data + weight)
+// The attention's 7x7 depthwise backward (DFormer.py:80-81, 115, 133; conv and e_conv) in ONE launch over
+// dy: a block (spatial lane, channel slab of NG vectors, as dw7_lds_wgrad_kernel) stages per TH x TW tile
+// the zero-padded input window and the dy window (tile + 3-pixel halo) in LDS once; the tile's input
+// gradient (the dy window against the flipped taps, 7 outputs of one row x half a channel vector per
+// thread) and the weight / bias partials (the dy tile against the input window, thread (g, kernel row i,
+// part) as the weight-gradient kernel) both read that staging. The separate kernels read dy twice from
+// HBM (the input gradient's window, the weight gradient's tile) in two launches.
+template <typename T>
+__global__ __launch_bounds__(256) void dw7_bwd_fused_kernel(int B, int H, int W, int C, int tiles_h, int tiles_w,
+                                                            int nsb, int slabs, const T* __restrict__ x, long ldx,
+                                                            const T* __restrict__ dy, long lddy,
+                                                            const float* __restrict__ w, T* __restrict__ dx, long lddx,
+                                                            int accumulate, float* __restrict__ part) {
+  constexpr int CPT = DwCfg<T>::CPT, CP = CPT / 2, NG = W7L_NG, TH = W7L_TH, TW = W7L_TW, NP = W7L_NP;
+  constexpr int IH = W7L_IH, IW = W7L_IW, NXW = IH * (TW + 6) * NG;  // vectors of one staged window
+  constexpr int NL = (2 * NXW + 255) / 256, NACT = NG * 7 * NP, BQ = 256 / NG;
+  constexpr int HCP = sizeof(T) == 2 ? 2 : 1;  // channel pairs in half a vector (one 8-byte load)
+  static_assert(NG * 2 * 2 * TH == 256, "input-gradient thread map");
+  static_assert(TW == 14, "two 7-column strips per tile row");
+  __shared__ uint4 xs[IH * IW * NG];
+  __shared__ uint4 ds[IH * IW * NG];
+  __shared__ float wl[49 * NG * CPT];  // the slab's taps, flipped (input gradient)
+  const int ncv = C / CPT;
+  const int lid = (int)xcd_remap(blockIdx.x, (long)nsb * slabs);
+  const int sb = lid / slabs;
+  const int cv0 = (lid % slabs) * NG;
+  const long ntiles = (long)B * tiles_h * tiles_w;
+  const int t = threadIdx.x;
+  // weight gradient map (as dw7_lds_wgrad_kernel)
+  const int g = t % NG, i = (t / NG) % 7, prt = t / (NG * 7);
+  const bool active = t < NACT;
+  // input gradient map: channel vector dg, half hf, 7-column strip st, tile row dr
+  const int dg = t & 3, hf = (t >> 2) & 1, st = (t >> 3) & 1, dr = t >> 4;
+  for (int e = t; e < 49 * NG * CPT; e += 256) {
+    const int tap = e / (NG * CPT), c = cv0 * CPT + e % (NG * CPT);
+    wl[e] = c < C ? w[(long)c * 49 + 48 - tap] : 0.f;
+  }
+  f2v acc[7][CP], bs[CP];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int e = 0; e < CP; ++e) acc[j][e] = f2v{0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < CP; ++e) bs[e] = f2v{0.f, 0.f};
+
+  for (long tile = sb; tile < ntiles; tile += nsb) {
+    const int tw = (int)(tile % tiles_w), th = (int)((tile / tiles_w) % tiles_h);
+    const long b = tile / ((long)tiles_w * tiles_h);
+    const int h0 = th * TH, w0 = tw * TW;
+    const long img = b * H * W;
+    uint4 buf[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int v = t + l * 256;
+      buf[l] = make_uint4(0, 0, 0, 0);
+      if (v < 2 * NXW) {
+        const bool isx = v < NXW;
+        const int u = isx ? v : v - NXW;
+        const int gg = u % NG, col = (u / NG) % (TW + 6), row = u / (NG * (TW + 6));
+        const int hh = h0 + row - 3, ww = w0 + col - 3, cv = cv0 + gg;
+        if (hh >= 0 && hh < H && ww >= 0 && ww < W && cv < ncv) {
+          const long pix = img + (long)hh * W + ww;
+          buf[l] = isx ? *reinterpret_cast<const uint4*>(x + pix * ldx + cv * CPT)
+                       : *reinterpret_cast<const uint4*>(dy + pix * lddy + cv * CPT);
+        }
+      }
+    }
+    __syncthreads();  // the previous tile's reads are done
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const int v = t + l * 256;
+      if (v < 2 * NXW) {
+        const bool isx = v < NXW;
+        const int u = isx ? v : v - NXW;
+        const int gg = u % NG, col = (u / NG) % (TW + 6), row = u / (NG * (TW + 6));
+        (isx ? xs : ds)[(row * IW + col) * NG + gg] = buf[l];
+      }
+    }
+    __syncthreads();
+    {  // bias gradient: thread (g, q) sums the tile's pixels q, q + BQ, ... of channel vector g
+      for (int pix = t / NG; pix < TH * TW; pix += BQ) {
+        f2v d[CP];
+        unpack_pairs<T>(ds[((pix / TW + 3) * IW + pix % TW + 3) * NG + g], d);
+#pragma unroll
+        for (int e = 0; e < CP; ++e) bs[e] += d[e];
+      }
+    }
+    {  // input gradient of output row h0 + dr, columns w0 + 7 st .. + 6, channels of half hf of vector dg
+      f2v o[7][HCP];
+#pragma unroll
+      for (int q = 0; q < 7; ++q)
+#pragma unroll
+        for (int e = 0; e < HCP; ++e) o[q][e] = f2v{0.f, 0.f};
+#pragma unroll 1
+      for (int ki = 0; ki < 7; ++ki) {
+        const uint2* dw_ = reinterpret_cast<const uint2*>(ds + ((dr + ki) * IW + 7 * st) * NG + dg) + hf;
+        f2v win[13][HCP];
+#pragma unroll
+        for (int u = 0; u < 13; ++u) w3_pairs<T>(dw_[u * NG * 2], win[u]);
+#pragma unroll
+        for (int kj = 0; kj < 7; ++kj) {
+          const float* wp = wl + (ki * 7 + kj) * NG * CPT + dg * CPT + hf * (CPT / 2);
+          f2v wv[HCP];
+#pragma unroll
+          for (int e = 0; e < HCP; ++e) wv[e] = f2v{wp[2 * e], wp[2 * e + 1]};
+#pragma unroll
+          for (int q = 0; q < 7; ++q)
+#pragma unroll
+            for (int e = 0; e < HCP; ++e) o[q][e] = __builtin_elementwise_fma(wv[e], win[q + kj][e], o[q][e]);
+        }
+      }
+      const int hh = h0 + dr;
+      if (hh < H && cv0 + dg < ncv) {
+        T* drow = dx + (img + (long)hh * W + w0 + 7 * st) * lddx + (cv0 + dg) * CPT + hf * (CPT / 2);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+          if (w0 + 7 * st + q >= W) break;
+          T* dp = drow + q * lddx;
+          float ov[2 * HCP];
+#pragma unroll
+          for (int e = 0; e < HCP; ++e) {
+            ov[2 * e] = o[q][e].x;
+            ov[2 * e + 1] = o[q][e].y;
+          }
+          if (accumulate) {
+            float pv[4];
+            w3_unpack<T>(*reinterpret_cast<const uint2*>(dp), pv);
+#pragma unroll
+            for (int e = 0; e < 2 * HCP; ++e) ov[e] += pv[e];
+          }
+          w3_store<T>(dp, ov);
+        }
+      }
+    }
+    if (active) {  // weight gradient: kernel row i of channel vector g over tile rows prt, prt + NP
+#pragma unroll 1
+      for (int r = prt; r < TH; r += NP) {
+        const uint4* xr = xs + ((r + i) * IW) * NG + g;
+        const uint4* drr = ds + ((r + 3) * IW + 3) * NG + g;
+        f2v xw[7][CP];  // ring: input column q of the row in slot q % 7
+#pragma unroll
+        for (int u = 0; u < 6; ++u) unpack_pairs<T>(xr[u * NG], xw[u]);
+#pragma unroll 1
+        for (int cb = 0; cb < TW; cb += 7) {
+#pragma unroll
+          for (int s7 = 0; s7 < 7; ++s7) {
+            const int c = cb + s7;
+            unpack_pairs<T>(xr[(c + 6) * NG], xw[(s7 + 6) % 7]);
+            f2v d[CP];
+            unpack_pairs<T>(drr[c * NG], d);
+#pragma unroll
+            for (int j = 0; j < 7; ++j)
+#pragma unroll
+              for (int e = 0; e < CP; ++e) acc[j][e] = __builtin_elementwise_fma(d[e], xw[(s7 + j) % 7][e], acc[j][e]);
+          }
+        }
+      }
+    }
+  }
+  // the NP parts of each (g, i) meet in LDS in part order, then part 0 writes the block's partial;
+  // the bias partials of the BQ pixel lanes of each g likewise (lane order)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);
+  constexpr int RS = 7 * CPT + 1;
+  for (int q = 1; q < NP; ++q) {
+    if (active && prt == q) {
+      float* o = red + (g * 7 + i) * RS;
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) {
+          o[j * CPT + 2 * e] = acc[j][e].x;
+          o[j * CPT + 2 * e + 1] = acc[j][e].y;
+        }
+    }
+    __syncthreads();
+    if (active && prt == 0) {
+      const float* o = red + (g * 7 + i) * RS;
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+#pragma unroll
+        for (int e = 0; e < CP; ++e) acc[j][e] += f2v{o[j * CPT + 2 * e], o[j * CPT + 2 * e + 1]};
+    }
+    __syncthreads();
+  }
+  float* bred = red + NG * 7 * RS;  // [BQ][NG][CPT]
+#pragma unroll
+  for (int e = 0; e < CP; ++e) {
+    bred[t * CPT + 2 * e] = bs[e].x;
+    bred[t * CPT + 2 * e + 1] = bs[e].y;
+  }
+  __syncthreads();
+  const long pbase = (long)sb * C * 50;
+  if (active && prt == 0 && cv0 + g < ncv) {
+#pragma unroll
+    for (int e = 0; e < CP; ++e) {
+      const int c = (cv0 + g) * CPT + 2 * e;
+      float* o = part + pbase + (long)c * 50;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        o[i * 7 + j] = acc[j][e].x;
+        o[50 + i * 7 + j] = acc[j][e].y;
+      }
+    }
+  }
+  if (t < NG * CPT) {  // bias: thread (g, e) sums the BQ lanes in order
+    const int gg = t / CPT, e = t % CPT;
+    if (cv0 + gg < ncv) {
+      float sum = 0.f;
+      for (int q = 0; q < BQ; ++q) sum += bred[(q * NG + gg) * CPT + e];
+      part[pbase + (long)((cv0 + gg) * CPT + e) * 50 + 49] = sum;
+    }
+  }
+}
+
 template <typename T>
 long w7l_nsb(int B, int H, int W, int C) {
   const long ntiles = (long)B * cdiv(H, W7L_TH) * cdiv(W, W7L_TW);
@@ -656,6 +884,16 @@ long w7l_launch(int B, int H, int W, int C, const void* x, long ldx, const void*
   return nsb;
 }
 
+template <typename T>
+long b7_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, const float* w,
+               void* dx, long lddx, int acc, float* part, hipStream_t s) {
+  const long nsb = w7l_nsb<T>(B, H, W, C);
+  const unsigned slabs = cdiv(C / DwCfg<T>::CPT, W7L_NG);
+  DFM_LAUNCH(dw7_bwd_fused_kernel<T>, dim3((unsigned)(nsb * slabs)), dim3(256), 0, s, B, H, W, C, cdiv(H, W7L_TH),
+             cdiv(W, W7L_TW), (int)nsb, (int)slabs, (const T*)x, ldx, (const T*)dy, lddy, w, (T*)dx, lddx, acc, part);
+  return nsb;
+}
+
 // ---------------------------------------------------------------- row-streaming 3x3 forward / input gradient
 // The forward counterpart of the streaming weight gradient: a lane owns one 8-byte channel vector
 // and a TW-column strip, keeps its 9 taps + bias and the three input rows of the current output
@@ -666,17 +904,6 @@ W3Geom f3_geom(int B, int H, int W, int C) {
   return w3_geom<T>(B, H, W, C, 2);
 }
 
-template <typename T>
-DFM_INLINE void w3_store(T* p, const float* v) {
-  if constexpr (sizeof(T) == 2) {
-    uint2 q;
-    q.x = (uint32_t)bits16<T>(v[0]) | ((uint32_t)bits16<T>(v[1]) << 16);
-    q.y = (uint32_t)bits16<T>(v[2]) | ((uint32_t)bits16<T>(v[3]) << 16);
-    *reinterpret_cast<uint2*>(p) = q;
-  } else {
-    *reinterpret_cast<uint2*>(p) = make_uint2(__float_as_uint(v[0]), __float_as_uint(v[1]));
-  }
-}
 
 template <typename T, bool FLIP, bool BUF>
 __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W, int C, int RC, int nstrips,
@@ -1101,11 +1328,32 @@ extern "C" int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, cons
                               dfm_stream_t stream) {
   if (defer) *defer = DfmPartialSum{};
   DFM_CHECK_ARG(x && dy && w && dx && dw && workspace, "dfm_dwconv_bwd: null argument");
-  DFM_CHECK_ARG(k == 3, "dfm_dwconv_bwd: k=%d unsupported (3x3 only)", k);
+  DFM_CHECK_ARG(k == 3 || (k == 7 && !add_identity), "dfm_dwconv_bwd: k=%d%s unsupported", k,
+                add_identity ? " with identity" : "");
   DFM_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0, "dfm_dwconv_bwd: bad shape");
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)workspace;
   long nsb;
+  if (k == 7) {  // one pass over dy for the input and the weight gradient (dw7_bwd_fused_kernel)
+    if (dtype == DFM_BF16) {
+      DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy) && dw_aligned<bf16_t>(C, dx, lddx),
+                    "dfm_dwconv_bwd: alignment");
+      nsb = b7_launch<bf16_t>(B, H, W, C, x, ldx, dy, lddy, w, dx, lddx, accumulate, part, s);
+    } else if (dtype == DFM_F16) {
+      DFM_CHECK_ARG(dw_aligned<f16_t>(C, x, ldx) && dw_aligned<f16_t>(C, dy, lddy) && dw_aligned<f16_t>(C, dx, lddx),
+                    "dfm_dwconv_bwd: alignment");
+      nsb = b7_launch<f16_t>(B, H, W, C, x, ldx, dy, lddy, w, dx, lddx, accumulate, part, s);
+    } else if (dtype == DFM_F32) {
+      DFM_CHECK_ARG(dw_aligned<float>(C, x, ldx) && dw_aligned<float>(C, dy, lddy) && dw_aligned<float>(C, dx, lddx),
+                    "dfm_dwconv_bwd: alignment");
+      nsb = b7_launch<float>(B, H, W, C, x, ldx, dy, lddy, w, dx, lddx, accumulate, part, s);
+    } else {
+      dfm_set_error("dfm_dwconv_bwd: bad dtype");
+      return DFM_ERR_DTYPE;
+    }
+    DFM_LAUNCH_CHECK();
+    return second_stage(2, (int)nsb, (long)C * 50, part, dw, db, 50L, 0, defer, s);
+  }
   if (dtype == DFM_BF16) {
     DFM_CHECK_ARG(dw_aligned<bf16_t>(C, x, ldx) && dw_aligned<bf16_t>(C, dy, lddy) && dw_aligned<bf16_t>(C, dx, lddx),
                   "dfm_dwconv_bwd: alignment");

@@ -439,6 +439,9 @@ class AttentionFn(torch.autograd.Function):
             grads["web"], grads["beb"] = K.linear_wgrad(dxep, e2, out=ow, bias_grad=True, bias_out=ob)
             de2 = K.linear_dgrad(dxep, wcast(dt, web))
             ow, ob = gslot(wec), gslot(bec)
+            # (the one-pass 7x7 backward, dfm_dwconv_bwd k = 7, is 4-15 % faster alone but measured slower on the
+            # step: 477.0 / 477.4 vs 479.3 / 478.4 images/s; its 65 KB of LDS per block keeps the two streams'
+            # 7x7 backwards from sharing a CU)
             grads["wec"], grads["bec"] = K.dwconv_bwd_weight(e1, de2, shape, 7, dw=ow, db=ob)
             de1 = K.dwconv_bwd_data(de2, shape, wec, 7)
             ow, ob = gslot2(wef), gslot(bef)

@@ -193,8 +193,9 @@ size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, int k);
 int dfm_dwconv_bwd_weight(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx,
                           const void* dy, long lddy, float* dw, float* db, void* workspace,
                           DfmPartialSum* defer, dfm_stream_t stream);
-/* bwd_data and bwd_weight of a 3x3 in one pass over dy and x (the ConvFFN's pos conv): dx (+= when
- * accumulate), dw, db as above; workspace from dfm_dwconv_bwd_weight_workspace (k = 3 only). */
+/* bwd_data and bwd_weight in one pass over dy and x: dx (+= when accumulate), dw, db as above; workspace
+ * from dfm_dwconv_bwd_weight_workspace. k = 3 (the ConvFFN's pos conv, add_identity allowed) or k = 7 (the
+ * attention's conv / e_conv, add_identity 0; dw and db bit-identical to dfm_dwconv_bwd_weight's). */
 int dfm_dwconv_bwd(int dtype, int B, int H, int W, int C, int k, const void* x, long ldx, const void* dy,
                    long lddy, const float* w, int add_identity, void* dx, long lddx, int accumulate, float* dw,
                    float* db, void* workspace, DfmPartialSum* defer, dfm_stream_t stream);

@@ -299,6 +299,39 @@ def test_dwconv_fused_bwd(dt, ident, acc, B, H, W, C):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("acc", [False, True])
+# every DFormer-B stage geometry (C and C/2), tile-ragged planes, a partial channel slab (C = 40: 5 bf16 /
+# 10 fp32 vectors) and strided views
+@pytest.mark.parametrize("B,H,W,C", [(1, 120, 160, 64), (2, 60, 80, 128), (2, 30, 40, 256), (3, 15, 20, 512),
+                                     (2, 11, 13, 48), (1, 17, 23, 40), (2, 5, 7, 32)])
+def test_dwconv7_fused_bwd(dt, acc, B, H, W, C):
+    """dfm_dwconv_bwd with k = 7 (one pass over dy: input gradient + weight / bias gradient) vs torch fp32,
+    and vs the separate kernels: the weight / bias gradients bit for bit (same tiles, lanes and order)."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(B * H * W + C)
+    xb = torch.randn(B * H * W, C + 8, device=DEV, generator=g).to(dt)
+    x = xb[:, 8:]
+    w = torch.randn(C, 1, 7, 7, device=DEV, generator=g) / 7
+    xr = x.float().reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous().requires_grad_()
+    wr, br = w.clone().requires_grad_(), torch.zeros(C, device=DEV, requires_grad=True)
+    ref = F.conv2d(xr, wr, br, padding=3, groups=C)
+    dyb = torch.randn(B * H * W, C + 16, device=DEV, generator=g).to(dt)
+    dy = dyb[:, 16:]
+    ref.backward(dy.float().reshape(B, H, W, C).permute(0, 3, 1, 2))
+    base = torch.randn(B * H * W, C, device=DEV, generator=g).to(dt)
+    dx = base.clone() if acc else None
+    dx, dw, db = k.dwconv_bwd(x, dy, (B, H, W), w, 7, dx=dx, accumulate=acc)
+    want = xr.grad + (base.float().reshape(B, H, W, C).permute(0, 3, 1, 2) if acc else 0)
+    assert rel(dx.float().reshape(B, H, W, C).permute(0, 3, 1, 2), want) < TOL[dt]
+    assert rel(dw, wr.grad) < TOL[dt] * 2
+    assert rel(db, br.grad) < TOL[dt]
+    dw2, db2 = k.dwconv_bwd_weight(x, dy, (B, H, W), 7)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    dx2 = k.dwconv_bwd_data(dy, (B, H, W), w, 7, dx=base.clone() if acc else None, accumulate=acc)
+    assert rel(dx.float(), dx2.float()) <= {torch.float32: 1e-6, torch.bfloat16: 2.0 ** -7, torch.float16: 2.0 ** -10}[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 # degenerate planes for the streaming 3x3 kernels' clamped-address loads (out-of-image taps read the
 # unit's own first row / column and are zeroed at first use): one pixel, one row, one column, widths
 # below the 4-column strip, a partial last strip and row chunk

@@ -39,6 +39,7 @@ def bench_stage(st):
         ("dw7_fwd", lambda: K.dwconv(x, (B, H, W), w7, b7, 7, out=y), P * C * E * 2),
         ("dw7_bwd_data", lambda: K.dwconv_bwd_data(dy, (B, H, W), w7, 7, dx=dx), P * C * E * 2),
         ("dw7_wgrad", lambda: K.dwconv_bwd_weight(x, dy, (B, H, W), 7), P * C * E * 2),
+        ("dw7_bwd_fused", lambda: K.dwconv_bwd(x, dy, (B, H, W), w7, 7, dx=dx), P * C * E * 3),
         ("ln_fwd", lambda: K.layernorm(x, lnw, lnb, out=xn), P * C * E * 2),
         ("ln_bwd", lambda: K.layernorm_bwd(x, dy, lnw, mu, rstd, dx=dx), P * C * E * 3),
         ("residual_bwd", lambda: K.residual_bwd(dy, x, ls, None, H * W, df=dx), P * C * E * 3),
