@@ -245,9 +245,7 @@ template <typename T> struct W3Cfg { static constexpr int EPL = 8 / sizeof(T); }
 // DFormer-B ConvFFN shapes (tools/dw3_geom_sweep.py, profiles/r04_dw3_geom_sweep.txt): a wave count
 // just past a round boundary cost up to 40 % (30x40x1024 backward 58 vs 42 us at 3200 vs 1920
 // waves); a fixed 3072 / 8192-wave target sat past one on five of the eight shapes.
-template <typename T>
-W3Geom w3_geom(int B, int H, int W, int C, int waves_per_simd = 2) {
-  constexpr int CPT = W3Cfg<T>::EPL;
+inline W3Geom w3_geom_cpl(int B, int H, int W, int C, int CPT, int waves_per_simd) {
   W3Geom g;
   const int G = C / CPT;
   g.LPU = std::min(64, G);
@@ -272,6 +270,10 @@ W3Geom w3_geom(int B, int H, int W, int C, int waves_per_simd = 2) {
   const long waves = (g.units + g.UPW - 1) / g.UPW;
   g.nsb = std::max(1L, (waves + 3) / 4);
   return g;
+}
+template <typename T>
+W3Geom w3_geom(int B, int H, int W, int C, int waves_per_simd = 2) {
+  return w3_geom_cpl(B, H, W, C, W3Cfg<T>::EPL, waves_per_simd);
 }
 
 // Out-of-image taps: every row load is issued unconditionally from an in-image address (the unit's
@@ -1212,9 +1214,205 @@ __global__ __launch_bounds__(256) void dw3_stream_bwd_kernel(int B, int H, int W
   }
 }
 
+// ---------------------------------------------------------------- fused 3x3 backward, row scatter
+// The same sums as dw3_stream_bwd_kernel with every input row unpacked ONCE: a lane owns one channel
+// pair (4 bytes of bf16 / f16) and walks the input rows r = h0-1 .. h1+1 of its unit. dy row r is
+// scattered into the three pending input-gradient rows it feeds (r-1 completes and is stored, r + 1
+// starts); x row r-1 meets the unpacked centre columns of dy rows r-2 .. r (kept from their own
+// steps) for the weight gradient. The gather form above re-unpacks its three-row windows for every
+// output row (3x the unpack work, ~1.3 unpack / address instructions per packed FMA); here a step is
+// 72 packed FMAs against 12 loads and 12 unpacks. Pending rows rotate with period 3; the loop is
+// unrolled by 3 so the rotation is register renaming, not moves. 135 VGPRs (the 8-byte-lane kernel:
+// 250), so 3 waves per SIMD. Units are wave-uniform (whole 64-lane channel slices), so the row / column
+// bookkeeping is scalar. Isolated (tools/ffn_kernels_bench.py, DFormer-B bs 16): s0 234 vs 244 us, s1
+// 135 vs 138, s2 34.2 vs 39.2, s3 25.9 vs 30.2 (mlp; mlp_e2 alike); step 480.4 / 482.0 vs 476.5 / 477.1.
+template <typename T> struct W3Pair { using type = uint32_t; };
+template <> struct W3Pair<float> { using type = uint2; };
+
+template <typename T>
+DFM_INLINE f2v w3p_unpack(typename W3Pair<T>::type q) {
+  if constexpr (std::is_same<T, f16_t>::value) return f2v{h2f((uint16_t)(q & 0xffffu)), h2f((uint16_t)(q >> 16))};
+  else if constexpr (sizeof(T) == 2) return f2v{__uint_as_float(q << 16), __uint_as_float(q & 0xffff0000u)};
+  else return f2v{__uint_as_float(q.x), __uint_as_float(q.y)};
+}
+template <typename T>
+DFM_INLINE typename W3Pair<T>::type w3p_pack(f2v v) {
+  if constexpr (sizeof(T) == 2) return (uint32_t)bits16<T>(v.x) | ((uint32_t)bits16<T>(v.y) << 16);
+  else return make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
+}
+template <typename P>
+DFM_INLINE P w3p_zero() {
+  if constexpr (sizeof(P) == 4) return 0u;
+  else return make_uint2(0u, 0u);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 3) void dw3_rows_bwd_kernel(int B, int H, int W, int C, int RC, int nstrips,
+                                                           int nchunks, const T* __restrict__ x, long ldx,
+                                                           const T* __restrict__ dy, long lddy,
+                                                           const float* __restrict__ w, int add_identity,
+                                                           T* __restrict__ dx, long lddx, int accumulate,
+                                                           float* __restrict__ part) {
+  using P = typename W3Pair<T>::type;
+  constexpr int TW = W3_TW, NX = TW + 2, NV = 20;
+  constexpr long ES = sizeof(T);
+  __shared__ float red[4][NV][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = (blockIdx.y * 64 + lane) * 2;  // every lane owns a channel pair (host: C % 128 == 0)
+  const long units = w3_units(B, nstrips, nchunks);
+
+  f2v wf[9];  // flipped taps (input gradient), centre tap + 1 when add_identity
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const float idt = (tap == 4 && add_identity) ? 1.0f : 0.0f;
+    wf[tap] = f2v{w[(long)c0 * 9 + 8 - tap] + idt, w[(long)(c0 + 1) * 9 + 8 - tap] + idt};
+  }
+  f2v acc[10];
+#pragma unroll
+  for (int a = 0; a < 10; ++a) acc[a] = f2v{0.f, 0.f};
+  const unsigned c0b = (unsigned)(c0 * ES);  // the lane's byte offset in a pixel; the rest of every address is scalar
+
+  // units are wave-uniform: row / column bookkeeping and the row and column base addresses are scalar,
+  // so a load is one scalar address plus the lane's channel offset (global_load saddr + voffset)
+  for (long u = (long)blockIdx.x * 4 + wave; u < units; u += (long)gridDim.x * 4) {
+    const int strip = (int)(u % nstrips), chunk = (int)((u / nstrips) % nchunks);
+    const long b = u / ((long)nstrips * nchunks);
+    const int w0 = strip * TW, h0 = chunk * RC, h1 = min(h0 + RC, H);
+    unsigned cm = 0;  // in-image window columns (out-of-image ones read column w0 and are zeroed)
+    long xcol[NX], ycol[NX];
+#pragma unroll
+    for (int q = 0; q < NX; ++q) {
+      const bool in = w0 - 1 + q >= 0 && w0 - 1 + q < W;
+      cm |= (unsigned)in << q;
+      const long cc = in ? w0 - 1 + q : w0;
+      xcol[q] = cc * ldx * ES;
+      ycol[q] = cc * lddy * ES;
+    }
+    const bool edge = cm != (1u << NX) - 1;
+    const char* xim = reinterpret_cast<const char*>(x + b * H * W * ldx);
+    const char* yim = reinterpret_cast<const char*>(dy + b * H * W * lddy);
+    auto fetch = [&](const char* im, long ld, const long* col, int h, P* r) -> bool {
+      const bool ok = h >= 0 && h < H;
+      const char* rp = im + (long)(ok ? h : h0) * W * ld * ES;
+#pragma unroll
+      for (int q = 0; q < NX; ++q) r[q] = *reinterpret_cast<const P*>(rp + col[q] + c0b);
+      return ok;
+    };
+    auto unpack_row = [&](const P* r, bool ok, f2v* v) {
+      if (ok && !edge) {
+#pragma unroll
+        for (int q = 0; q < NX; ++q) v[q] = w3p_unpack<T>(r[q]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < NX; ++q) v[q] = (ok && ((cm >> q) & 1u)) ? w3p_unpack<T>(r[q]) : f2v{0.f, 0.f};
+      }
+    };
+    // one packed row buffer per operand: a step unpacks the row fetched by the previous step, then
+    // fetches the next one into the same registers (its latency hides under this step's FMAs)
+    P D[NX], X[NX];
+    bool dok, xok = false;
+    f2v O[3][TW], Cc[3][TW];  // pending input-gradient rows; unpacked dy centre columns (chunk rows only)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int t = 0; t < TW; ++t) O[i][t] = Cc[i][t] = f2v{0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NX; ++q) X[q] = w3p_zero<P>();
+    dok = fetch(yim, lddy, ycol, h0 - 1, D);
+    int r = h0 - 1;
+    // step r (k = (r - h0 + 1) % 3): D holds dy row r, X x row r - 1; fetches dy row r + 1 and x row r.
+    // Rows past h1 + 1 / h1 are never used for anything that is kept.
+    auto step = [&](auto kc) {
+      constexpr int k = decltype(kc)::value, k1 = (k + 1) % 3, k2 = (k + 2) % 3;
+      f2v dv[NX], xv[NX];
+      unpack_row(D, dok, dv);
+      dok = fetch(yim, lddy, ycol, r + 1, D);
+      unpack_row(X, xok, xv);
+      xok = fetch(xim, ldx, xcol, r, X);
+      // dy row r feeds input-gradient rows r - 1 (taps a = 2), r (a = 1), r + 1 (a = 0, the row's first)
+#pragma unroll
+      for (int t = 0; t < TW; ++t) {
+        O[k1][t] = wf[0] * dv[t];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          O[k2][t] = __builtin_elementwise_fma(wf[6 + j], dv[t + j], O[k2][t]);
+          O[k][t] = __builtin_elementwise_fma(wf[3 + j], dv[t + j], O[k][t]);
+          if (j) O[k1][t] = __builtin_elementwise_fma(wf[j], dv[t + j], O[k1][t]);
+        }
+      }
+      if (r >= h0 && r < h1) {  // dy rows of this chunk carry the weight gradient
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          Cc[k][t] = dv[t + 1];
+          acc[9] += dv[t + 1];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < TW; ++t) Cc[k][t] = f2v{0.f, 0.f};
+      }
+      // x row r - 1 against dy rows r (a = 0), r - 1 (a = 1), r - 2 (a = 2)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int cr = a == 0 ? k : (a == 1 ? k2 : k1);
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int t = 0; t < TW; ++t) acc[a * 3 + j] = __builtin_elementwise_fma(Cc[cr][t], xv[t + j], acc[a * 3 + j]);
+      }
+      // input-gradient row r - 1 is complete
+      if (r - 1 >= h0 && r - 1 < h1) {
+        char* dp = reinterpret_cast<char*>(dx + ((b * H + r - 1) * W + w0) * lddx);
+#pragma unroll
+        for (int t = 0; t < TW; ++t) {
+          if (w0 + t >= W) break;
+          P* op = reinterpret_cast<P*>(dp + t * lddx * ES + c0b);
+          f2v v = O[k2][t];
+          if (accumulate) v += w3p_unpack<T>(*op);
+          *op = w3p_pack<T>(v);
+        }
+      }
+    };
+    for (;;) {
+      step(std::integral_constant<int, 0>{});
+      if (++r > h1 + 1) break;
+      step(std::integral_constant<int, 1>{});
+      if (++r > h1 + 1) break;
+      step(std::integral_constant<int, 2>{});
+      if (++r > h1 + 1) break;
+    }
+  }
+
+  // block reduction over the 4 waves
+  const long pbase = (long)blockIdx.x * C * 10;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) red[wave][v][lane] = (v & 1) ? acc[v >> 1].y : acc[v >> 1].x;
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < NV * 64; idx += 256) {
+    const int v = idx / 64, l = idx % 64;
+    const int c = (blockIdx.y * 64 + l) * 2 + (v & 1);
+    part[pbase + (long)c * 10 + (v >> 1)] = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
+  }
+}
+
+// waves per SIMD of dw3_rows_bwd_kernel (135 VGPRs; its geometry's round size). Capped at 4 (128 VGPRs)
+// it spills and is 10-22 % slower (s0 286 vs 234 us; step 470.2 vs 480.8 images/s)
+constexpr int W3R_WPS = 3;
+
+// the row-scatter kernel: whole 64-lane channel slices (wave-uniform units), 32-bit byte offsets in a row
+inline bool w3r_ok(int W, int C, long ldx, long lddy, long lddx, long es) {
+  return C % 128 == 0 && (long)W * std::max({ldx, lddy, lddx}) * es < (1L << 31);
+}
+
 template <typename T>
 long b3_launch(int B, int H, int W, int C, const void* x, long ldx, const void* dy, long lddy, const float* w,
                int id, void* dx, long lddx, int acc, float* part, hipStream_t s) {
+  if (w3r_ok(W, C, ldx, lddy, lddx, sizeof(T))) {
+    const W3Geom g = w3_geom_cpl(B, H, W, C, 2, W3R_WPS);
+    DFM_LAUNCH((dw3_rows_bwd_kernel<T>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C,
+               g.RC, g.nstrips, g.nchunks, (const T*)x, ldx, (const T*)dy, lddy, w, id, (T*)dx, lddx, acc, part);
+    return g.nsb;
+  }
   const W3Geom g = w3_geom<T>(B, H, W, C);
   DFM_LAUNCH((dw3_stream_bwd_kernel<T>), dim3((unsigned)g.nsb, (unsigned)g.slices), dim3(256), 0, s, B, H, W, C,
                      g.RC, g.nstrips, g.nchunks, g.LPU, g.UPW, (const T*)x, ldx, (const T*)dy, lddy, w, id,
@@ -1316,7 +1514,8 @@ extern "C" size_t dfm_dwconv_bwd_weight_workspace(int B, int H, int W, int C, in
   long nsb = 1;
   if (k == 3)
     for (int occ = 2; occ <= 3; ++occ)  // fused backward (2 waves / SIMD), weight gradient alone (3)
-      nsb = std::max({nsb, w3_geom<float>(B, H, W, C, occ).nsb, w3_geom<bf16_t>(B, H, W, C, occ).nsb});
+      nsb = std::max({nsb, w3_geom<float>(B, H, W, C, occ).nsb, w3_geom<bf16_t>(B, H, W, C, occ).nsb,
+                      w3_geom_cpl(B, H, W, C, 2, W3R_WPS).nsb});  // (row-scatter fused backward)
   else if (k == 7)
     nsb = std::max(w7l_nsb<float>(B, H, W, C), w7l_nsb<bf16_t>(B, H, W, C));
   return (size_t)nsb * C * (k * k + 1) * sizeof(float);

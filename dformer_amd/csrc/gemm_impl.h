@@ -1199,7 +1199,8 @@ int gemm_typed(const DfmGemmDesc* d, const void* A, const void* B, void* C, void
   // per step replayed in isolation, tools/gemm_variants.py) measured flat on the step (37.45-37.59
   // ms/step either way, profiles/r04_glds_variants.txt).
   if constexpr (sizeof(T) == 2) {  // the LDS-DMA ring kernel: bf16 and fp16
-    const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 256) : d->K >= 128);
+    // (wide-N x K = 256 forward GEMMs, the stage-2 fc1, on the ring too: 477.2 -> 480.7 images/s)
+    const bool route = ak && (bk ? !(a.Nw > 512 && d->K <= 128) : d->K >= 128);
     if (glds_ok && route) {
       if (BN == 32) return glds_ak<T, 128, 32, 4, 4, 2, 3>(a, bk, s);
       // the decoder's 1x1 convs (76,800 rows x 512-896 x 512-896): 128 x 128 tiles, 8 waves
