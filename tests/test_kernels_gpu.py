@@ -216,8 +216,10 @@ def test_layernorm_views_accumulate(dt, C):
 @pytest.mark.parametrize("ks,ident", [(7, False), (3, True)])
 # (1, 9, 10, 520) / (1, 33, 34, 520): channel vectors not a multiple of the 64-lane slice of the
 # row-streaming kernels (partial last slice), the latter also on the streaming 3x3 forward's planes
+# (planes below the 7-row window, whole 128-channel slices)
 @pytest.mark.parametrize("B,H,W,C", [(2, 11, 13, 48), (1, 30, 40, 64), (2, 5, 7, 16), (1, 33, 41, 40),
-                                     (1, 9, 10, 520), (1, 33, 34, 520)])
+                                     (1, 9, 10, 520), (1, 33, 34, 520), (2, 11, 13, 128), (1, 3, 2, 256),
+                                     (2, 30, 40, 256), (1, 15, 20, 512), (1, 1, 1, 128)])
 def test_dwconv(dt, ks, ident, B, H, W, C):
     k = K()
     x = torch.randn(B, H, W, C, device=DEV).to(dt)
@@ -237,6 +239,34 @@ def test_dwconv(dt, ks, ident, B, H, W, C):
     dw, db = k.dwconv_bwd_weight(x.view(-1, C), dy.view(-1, C), (B, H, W), ks)
     assert rel(dw, wr.grad) < TOL[dt] * 2
     assert rel(db, br.grad) < TOL[dt]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("flip", [False, True])
+@pytest.mark.parametrize("B,H,W,C", [(2, 19, 37, 128), (1, 60, 80, 128), (3, 8, 5, 256), (2, 7, 7, 384)])
+def test_dwconv7_strided_accumulate(dt, flip, B, H, W, C):
+    """7x7 on column-slice views at 128-lane channel multiples: forward with and without bias, and the
+    input gradient (flipped taps) accumulated into a strided destination."""
+    k = K()
+    g = torch.Generator(device=DEV).manual_seed(B * H * W + C + flip)
+    xb = torch.randn(B * H * W, C + 16, device=DEV, generator=g).to(dt)
+    x = xb[:, 8:8 + C]
+    w = torch.randn(C, 1, 7, 7, device=DEV, generator=g) / 7
+    bias = torch.randn(C, device=DEV, generator=g)
+    xr = x.float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    base = torch.randn(B * H * W, C + 8, device=DEV, generator=g).to(dt)
+    out = base.clone()
+    if flip:
+        k.dwconv_bwd_data(x, (B, H, W), w, 7, False, dx=out[:, 8:], accumulate=True)
+        ref = F.conv_transpose2d(xr, w, padding=3, groups=C) + base[:, 8:].float().reshape(B, H, W, C).permute(0, 3, 1, 2)
+    else:
+        k.dwconv(x, (B, H, W), w, None, 7, False, out=out[:, 8:])
+        ref = F.conv2d(xr, w, None, padding=3, groups=C)
+    assert rel(out[:, 8:].float().reshape(B, H, W, C).permute(0, 3, 1, 2), ref) < TOL[dt]
+    assert torch.equal(out[:, :8], base[:, :8])
+    if not flip:
+        y = k.dwconv(x, (B, H, W), w, bias, 7, False)
+        assert rel(y.float().reshape(B, H, W, C).permute(0, 3, 1, 2), F.conv2d(xr, w, bias, padding=3, groups=C)) < TOL[dt]
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -7,6 +7,7 @@
 #   bash tools/gpu_run.sh py     TAG SCRIPT [ARGS...]  one diagnostic python script (output under gpurun_out/)
 #   bash tools/gpu_run.sh final  TAG              round record: suite, smoke, bench + table, PMC passes over the
 #                                                 census-dominant kernels, rocprofv3 --stats, kernel trace, configs 2 / 5
+#   bash tools/gpu_run.sh record TAG              the same without the suite
 # Every library load prints its path and build tag (dformer_amd._lib), so a variant run names what it loaded.
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
@@ -52,8 +53,8 @@ case $CMD in
     S=$1; shift
     timeout -k 10 600 python -u "$S" "$@" > gpurun_out/${T}_py.log 2>&1; rc=$?
     tail -40 gpurun_out/${T}_py.log; exit $rc ;;
-  final)
-    suite || exit $?
+  final|record)  # record = final without the suite (run it as its own call when a box's limit is tight)
+    [ $CMD = final ] && { suite || exit $?; }
     timeout -k 10 400 python -u bench.py --table-out gpurun_out/${T}_step_table.json > gpurun_out/${T}_bench.log 2>&1 || exit 12
     tail -1 gpurun_out/${T}_bench.log | cut -c1-600
     bash tools/gpu_pmc.sh ${T} gpurun_out/${T}_step_table.json || exit 15
