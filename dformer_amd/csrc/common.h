@@ -62,6 +62,28 @@ DFM_INLINE void normal_cdf_pdf(float x, float& cdf, float& pdf) {
   cdf = u < 0.0f ? tail : 1.0f - tail;
   pdf = 0.39894228040143268f * e;
 }
+// The same on a channel pair: every non-transcendental step as one v_pk_* instruction (the 0.5 of the
+// tail is folded into the coefficients, exact in binary), so each element is bit-identical to
+// normal_cdf_pdf's; 25 instructions per pair instead of 2 x 19.
+typedef __attribute__((ext_vector_type(2))) float float2_t;
+DFM_INLINE void normal_cdf_pdf2(float2_t x, float2_t& cdf, float2_t& pdf) {
+  const float2_t u = x * 0.70710678118654752f;
+  const float2_t au = __builtin_elementwise_abs(u);
+  const float2_t den = __builtin_elementwise_fma(au, float2_t{0.3275911f, 0.3275911f}, float2_t{1.0f, 1.0f});
+  const float2_t t = float2_t{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  float2_t p = __builtin_elementwise_fma(float2_t{0.5307027145f, 0.5307027145f}, t,
+                                         float2_t{-0.7265760135f, -0.7265760135f});
+  p = __builtin_elementwise_fma(p, t, float2_t{0.7107068705f, 0.7107068705f});
+  p = __builtin_elementwise_fma(p, t, float2_t{-0.142248368f, -0.142248368f});
+  p = __builtin_elementwise_fma(p, t, float2_t{0.127414796f, 0.127414796f});
+  p *= t;
+  const float2_t z = (au * au) * -1.4426950408889634f;
+  const float2_t e = float2_t{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)};
+  const float2_t tail = p * e;  // Phi(-|x|)
+  cdf.x = u.x < 0.0f ? tail.x : 1.0f - tail.x;
+  cdf.y = u.y < 0.0f ? tail.y : 1.0f - tail.y;
+  pdf = e * 0.39894228040143268f;
+}
 DFM_INLINE float gelu_f(float x) {
   float c, d;
   normal_cdf_pdf(x, c, d);

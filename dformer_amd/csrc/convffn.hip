@@ -328,12 +328,13 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
 #pragma unroll
       for (int ks = 0; ks < G::KS2; ++ks) {
         const int cc = 32 * ks + 8 * lq;
-        float hp[8];
+        // DW3x3 + bias on channel pairs (v_pk_fma_f32), GELU / GELU' packed too (normal_cdf_pdf2)
+        float2_t hp2[4];
         {
           const float4 p0 = *reinterpret_cast<const float4*>(Pw + 9 * HC + cc);
           const float4 p1 = *reinterpret_cast<const float4*>(Pw + 9 * HC + cc + 4);
-          hp[0] = p0.x; hp[1] = p0.y; hp[2] = p0.z; hp[3] = p0.w;
-          hp[4] = p1.x; hp[5] = p1.y; hp[6] = p1.z; hp[7] = p1.w;
+          hp2[0] = float2_t{p0.x, p0.y}; hp2[1] = float2_t{p0.z, p0.w};
+          hp2[2] = float2_t{p1.x, p1.y}; hp2[3] = float2_t{p1.z, p1.w};
         }
         const T* hb = Hw + (py * G::EW + px) * G::HP + cc;
 #pragma unroll
@@ -343,19 +344,22 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
           unpack8w<T>(u, hv);
           const float4 q0 = *reinterpret_cast<const float4*>(Pw + tap * HC + cc);
           const float4 q1 = *reinterpret_cast<const float4*>(Pw + tap * HC + cc + 4);
-          const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+          const float2_t wv[4] = {float2_t{q0.x, q0.y}, float2_t{q0.z, q0.w}, float2_t{q1.x, q1.y},
+                                  float2_t{q1.z, q1.w}};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) hp[j] = fmaf(wv[j], hv[j], hp[j]);
+          for (int j = 0; j < 4; ++j)
+            hp2[j] = __builtin_elementwise_fma(wv[j], float2_t{hv[2 * j], hv[2 * j + 1]}, hp2[j]);
         }
         float g[8];
         if constexpr (SAVEG) {  // GELU and GELU' from one erf, both stored for the op-level backward
           float gd[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float cdf, pdf;
-            normal_cdf_pdf(hp[j], cdf, pdf);
-            g[j] = hp[j] * cdf;
-            gd[j] = fmaf(hp[j], pdf, cdf);
+          for (int j = 0; j < 4; ++j) {
+            float2_t cdf, pdf;
+            normal_cdf_pdf2(hp2[j], cdf, pdf);
+            const float2_t gg = hp2[j] * cdf, dd = __builtin_elementwise_fma(hp2[j], pdf, cdf);
+            g[2 * j] = gg.x; g[2 * j + 1] = gg.y;
+            gd[2 * j] = dd.x; gd[2 * j + 1] = dd.y;
           }
           if (pin) {
             st8<T>(static_cast<T*>(a.gout) + pix * R + c0 + cc, g);
@@ -363,7 +367,12 @@ __global__ __launch_bounds__(256, 2) void ffn_fwd_kernel(FfnFwdArgs a) {
           }
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) g[j] = gelu_f(hp[j]);
+          for (int j = 0; j < 4; ++j) {
+            float2_t cdf, pdf;
+            normal_cdf_pdf2(hp2[j], cdf, pdf);
+            const float2_t gg = hp2[j] * cdf;
+            g[2 * j] = gg.x; g[2 * j + 1] = gg.y;
+          }
         }
         const bf16x8_t gf = pack16x8<T>(g);
 #pragma unroll

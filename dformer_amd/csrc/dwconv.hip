@@ -19,6 +19,20 @@ template <typename T> struct DwCfg { static constexpr int CPT = 16 / sizeof(T); 
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+// GELU(v) and GELU'(v) of N (even) channels, a channel pair per packed evaluation
+template <int N>
+DFM_INLINE void gelu_pairs(const float* v, float* g, float* d) {
+#pragma unroll
+  for (int e = 0; e < N; e += 2) {
+    const f2v x = f2v{v[e], v[e + 1]};
+    f2v cdf, pdf;
+    normal_cdf_pdf2(x, cdf, pdf);
+    const f2v gg = x * cdf, dd = __builtin_elementwise_fma(x, pdf, cdf);
+    g[e] = gg.x; g[e + 1] = gg.y;
+    d[e] = dd.x; d[e + 1] = dd.y;
+  }
+}
+
 // one 16-byte vector -> CPT/2 channel pairs (packed-FMA operands; bf16 / f16 widen exactly)
 template <typename T>
 DFM_INLINE void unpack_pairs(uint4 q, f2v* v) {
@@ -199,13 +213,7 @@ __global__ __launch_bounds__(256) void dw_tile_fwd_kernel(int B, int H, int W, i
     }
     if (gout) {  // GELU output; y holds the pre-activation or (flag 2) its GELU derivative
       float gv[CPT], dv[CPT];
-#pragma unroll
-      for (int e = 0; e < CPT; ++e) {
-        float cdf, pdf;
-        normal_cdf_pdf(acc[t][e], cdf, pdf);
-        gv[e] = acc[t][e] * cdf;
-        dv[e] = fmaf(acc[t][e], pdf, cdf);
-      }
+      gelu_pairs<CPT>(acc[t], gv, dv);
       stv<T>(yp, (add_identity & 2) ? dv : acc[t]);
       stv<T>(gout + p * ldg + c0, gv);
     } else {
@@ -1016,13 +1024,7 @@ __global__ __launch_bounds__(256) void dw3_stream_fwd_kernel(int B, int H, int W
         }
         if (gout) {  // GELU output; y holds the pre-activation or (flag 2) its GELU derivative
           float gv[CPT], dv[CPT];
-#pragma unroll
-          for (int e = 0; e < CPT; ++e) {
-            float cdf, pdf;
-            normal_cdf_pdf(acc[t][e], cdf, pdf);
-            gv[e] = acc[t][e] * cdf;
-            dv[e] = fmaf(acc[t][e], pdf, cdf);
-          }
+          gelu_pairs<CPT>(acc[t], gv, dv);
           w3_store<T>(yp, (add_identity & 2) ? dv : acc[t]);
           w3_store<T>(grow + t * ldg, gv);
         } else {
