@@ -61,12 +61,13 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs a, const T* 
   const T* Bp = (const T*)a.B;
 
   // ---- the block's W slice -> LDS as [n][k] (zero rows past N), bias / column scale
+  // (K < KD, a multiple of 16: the image's columns / rows k >= K are zero, and so are the A fragments there)
   if constexpr (BKC) {  // W[n][k]: 16-byte k-vectors
     for (int e = threadIdx.x; e < WIDE_NSL * (KD / 8); e += 256) {
       const int nl = e / (KD / 8), kc = (e % (KD / 8)) * 8;
       const int n = n0 + nl;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < a.N) v = *reinterpret_cast<const uint4*>(Bp + (long)n * a.ldb + kc);
+      if (n < a.N && kc < a.K) v = *reinterpret_cast<const uint4*>(Bp + (long)n * a.ldb + kc);
       *reinterpret_cast<uint4*>(wimg + nl * CF::WP + kc) = v;
     }
   } else {  // W[k][n]: 16-byte n-vectors transposed into the [n][k] image
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs a, const T* 
       const int k = e / (WIDE_NSL / 8), nl = (e % (WIDE_NSL / 8)) * 8;
       const int n = n0 + nl;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < a.N) v = *reinterpret_cast<const uint4*>(Bp + (long)k * a.ldb + n);
+      if (n < a.N && k < a.K) v = *reinterpret_cast<const uint4*>(Bp + (long)k * a.ldb + n);
       const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) reinterpret_cast<uint16_t*>(wimg)[(nl + i) * CF::WP + k] = h[i];
@@ -92,7 +93,15 @@ __global__ __launch_bounds__(256, 2) void gemm_wide_kernel(GemmArgs a, const T* 
     const int row = min(ms * WIDE_MS + wid * 16 + (lane & 15), a.M - 1);
     const T* p = A + (long)row * a.lda + 8 * (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) af[s] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p + 32 * s));
+    for (int s = 0; s < KS; ++s) {
+      if (s < KS - 1 || a.K == KD) {
+        af[s] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p + 32 * s));
+      } else {  // the padded last k-step: lanes past K load their row's first vector and zero it
+        const bool kin = 32 * s + 8 * (lane >> 4) < a.K;
+        const uint4 v = *reinterpret_cast<const uint4*>(p + (kin ? 32 * s : 0));
+        af[s] = __builtin_bit_cast(bf16x8_t, kin ? v : make_uint4(0, 0, 0, 0));
+      }
+    }
   };
   auto load_e = [&](int ms, uint4* ev) {  // epilogue operand rows, coalesced 16-byte chunks
 #pragma unroll
@@ -218,7 +227,8 @@ bool wide_eligible(const GemmArgs& a, const DfmGemmDesc* d) {
   if (!d->a_kcontig || a.splits != 1 || a.batch != 1 || d->colsum || d->c_f32 || d->out2 || !a.ala || !a.alb ||
       !a.vec_ok)
     return false;
-  if (d->K % 32 != 0 || d->K > 128 || d->K < 32 || d->N % 8 != 0 || d->M < 65536 || d->N < 144) return false;
+  // K a multiple of 16 (48 / 80 / 112: DFormer-Large's stage-0 depth branch, C = 48) padded to the next 32
+  if (d->K % 16 != 0 || d->K > 128 || d->K < 32 || d->N % 8 != 0 || d->M < 65536 || d->N < 144) return false;
   const int tiles = (d->mul != nullptr) + (d->res != nullptr) + (d->beta != 0.0f);
   if (tiles > 1) return false;
   if (d->mul && d->ldmul % 8 != 0) return false;
@@ -253,10 +263,10 @@ int wide_launch_cfg(GemmArgs& a, const DfmGemmDesc* d, hipStream_t s) {
 
 template <typename T, bool BKC>
 int wide_launch_k(GemmArgs& a, const DfmGemmDesc* d, hipStream_t s) {
-  switch (d->K) {
-    case 32: return wide_launch_cfg<T, 32, BKC>(a, d, s);
-    case 64: return wide_launch_cfg<T, 64, BKC>(a, d, s);
-    case 96: return wide_launch_cfg<T, 96, BKC>(a, d, s);
+  switch ((d->K + 31) / 32) {
+    case 1: return wide_launch_cfg<T, 32, BKC>(a, d, s);
+    case 2: return wide_launch_cfg<T, 64, BKC>(a, d, s);
+    case 3: return wide_launch_cfg<T, 96, BKC>(a, d, s);
     default: return wide_launch_cfg<T, 128, BKC>(a, d, s);
   }
 }

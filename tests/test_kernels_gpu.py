@@ -966,8 +966,11 @@ def test_gemm_nmf_backward_input_gradient_descriptor(dt):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+# (the last three: the tall short-K kernel, its K padded to a multiple of 32 — DFormer-Large's C = 48 —,
+# ragged M, strided A)
 @pytest.mark.parametrize("M,N,Kd,ldx", [(19200, 256, 256, 256), (4800 + 37, 200, 1024, 1032), (130, 64, 64, 64),
-                                        (307200 // 16, 512, 64, 64), (777, 1152, 128, 136)])
+                                        (307200 // 16, 512, 64, 64), (777, 1152, 128, 136), (70000, 384, 48, 56),
+                                        (65536 + 77, 192, 80, 80), (66000, 160, 112, 120)])
 def test_gemm_fused_epilogues_step_shapes(dt, M, N, Kd, ldx):
     """Forward and input-gradient GEMMs at step-like shapes (whichever kernel the routing picks) with
     every fused epilogue the Block uses: bias + GELU with GELU' stored from a column offset (act 3),
