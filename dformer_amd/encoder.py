@@ -109,8 +109,8 @@ _SIDE = {}
 
 
 def _side_stream(dev):
-    """The depth-branch ConvFFN (mlp_e2) stream: independent of the RGB branch's ConvFFN within a
-    Block, so the two overlap (the stage-2/3 kernels alone leave most CUs idle)."""
+    """The RGB ConvFFN's stream: independent of the depth branch's ConvFFN (mlp_e2) within a Block, so
+    the two overlap (the stage-2/3 kernels alone leave most CUs idle)."""
     s = _SIDE.get(dev)
     if s is None:
         s = _SIDE[dev] = torch.cuda.Stream(device=dev)
@@ -171,21 +171,24 @@ class Block(nn.Module):
             K.TAG = st + ".mlp"
             x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
             return x2.view(B, H, W, C), xe1.view(B, H, W, C // 2)  # DFormer.py:177-181: e_back's output
-        # the RGB and depth ConvFFNs are independent: the depth one runs on a side stream (and so
-        # does its backward: autograd replays a node on its forward's stream), which fills the GPU
-        # at the late stages where each kernel alone is latency-bound
+        # the RGB and depth ConvFFNs are independent: the RGB one runs on a side stream (and so does its
+        # backward: autograd replays a node on its forward's stream) while the depth one runs on the
+        # step's stream; the overlap fills the GPU at the late stages where each kernel alone is
+        # latency-bound. (RGB on the side: 491.8 / 491.0 vs 488.2 / 487.8 images/s with the depth
+        # ConvFFN there — the side stream's kernels get the smaller share of the CUs, and the join waited
+        # 2.3 ms per step on the depth ConvFFN finishing after the RGB one, profiles/r06_queue_analysis.txt)
         side = _side_stream(x.device) if x1.is_cuda else None
         if side is not None:
             main = torch.cuda.current_stream(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                K.TAG = st + ".mlp_e2"
-                xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
-            xe1.record_stream(side)
-            K.TAG = st + ".mlp"
-            x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
+                K.TAG = st + ".mlp"
+                x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)
+            x1.record_stream(side)
+            K.TAG = st + ".mlp_e2"
+            xe2 = self.mlp_e2.fused(xe1, shape, rs[3], self.layer_scale_2_e)
             main.wait_stream(side)
-            xe2.record_stream(main)
+            x2.record_stream(main)
         else:
             K.TAG = st + ".mlp"
             x2 = self.mlp.fused(x1, shape, rs[1], self.layer_scale_2)

@@ -278,8 +278,9 @@ class ConvFFNFn(torch.autograd.Function):
 
 # ====================================================================== Attention (+ residuals)
 # The depth branch of the attention BACKWARD (dual product -> e_back -> DW7x7 -> e_fore gradients,
-# DFormer.py:84-88, 133) is the longer chain (8 launches) and independent of the RGB branch until
-# the q|q_cut|l gradients, so it is issued on a side stream. Measured on MI355X, DFormer-B bf16
+# DFormer.py:84-88, 133) is independent of the RGB branch (pooled attention, q * a, the 7x7
+# modulation) until the q|q_cut|l gradients, so the two overlap on two streams (round 6: the RGB part
+# on the side stream, the depth branch on the step's own). Measured on MI355X, DFormer-B bf16
 # bs 16 graph replay: 407.4-408.0 vs 386.9-387.5 images/s on one stream. (The forward's depth
 # branch on a side stream measured 381.6 vs 383.4 images/s and was dropped: it is short and the
 # fork / join costs what the overlap gains; a second backward stream for the pooled-attention
@@ -448,54 +449,59 @@ class AttentionFn(torch.autograd.Function):
             grads["wef"], grads["bef"] = K.linear_wgrad(de1, xen, out=ow, bias_grad=True, bias_out=ob)
             return K.linear_dgrad(de1, wcast(dt, wef)), (dxep, de2, de1)
 
-        if side is not None:  # the depth branch overlaps the RGB branch; joined before q|q_cut|l
+        def rgb_part():  # the pooled attention, q * a and the 7x7 modulation branch
+            dg = torch.empty(P, C, device=dev, dtype=dt)
+            dxn = dpooled = dkv = None
+
+            def pooled_branch():  # softmax(q_pool k^T) v over the pooled queries, DFormer.py:119-131
+                kv, pooled, m, o, lse = saved_attn
+                dh = C // heads // 2
+                do = K.bilinear_bwd(dfa, (7, 7), (H, W), B)
+                dm = torch.empty_like(m)
+                dkv = torch.empty(P, C, device=dev, dtype=dt)
+                K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
+                                  dkv[:, :Ch], dkv[:, Ch:])
+                ow, ob = gslot2(wsc), gslot(bsc)
+                grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, out=ow, bias_grad=True, bias_out=ob)
+                dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
+                dxn = K.pool7_bwd(dpooled[:, :C], shape)
+                ow, ob = gslot2(wkv), gslot(bkv)
+                grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, out=ow, bias_grad=True, bias_out=ob)
+                return dxn, dpooled, dkv, (do, dm)
+
+            tmp = ()
+            if window:
+                dxn, dpooled, dkv, tmp = pooled_branch()
+            # q * a (dq, da came out of the projection's input-gradient epilogue)
+            ow, ob = gslot2(wa), gslot(ba)
+            grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=ow, bias_grad=True, bias_out=ob)
+            dapre = torch.empty(P, C, device=dev, dtype=dt)
+            # the a and kv input gradients as one grouped launch
+            calls = [lambda c: K.linear_dgrad(da, wcast(dt, wa), out=dapre, collect=c)]
+            if window:
+                calls.append(lambda c: K.linear_dgrad(dkv, wcast(dt, wkv), out=dg, collect=c))
+            K.gemm_many(calls)
+            ow, ob = gslot(wconv), gslot(bconv)
+            grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=ow, db=ob)
+            K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
+            K.scale_mul(dg, mul=lpre, out=dl)  # lpre holds GELU'(l pre-activation)
+            made = tuple(t for t in (dg, dapre, dkv, dpooled, dxn) + tuple(tmp) if t is not None)
+            return dxn, (dpooled[:, C:] if dpooled is not None else None), made
+
+        # The RGB part runs on the side stream and the depth branch on the step's stream: the side stream's
+        # kernels get the smaller share of the CUs, and with the depth branch there the join waited ~2 ms per
+        # step for it (profiles/r06_queue_analysis.txt); swapped: 495.7 / 495.1 vs 491.3 / 492.6 images/s
+        if side is not None:
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                dxen, side_tmp = depth_branch()
-            for t in (dxep, e2, e1, xen) + ((dxe1,) if drop_depth and dxe1 is not None else ()):
-                t.record_stream(side)
+                dxn, dpooled_e, made = rgb_part()
+            dxen, _ = depth_branch()
+            main.wait_stream(side)
+            for t in made:  # side allocations read here or by the block's queued weight gradients
+                t.record_stream(main)
         else:
             dxen, _ = depth_branch()
-        dg = torch.empty(P, C, device=dev, dtype=dt)
-        dxn = None
-        dpooled_e = None
-
-        def pooled_branch():  # softmax(q_pool k^T) v over the pooled queries, DFormer.py:119-131
-            kv, pooled, m, o, lse = saved_attn
-            dh = C // heads // 2
-            do = K.bilinear_bwd(dfa, (7, 7), (H, W), B)
-            dm = torch.empty_like(m)
-            dkv = torch.empty(P, C, device=dev, dtype=dt)
-            K.pooled_attn_bwd(m, kv[:, :Ch], kv[:, Ch:], o, do, lse, B, heads, P // B, dh, dh ** -0.5, dm,
-                              dkv[:, :Ch], dkv[:, Ch:])
-            ow, ob = gslot2(wsc), gslot(bsc)
-            grads["wsc"], grads["bsc"] = K.linear_wgrad(dm, pooled, out=ow, bias_grad=True, bias_out=ob)
-            dpooled = K.linear_dgrad(dm, wcast(dt, wsc))
-            dxn = K.pool7_bwd(dpooled[:, :C], shape)
-            ow, ob = gslot2(wkv), gslot(bkv)
-            grads["wkv"], grads["bkv"] = K.linear_wgrad(dkv, g, out=ow, bias_grad=True, bias_out=ob)
-            return dxn, dpooled, dkv
-
-        if window:
-            dxn, dpooled, dkv = pooled_branch()
-            dpooled_e = dpooled[:, C:]
-        # q * a (dq, da came out of the projection's input-gradient epilogue)
-        ow, ob = gslot2(wa), gslot(ba)
-        grads["wa"], grads["ba"] = K.linear_wgrad(da, apre, out=ow, bias_grad=True, bias_out=ob)
-        dapre = torch.empty(P, C, device=dev, dtype=dt)
-        # the a and kv input gradients as one grouped launch
-        calls = [lambda c: K.linear_dgrad(da, wcast(dt, wa), out=dapre, collect=c)]
-        if window:
-            calls.append(lambda c: K.linear_dgrad(dkv, wcast(dt, wkv), out=dg, collect=c))
-        K.gemm_many(calls)
-        ow, ob = gslot(wconv), gslot(bconv)
-        grads["wconv"], grads["bconv"] = K.dwconv_bwd_weight(g, dapre, shape, 7, dw=ow, db=ob)
-        K.dwconv_bwd_data(dapre, shape, wconv, 7, dx=dg, accumulate=bool(window))
-        K.scale_mul(dg, mul=lpre, out=dl)  # lpre holds GELU'(l pre-activation)
-        if side is not None:  # join the depth branch (dcx columns of dqcl, dxen)
-            main.wait_stream(side)
-            for t in (dxen,) + side_tmp:
-                t.record_stream(main)
+            dxn, dpooled_e, _ = rgb_part()
         if dpooled_e is not None:
             K.pool7_bwd(dpooled_e, shape, dx=dxen, accumulate=True)
         # q | q_cut | l
