@@ -137,8 +137,28 @@ def gslot_rows(*ps):
     return ss[0][0][ss[0][1]:off].view(rows, *cols) if cols else ss[0][0][ss[0][1]:off]
 
 
-def wgrad_group():
-    """The weight-gradient queue of one Block backward (kernels.wgrad_group)."""
+# The grouped weight gradients (and deferred reduction second stages) of every Block backward -- the
+# attention's and both ConvFFNs' -- are issued on a stream of their own, after that stream waits for
+# the block's data gradients: nothing downstream reads them before the optimizer (join_streams), so the
+# next block's backward no longer waits for them. Measured (alternating runs): 492.2-495.9 vs
+# 499.1-501.9 images/s; the ConvFFNs' groups alone (490.6 / 492.2) or the attention's alone (486.5 /
+# 488.1) were slower.
+_WG_STREAM = {}
+
+
+def _wg_stream(dev):
+    st = _WG_STREAM.get(dev)
+    if st is None:
+        st = _WG_STREAM[dev] = torch.cuda.Stream(device=dev)
+        register_side_stream(st)
+    return st
+
+
+def wgrad_group(dev=None):
+    """The weight-gradient queue of one Block backward (kernels.wgrad_group), flushed on the
+    weight-gradient stream for CUDA tensors."""
+    if dev is not None and dev.type == "cuda":
+        return K.wgrad_group(stream=_wg_stream(dev))
     return K.wgrad_group()
 
 
@@ -257,7 +277,7 @@ class ConvFFNFn(torch.autograd.Function):
                 rowscale, grads=slots)
             return (dx, None, None, dlnw, dlnb, dW1.view_as(w1), db1, dwpos.view_as(wpos), dbpos, dW2.view_as(w2), db2,
                     dls)
-        with wgrad_group():  # the fc2 and fc1 weight gradients as one grouped launch at the end
+        with wgrad_group(dout.device):  # the fc2 and fc1 weight gradients as one grouped launch at the end
             x, xn, mu, rs, h, gp, g, f, rowscale, ln_w, w1, b1, wpos, bpos, w2, b2, ls = ctx.saved_tensors
             B, H, W = ctx.shape
             dt = x.dtype
@@ -375,8 +395,9 @@ class AttentionFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx1, dxe1):
         K.TAG = ctx.tag + ".bwd"
-        with wgrad_group():  # the Block attention's weight gradients as grouped launches at the end
-            return AttentionFn._backward(ctx, dx1, dxe1)
+        g0 = dx1 if dx1 is not None else dxe1
+        with wgrad_group(g0.device if g0 is not None else None):  # the Block attention's weight gradients
+            return AttentionFn._backward(ctx, dx1, dxe1)                 # as grouped launches at the end
 
     @staticmethod
     def _backward(ctx, dx1, dxe1):

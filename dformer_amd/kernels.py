@@ -113,7 +113,11 @@ _RED_PENDING = None
 
 class wgrad_group:
     """Queue the weight-gradient GEMMs and reduction second stages issued inside; at exit issue
-    them (flush_wgrad, flush_reductions) on the current stream."""
+    them (flush_wgrad, flush_reductions) on the current stream, or on `stream` (after it waits for
+    the current one), so that the current stream's later work does not wait for them."""
+
+    def __init__(self, stream=None):
+        self.stream = stream
 
     def __enter__(self):
         global _WG_PENDING, _RED_PENDING
@@ -125,11 +129,22 @@ class wgrad_group:
         global _WG_PENDING, _RED_PENDING
         pending, reds = _WG_PENDING, _RED_PENDING
         _WG_PENDING, _RED_PENDING = self.prev
-        if exc_type is None:
-            if pending:
-                flush_wgrad(pending)
-            if reds:
-                flush_reductions(reds)
+        if exc_type is None and (pending or reds):
+            if self.stream is None:
+                if pending:
+                    flush_wgrad(pending)
+                if reds:
+                    flush_reductions(reds)
+            else:
+                self.stream.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.stream):
+                    for item in pending:  # operands written on the current stream, read on this one
+                        item[2].record_stream(self.stream)
+                        item[3].record_stream(self.stream)
+                    if pending:
+                        flush_wgrad(pending)
+                    if reds:
+                        flush_reductions(reds)
         return False
 
 
