@@ -142,7 +142,7 @@ def gslot_rows(*ps):
 # the block's data gradients: nothing downstream reads them before the optimizer (join_streams), so the
 # next block's backward no longer waits for them. Measured (alternating runs): 492.2-495.9 vs
 # 499.1-501.9 images/s; the ConvFFNs' groups alone (490.6 / 492.2) or the attention's alone (486.5 /
-# 488.1) were slower.
+# 488.1) were slower. Groups under kernels.WG_STREAM_MIN_FLOPS stay on the current stream.
 _WG_STREAM = {}
 
 

@@ -111,6 +111,9 @@ _WG_PENDING = None
 _RED_PENDING = None
 
 
+WG_STREAM_MIN_FLOPS = 4e9
+
+
 class wgrad_group:
     """Queue the weight-gradient GEMMs and reduction second stages issued inside; at exit issue
     them (flush_wgrad, flush_reductions) on the current stream, or on `stream` (after it waits for
@@ -130,7 +133,12 @@ class wgrad_group:
         pending, reds = _WG_PENDING, _RED_PENDING
         _WG_PENDING, _RED_PENDING = self.prev
         if exc_type is None and (pending or reds):
-            if self.stream is None:
+            # a group worth less than WG_STREAM_MIN_FLOPS stays on the current stream: its launches take
+            # about as long as the two cross-stream edges cost. Every group on the stream: DFormer-Tiny bs 8
+            # (~2.5 GFLOP groups) 628.1 / 625.0 vs 639.9 / 639.0 images/s with none; from 8 GFLOP up: Tiny
+            # 642.4 / 639.8 vs 639.5 / 638.7, DFormer-B flat (its ~5 GFLOP depth-branch ConvFFN groups stay);
+            # from 4 GFLOP up: Tiny 651.2 / 649.5 vs 640.4 / 639.2, DFormer-B 496.9 / 504.7 vs 496.4 / 495.0
+            if self.stream is None or sum(it[5] for it in pending) < WG_STREAM_MIN_FLOPS:
                 if pending:
                     flush_wgrad(pending)
                 if reds:
