@@ -26,8 +26,8 @@ DFM_INLINE void src_idx(int dst, int in, int out, int& i0, int& i1, float& l1) {
 }
 
 // z[c] for c < ncls (others -inf); returns the logit of class `lab` through a predicated select
-template <typename T>
-DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float (&z)[MAXC],
+template <typename T, int NC>
+DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x, int H, int W, float (&z)[NC],
                        bool vec) {
   int h0, h1, w0, w1;
   float lh, lw;
@@ -41,7 +41,7 @@ DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x,
   if constexpr (sizeof(T) == 2) {
     if (vec) {  // 16-byte rows of 8 classes: 4 vector loads per 8 classes instead of 32 scalar ones
 #pragma unroll
-      for (int v = 0; v < MAXC / 8; ++v) {
+      for (int v = 0; v < NC / 8; ++v) {
         if (v * 8 < ncls) {
           float f00[8], f01[8], f10[8], f11[8];
           ld8<T>(p00 + v * 8, f00);
@@ -59,11 +59,11 @@ DFM_INLINE void interp(const T* lg, int b, int h, int w, int ncls, int y, int x,
     }
   }
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c)
+  for (int c = 0; c < NC; ++c)
     z[c] = c < ncls ? a00 * ldf(p00 + c) + a01 * ldf(p01 + c) + a10 * ldf(p10 + c) + a11 * ldf(p11 + c) : -INFINITY;
 }
 
-template <typename T>
+template <typename T, int NC>
 __global__ __launch_bounds__(256) void seg_loss_fwd_kernel(int B, int h, int w, int ncls, const T* __restrict__ lg,
                                                            int H, int W, const long* __restrict__ label, int ignore,
                                                            float* __restrict__ lse_out, float* __restrict__ part) {
@@ -73,17 +73,17 @@ __global__ __launch_bounds__(256) void seg_loss_fwd_kernel(int B, int h, int w, 
   for (long p = blockIdx.x * (long)blockDim.x + threadIdx.x; p < n; p += (long)gridDim.x * blockDim.x) {
     const int x = p % W, y = (p / W) % H, b = p / ((long)W * H);
     const long lab = label[p];
-    float z[MAXC];
+    float z[NC];
     interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
     float m = -INFINITY, zl = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
+    for (int c = 0; c < NC; ++c) {
       m = fmaxf(m, z[c]);
       zl = (c == lab) ? z[c] : zl;
     }
     float se = 0.f;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) se += c < ncls ? __expf(z[c] - m) : 0.f;
+    for (int c = 0; c < NC; ++c) se += c < ncls ? __expf(z[c] - m) : 0.f;
     const float lse = m + __logf(se);
     if (lse_out) lse_out[p] = lse;
     if (lab != ignore && lab >= 0 && lab < ncls) {
@@ -140,7 +140,7 @@ DFM_INLINE int first_pixel(int j, int in, int out) {
   return max(0, (int)floorf(((float)j + 0.5f) * inv - 0.5f) - 2);
 }
 
-template <typename T>
+template <typename T, int NC>
 __global__ __launch_bounds__(XP_NT) void seg_loss_bwd_xpass_kernel(int B, int h, int w, int ncls,
                                                                     const T* __restrict__ lg, int H, int W,
                                                                     const long* __restrict__ label, int ignore,
@@ -177,20 +177,20 @@ __global__ __launch_bounds__(XP_NT) void seg_loss_bwd_xpass_kernel(int B, int h,
     long lab = -1;
     if (touch) lab = label[((long)b * H + y) * W + x];
     if (lab != ignore && lab >= 0 && lab < ncls) {
-      float z[MAXC];
+      float z[NC];
       interp(lg, b, h, w, ncls, y, x, H, W, z, vec);
       float m = -INFINITY;
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c) m = fmaxf(m, z[c]);
+      for (int c = 0; c < NC; ++c) m = fmaxf(m, z[c]);
       float se = 0.f;
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c) {
+      for (int c = 0; c < NC; ++c) {
         z[c] = c < ncls ? __expf(z[c] - m) : 0.f;
         se += z[c];
       }
       const float rs = inv / se;
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c)
+      for (int c = 0; c < NC; ++c)
         if (c < ncls) row[c] = z[c] * rs - (c == lab ? inv : 0.f);
     } else {
       for (int c = 0; c < ncls; ++c) row[c] = 0.f;
@@ -610,13 +610,13 @@ extern "C" int dfm_seg_loss_fwd(int dtype, int B, int h, int w, int ncls, const 
   const long n = (long)B * H * W;
   const int nblk = (int)min((long)LOSS_BLOCKS, (n + 255) / 256);
   if (dtype == DFM_BF16)
-    DFM_LAUNCH(seg_loss_fwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H, W,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_fwd_kernel<bf16_t, 40> : seg_loss_fwd_kernel<bf16_t, MAXC>), dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const bf16_t*)logits, H, W,
                label, ignore, lse, (float*)workspace);
   else if (dtype == DFM_F16)
-    DFM_LAUNCH(seg_loss_fwd_kernel<f16_t>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const f16_t*)logits, H, W,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_fwd_kernel<f16_t, 40> : seg_loss_fwd_kernel<f16_t, MAXC>), dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const f16_t*)logits, H, W,
                label, ignore, lse, (float*)workspace);
   else
-    DFM_LAUNCH(seg_loss_fwd_kernel<float>, dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H, W,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_fwd_kernel<float, 40> : seg_loss_fwd_kernel<float, MAXC>), dim3(nblk), dim3(256), 0, s, B, h, w, ncls, (const float*)logits, H, W,
                label, ignore, lse, (float*)workspace);
   DFM_LAUNCH_CHECK();
   DFM_LAUNCH(seg_loss_sum_kernel, dim3(1), dim3(64), 0, s, nblk, (const float*)workspace, loss_out);
@@ -707,22 +707,28 @@ extern "C" int dfm_seg_loss_bwd(int dtype, int B, int h, int w, int ncls, const 
   const unsigned nblk = (unsigned)((long)B * ((H + RY - 1) / RY) * ((w + PJ - 1) / PJ));
   const size_t lds = (size_t)XP_NT * (ncls + 1) * sizeof(float);
   if (lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<bf16_t>,
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<bf16_t, 40>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<f16_t>,
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<bf16_t, MAXC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<float>,
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<f16_t, 40>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<f16_t, MAXC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<float, 40>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)seg_loss_bwd_xpass_kernel<float, MAXC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipGetLastError();  // a refused attribute must not read as this launch's error
   }
   if (dtype == DFM_BF16)
-    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<bf16_t>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_bwd_xpass_kernel<bf16_t, 40> : seg_loss_bwd_xpass_kernel<bf16_t, MAXC>), dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
                (const bf16_t*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
   else if (dtype == DFM_F16)
-    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<f16_t>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_bwd_xpass_kernel<f16_t, 40> : seg_loss_bwd_xpass_kernel<f16_t, MAXC>), dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
                (const f16_t*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
   else
-    DFM_LAUNCH(seg_loss_bwd_xpass_kernel<float>, dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
+    DFM_LAUNCH((ncls <= 40 ? seg_loss_bwd_xpass_kernel<float, 40> : seg_loss_bwd_xpass_kernel<float, MAXC>), dim3(nblk), dim3(XP_NT), lds, s, B, h, w, ncls,
                (const float*)logits, H, W, label, ignore, loss_out, gscale, rx, RY, PJ);
   DFM_LAUNCH_CHECK();
   DFM_LAUNCH(seg_loss_bwd_ypass_kernel, dim3((unsigned)std::min(8192L, (nl + 255) / 256)), dim3(256), 0, s, B, h,

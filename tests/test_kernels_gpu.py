@@ -596,9 +596,9 @@ def test_column_reductions_block_tails(dt, rows):
     operands, bounded by the fp32 summation error relative to sum|terms| (conditioning-free)."""
     k = K()
     g = torch.Generator(device=DEV).manual_seed(rows)
-    for C in (16, 48, 72, 512):
+    for C in (16, 20, 48, 72, 512):
         base = (torch.randn(rows, C + 8, device=DEV, generator=g) * 3 + 1).to(dt)
-        x = base[:, 8:]  # a strided view; C = 48 / 72 take the scalar kernel, 16 / 512 the vector one
+        x = base[:, 8:]  # a strided view; C = 20 takes the scalar kernel (16-bit), the others the vector one
         y = torch.randn(rows, C, device=DEV, generator=g).to(dt)
         rps = max(1, rows // 3)
         rs = torch.rand((rows + rps - 1) // rps, device=DEV, generator=g)
