@@ -645,7 +645,8 @@ def test_nmf_update_softmax():
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,h,w,H,W,ncls", [(2, 60, 80, 480, 640, 40), (1, 17, 23, 67, 92, 37), (2, 8, 12, 64, 96, 40), (1, 30, 40, 37, 50, 19), (1, 13, 11, 100, 90, 16),
                                                 (1, 24, 20, 96, 80, 40), (2, 10, 14, 20, 28, 64), (1, 7, 9, 56, 72, 3),
-                                                (1, 133, 183, 530, 730, 40), (1, 5, 4, 300, 290, 8)])
+                                                (1, 133, 183, 530, 730, 40), (1, 5, 4, 300, 290, 8),
+                                                (2, 133, 183, 530, 730, 37)])
 def test_seg_loss(dt, B, h, w, H, W, ncls):
     k = K()
     lg = torch.randn(B, h, w, ncls, device=DEV).to(dt)
