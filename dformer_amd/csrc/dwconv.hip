@@ -1457,11 +1457,12 @@ int dw_fwd(int B, int H, int W, int C, int k, const void* x, long ldx, const flo
   DFM_CHECK_ARG(dw_aligned<T>(C, x, ldx) && dw_aligned<T>(C, y, ldy) && (!gout || dw_aligned<T>(C, gout, ldg)),
                 "dwconv: C, row strides and pointers must be 16-byte vector aligned");
   DFM_CHECK_ARG(k == 3 || k == 7, "dwconv: k=%d unsupported", k);
-  // streaming 3x3 wins up to 60x80 planes with its round-aware chunking (60x80 / 30x40: 4-17 %
-  // faster on DFormer-B, 15x20 x 2048: 21 vs 24 us); the LDS-tiled kernel stays ahead on the 120x160
-  // planes (302 vs 328 us at 512 channels, profiles/r04_dw3_geom_sweep.txt)
+  // streaming 3x3 up to 65,536-pixel planes: with its buffer-addressed loads (round 6) it also wins on
+  // DFormer-Large's 133x183 stage-0 planes (config 5: 274.1 / 275.7 -> 276.6 / 279.5 images/s; DFormer-B
+  // and -Tiny, whose stage-0 ConvFFN forward is the fused kernel, within noise). Round 4 had the LDS-tiled
+  // kernel ahead on 120x160 (302 vs 328 us at 512 channels, profiles/r04_dw3_geom_sweep.txt).
   const long plane = (long)H * W;
-  if (k == 3 && plane <= 6144) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
+  if (k == 3 && plane <= 65536) return f3_launch<T, FLIP>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s);
   const int G = C / DwCfg<T>::CPT;
   // channel groups per block: as many as the tile geometry allows without idling lanes
 #define GO(KK, NGV) return dw_tile_launch<T, KK, FLIP, NGV>(B, H, W, C, x, ldx, w, bias, id, y, ldy, acc, gout, ldg, s)
