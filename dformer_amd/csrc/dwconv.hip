@@ -1261,7 +1261,10 @@ __global__ __launch_bounds__(256, 3) void dw3_rows_bwd_kernel(int B, int H, int 
   __shared__ float red[4][NV][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int c0 = (blockIdx.y * 64 + lane) * 2;  // every lane owns a channel pair (host: C % 128 == 0)
+  // every lane owns a channel pair; lanes past C (a partial last slice) read the last pair and store nothing
+  const int cq = (blockIdx.y * 64 + lane) * 2;
+  const bool cvalid = cq < C;
+  const int c0 = cvalid ? cq : C - 2;
   const long units = w3_units(B, nstrips, nchunks);
 
   f2v wf[9];  // flipped taps (input gradient), centre tap + 1 when add_identity
@@ -1363,7 +1366,7 @@ __global__ __launch_bounds__(256, 3) void dw3_rows_bwd_kernel(int B, int H, int 
           for (int t = 0; t < TW; ++t) acc[a * 3 + j] = __builtin_elementwise_fma(Cc[cr][t], xv[t + j], acc[a * 3 + j]);
       }
       // input-gradient row r - 1 is complete
-      if (r - 1 >= h0 && r - 1 < h1) {
+      if (r - 1 >= h0 && r - 1 < h1 && cvalid) {
         char* dp = reinterpret_cast<char*>(dx + ((b * H + r - 1) * W + w0) * lddx);
 #pragma unroll
         for (int t = 0; t < TW; ++t) {
@@ -1393,7 +1396,7 @@ __global__ __launch_bounds__(256, 3) void dw3_rows_bwd_kernel(int B, int H, int 
   for (int idx = threadIdx.x; idx < NV * 64; idx += 256) {
     const int v = idx / 64, l = idx % 64;
     const int c = (blockIdx.y * 64 + l) * 2 + (v & 1);
-    part[pbase + (long)c * 10 + (v >> 1)] = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
+    if (c < C) part[pbase + (long)c * 10 + (v >> 1)] = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
   }
 }
 
@@ -1401,9 +1404,10 @@ __global__ __launch_bounds__(256, 3) void dw3_rows_bwd_kernel(int B, int H, int 
 // it spills and is 10-22 % slower (s0 286 vs 234 us; step 470.2 vs 480.8 images/s)
 constexpr int W3R_WPS = 3;
 
-// the row-scatter kernel: whole 64-lane channel slices (wave-uniform units), 32-bit byte offsets in a row
+// the row-scatter kernel: 64-lane channel slices (wave-uniform units; a partial last slice only from 384
+// channels, where it idles at most a sixth of the lanes: DFormer-Large's 576), 32-bit byte offsets in a row
 inline bool w3r_ok(int W, int C, long ldx, long lddy, long lddx, long es) {
-  return C % 128 == 0 && (long)W * std::max({ldx, lddy, lddx}) * es < (1L << 31);
+  return (C % 128 == 0 || (C % 2 == 0 && C >= 384)) && (long)W * std::max({ldx, lddy, lddx}) * es < (1L << 31);
 }
 
 template <typename T>
