@@ -167,7 +167,7 @@ _SIDE_STREAMS = []
 
 def register_side_stream(s):
     """Streams besides the step's own on which this package issues gradient-writing kernels (the
-    encoder's depth-branch ConvFFN stream, the attention / weight-gradient streams)."""
+    encoder's RGB ConvFFN stream, the attention-backward and weight-gradient streams)."""
     if all(s is not t for t in _SIDE_STREAMS):
         _SIDE_STREAMS.append(s)
 

@@ -205,9 +205,10 @@ class GradBuckets:
             # first step: every bucket is reduced in finish(), after the cross-rank unused-set check
             # (a collective issued here on one rank would pair with that check on another)
             if collectives_on(self.world) and self.checked:
-                # the bucket mixes slots written on the main stream, the depth-branch ConvFFN stream
-                # and the weight-gradient stream, and this hook runs on whichever stream autograd
-                # replays the last AccumulateGrad on: wait for all of them before RCCL reads it
+                # the bucket mixes slots written on the main stream, the side streams (RGB ConvFFN,
+                # attention backward) and the weight-gradient stream, and this hook runs on whichever
+                # stream autograd replays the last AccumulateGrad on: wait for all of them before RCCL
+                # reads it
                 join_streams(self.main_stream)
                 self.handles.append(dist.all_reduce(self.buckets[bi][0], async_op=True))
 
